@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""bench.py — headline measurement of the Smith-Waterman database scan.
+
+Workload (BASELINE.json configs[1]): the 375-residue
+query P07327 (data/queries/P07327.fasta of the reference, shipped as a fixture)
+against a Swiss-Prot-sized synthetic database (570,000 subjects, log-normal
+lengths median 290 / mean ~360, Swiss-Prot residue frequencies; Swiss-Prot
+itself is not available here), BLOSUM50 of SWSolver.cu:54-81, linear gap 2.
+
+One step = one pass of the hot path over the rank's resident shard: build the
+query profile, run the intra-sequence kernel (subjects longer than the long
+threshold) and the inter-sequence kernel, then the top-K exchange (local
+top-K, RCCL all-gather of K (score, id) keys per rank, global merge).
+
+Multi-GPU (torchrun, one process per GPU): every rank holds its OWN shard of
+the same size (weak scaling; shard = the rank's seed), so the global database
+grows with N (config C4's pattern).  value = all cells processed by all ranks
+/ the max-over-ranks time of K steps.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "GCUPS (DP cell updates/s) query-vs-SwissProt, 1/2/4/8 MI355X; bit-exact scores"
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-ops/s
+INTER_OPS_PER_CELL = 3.5        # v_add_sdwa + v_max3 + v_sub clamp + 1/2 v_max3 (running max)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def read_query(name):
+    with open(os.path.join(REPO, "tests", "golden", "queries", name + ".fasta")) as f:
+        return "".join(f.read().split("\n")[1:])
+
+
+def cpu_baseline(sw, q, res, offs, gpu_scores, seconds, threads):
+    """The oracle (C restatement of cpu.cpp's recurrence, kind "port") on a
+    bounded random sample of the same shard, on this host's cores."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import sw_oracle
+    n = len(offs) - 1
+    rng = np.random.default_rng(1782)
+    perm = rng.permutation(n)
+
+    def sample(m):
+        idx = np.sort(perm[:m])
+        lens = offs[idx + 1] - offs[idx]
+        so = np.zeros(m + 1, dtype=np.int64)
+        so[1:] = np.cumsum(lens)
+        sr = np.concatenate([res[offs[i]:offs[i + 1]] for i in idx]) if m else np.zeros(0, np.uint8)
+        return idx, sr, so
+
+    # calibrate on a small sample, then size the real one to ~`seconds`
+    idx, sr, so = sample(min(n, 2000))
+    t = time.perf_counter()
+    sw_oracle.scan(q, sr, so, nthreads=threads)
+    dt = max(time.perf_counter() - t, 1e-3)
+    m = int(min(n, max(2000, 2000 * seconds / dt)))
+    idx, sr, so = sample(m)
+    t = time.perf_counter()
+    cpu = sw_oracle.scan(q, sr, so, nthreads=threads)
+    dt = time.perf_counter() - t
+    cells = len(q) * int(so[-1])
+    parity = bool(np.array_equal(cpu, gpu_scores[idx]))
+    return {"value": round(cells / dt / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": "port",
+            "sample": "%d of %d subjects (%d residues, %.3g cells) of rank 0's shard, same query, "
+                      "%.1f s on %d threads; scores equal to the GPU's: %s"
+                      % (m, n, int(so[-1]), cells, dt, threads, parity)}, parity
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--db-seqs", type=int, default=570000, help="subjects per rank")
+    ap.add_argument("--query", default="P07327")
+    ap.add_argument("--topk", type=int, default=100)
+    ap.add_argument("--long-threshold", type=int, default=0, help="0 = library default")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r01_pmc_traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    import _swpkg
+    sw = _swpkg.load()
+
+    t0 = time.perf_counter()
+    res, offs = sw.synth.database(args.db_seqs, shard=rank)
+    n = len(offs) - 1
+    residues = int(offs[-1])
+    q = sw.encode(read_query(args.query))
+    log("rank %d: shard %d subjects, %d residues, generated in %.1fs" % (rank, n, residues, time.perf_counter() - t0))
+
+    handle = sw.Handle(local)
+    # The library launches on a torch stream (not the legacy null stream,
+    # whose handle is 0 = "library-owned stream" for sw_set_stream), so the
+    # scan is stream-ordered with the top-K ops that read its scores.
+    stream = torch.cuda.Stream(dev)
+    handle.set_stream(stream.cuda_stream)
+    torch.cuda.set_stream(stream)
+    t0 = time.perf_counter()
+    db = sw.Database(handle, res, offs, long_threshold=(args.long_threshold or None))
+    st = db.stats()
+    log("rank %d: packed + uploaded in %.1fs: %s" % (rank, time.perf_counter() - t0, st))
+
+    scores = torch.zeros(n, dtype=torch.int32, device=dev)
+    gid = torch.arange(n, dtype=torch.int64, device=dev) + rank * n
+    K = min(args.topk, n)
+    gathered = torch.empty(world * K, dtype=torch.int64, device=dev)
+
+    def step():
+        db.scan_device(q, scores.data_ptr())
+        # key orders (score desc, global id asc); ids < 2^31
+        key = (scores.to(torch.int64) << 32) | ((1 << 31) - 1 - gid)
+        top = torch.topk(key, K, sorted=False).values
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, top)
+            return torch.topk(gathered, K).values
+        return torch.topk(top, K).values
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    handle.timing_reset()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        final = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    kt = handle.timing_total()
+
+    cells_rank = float(len(q)) * residues
+    if world > 1:
+        t = torch.tensor([elapsed, cells_rank], dtype=torch.float64, device=dev)
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed_max, cells_all = float(tmax[0]), float(t[1])
+    else:
+        elapsed_max, cells_all = elapsed, cells_rank
+
+    # check one step's scores against themselves across the run (determinism)
+    top_ids = ((1 << 31) - 1 - (final & 0xFFFFFFFF)).cpu().numpy()
+    top_scores = (final >> 32).cpu().numpy()
+
+    if rank == 0:
+        value = cells_all * args.steps / elapsed_max / 1e9
+        ms_step = elapsed_max * 1e3 / args.steps
+        nsc = max(kt["scans"], 1)
+        inter_ms = kt["inter_ms"] / nsc
+        intra_ms = kt["intra_ms"] / nsc
+        # dominant kernel: inter-sequence.  Algorithmic bytes per launch
+        # (SURVEY.md §8d): 1 B per residue it scans + 12 B per subject
+        # (offset, length, int32 score).
+        n_inter = n - st["n_long"]
+        inter_res = residues - int(sum(
+            np.sort(offs[1:] - offs[:-1])[::-1][:st["n_long"]])) if st["n_long"] else residues
+        alg_bytes = inter_res + 12 * n_inter
+        achieved = alg_bytes / (inter_ms * 1e-3) / 1e9 if inter_ms > 0 else 0.0
+        inter_cells = float(len(q)) * inter_res
+        inter_gcups = inter_cells / (inter_ms * 1e-3) / 1e9 if inter_ms > 0 else 0.0
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("workload_key") == "%s/%d/%d" % (args.query, args.db_seqs, len(q)):
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GCUPS",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic",
+            "config": {
+                "workload": "C2: query %s (%d aa) vs synthetic Swiss-Prot-sized db, %d subjects/rank "
+                            "(%d residues/rank), BLOSUM50 (SWSolver.cu:54-81), linear gap 2, top-%d "
+                            "all-gathered" % (args.query, len(q), n, residues, K),
+                "query": args.query, "query_len": int(len(q)), "subjects_per_rank": n,
+                "residues_per_rank": residues, "parallelism": "db-shard x%d + RCCL allgather top-K" % world,
+                "long_threshold": st["long_threshold"], "long_subjects": st["n_long"],
+                "cells_per_step": cells_all,
+            },
+            "kernel_ms": {"inter": round(inter_ms, 4), "intra": round(intra_ms, 4),
+                          "scan_total": round(kt["total_ms"] / nsc, 4)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                         "traffic": traffic,
+                         "kernel": "sw_inter (inter-sequence, linear gap)",
+                         "alg_bytes_per_launch": alg_bytes},
+            "valu_roofline": {"bound": "valu-int32", "achieved": round(inter_gcups * INTER_OPS_PER_CELL / 1e3, 3),
+                              "peak": round(VALU_PEAK_TOPS, 2), "unit": "T lane-ops/s",
+                              "frac": round(inter_gcups * INTER_OPS_PER_CELL / 1e3 / VALU_PEAK_TOPS, 4),
+                              "inter_gcups": round(inter_gcups, 1), "ops_per_cell": INTER_OPS_PER_CELL},
+            "top_hit": {"id": int(top_ids[np.argmax(top_scores)]), "score": int(top_scores.max())},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            gs = scores.cpu().numpy()
+            threads = min(args.cpu_threads, os.cpu_count() or 1)
+            cb, parity = cpu_baseline(sw, q, res, offs, gs, args.cpu_seconds, threads)
+            out["cpu_baseline"] = cb
+            out["parity_sample_ok"] = parity
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    db.close()
+    handle.close()
+
+
+if __name__ == "__main__":
+    main()

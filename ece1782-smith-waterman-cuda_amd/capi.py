@@ -1,0 +1,288 @@
+"""ctypes binding of the C ABI in include/sw_amd.h (lib/libswamd.so).
+
+This is the product path's Python face: it loads ONLY the in-tree HIP
+library and raises if it is missing — there is no CPU fallback.
+"""
+import ctypes
+import os
+import weakref
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libswamd.so")
+
+SW_OK = 0
+SW_ALPHABET = 25
+MATRIX_BLOSUM50_REF = 0
+MATRIX_BLOSUM62 = 1
+MATRIX_IDENTITY3 = 2
+
+# Every symbol include/sw_amd.h declares (checked by tests/test_abi.py).
+EXPORTED = (
+    "sw_version", "sw_last_error", "sw_encode", "sw_builtin_matrix",
+    "sw_create", "sw_destroy", "sw_stream", "sw_set_stream",
+    "sw_db_create", "sw_db_free", "sw_db_get_stats", "sw_db_set_long_threshold",
+    "sw_scan", "sw_scan_device", "sw_scan_batch", "sw_get_timing",
+    "sw_timing_reset", "sw_timing_total",
+    "sw_topk", "sw_score_pair",
+)
+
+
+class SWError(RuntimeError):
+    pass
+
+
+class Scoring(ctypes.Structure):
+    _fields_ = [("matrix", ctypes.POINTER(ctypes.c_int8)),
+                ("gap_open", ctypes.c_int32),
+                ("gap_extend", ctypes.c_int32)]
+
+
+class DbStats(ctypes.Structure):
+    _fields_ = [("n_subjects", ctypes.c_int64), ("residues", ctypes.c_int64),
+                ("packed_cells", ctypes.c_int64), ("n_blocks", ctypes.c_int64),
+                ("n_long", ctypes.c_int64), ("device_bytes", ctypes.c_int64),
+                ("max_length", ctypes.c_int32), ("long_threshold", ctypes.c_int32)]
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [("inter_ms", ctypes.c_float), ("intra_ms", ctypes.c_float),
+                ("total_ms", ctypes.c_float), ("rescued", ctypes.c_int32),
+                ("launches", ctypes.c_int32)]
+
+
+_LIB = None
+
+
+def lib():
+    """Load lib/libswamd.so (built by build()); raise if absent."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise SWError("HIP library %s not built; run __graft_entry__.build() "
+                      "or make -C ece1782-smith-waterman-cuda_amd/csrc" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    i64p = ctypes.POINTER(ctypes.c_int64)
+    sig = {
+        "sw_version": (i32, []),
+        "sw_last_error": (ctypes.c_char_p, []),
+        "sw_encode": (ctypes.c_int, [ctypes.c_char_p, i64, u8p]),
+        "sw_builtin_matrix": (ctypes.c_int, [i32, ctypes.POINTER(ctypes.c_int8)]),
+        "sw_create": (ctypes.c_int, [i32, ctypes.POINTER(vp)]),
+        "sw_destroy": (ctypes.c_int, [vp]),
+        "sw_stream": (vp, [vp]),
+        "sw_set_stream": (ctypes.c_int, [vp, vp]),
+        "sw_db_create": (ctypes.c_int, [vp, u8p, i64p, i64, i32p, ctypes.POINTER(vp)]),
+        "sw_db_free": (ctypes.c_int, [vp]),
+        "sw_db_get_stats": (ctypes.c_int, [vp, ctypes.POINTER(DbStats)]),
+        "sw_db_set_long_threshold": (ctypes.c_int, [vp, i32]),
+        "sw_scan": (ctypes.c_int, [vp, vp, u8p, i32, ctypes.POINTER(Scoring), i32p]),
+        "sw_scan_device": (ctypes.c_int, [vp, vp, u8p, i32, ctypes.POINTER(Scoring), vp]),
+        "sw_scan_batch": (ctypes.c_int, [vp, vp, u8p, i64p, i32, ctypes.POINTER(Scoring), i32p]),
+        "sw_get_timing": (ctypes.c_int, [vp, ctypes.POINTER(Timing)]),
+        "sw_timing_reset": (ctypes.c_int, [vp]),
+        "sw_timing_total": (ctypes.c_int, [vp, ctypes.POINTER(Timing), i32p]),
+        "sw_topk": (ctypes.c_int, [i32p, i64, i32, i32p, i32p]),
+        "sw_score_pair": (ctypes.c_int, [vp, u8p, i32, u8p, i32, ctypes.POINTER(Scoring), i32p]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = L
+    return L
+
+
+def _check(rc):
+    if rc != SW_OK:
+        raise SWError("sw_amd error %d: %s" % (rc, lib().sw_last_error().decode(errors="replace")))
+
+
+def _u8(a):
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+def encode(seq):
+    """ASCII -> residue codes (SWSolver.cu:91-120 mapping)."""
+    b = seq.encode() if isinstance(seq, str) else bytes(seq)
+    out = np.empty(len(b), dtype=np.uint8)
+    _check(lib().sw_encode(b, len(b), out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+    return out
+
+
+def builtin_matrix(mid=MATRIX_BLOSUM50_REF):
+    out = np.empty(625, dtype=np.int8)
+    _check(lib().sw_builtin_matrix(mid, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int8))))
+    return out.reshape(25, 25)
+
+
+class _ScoringArg:
+    """Keeps the matrix buffer alive for the duration of a call."""
+
+    def __init__(self, matrix=None, gap_open=2, gap_extend=None):
+        gap_extend = gap_open if gap_extend is None else gap_extend
+        if matrix is None:
+            self._m = None
+            self.s = Scoring(None, gap_open, gap_extend)
+        else:
+            self._m = np.ascontiguousarray(np.asarray(matrix, dtype=np.int8).reshape(625))
+            self.s = Scoring(self._m.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)), gap_open, gap_extend)
+
+    def ptr(self):
+        return ctypes.byref(self.s)
+
+
+class Handle:
+    """One device + one HIP stream (sw_create)."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        _check(lib().sw_create(device, ctypes.byref(h)))
+        self._h = h
+        self.device = device
+        self._dbs = weakref.WeakSet()  # databases must be freed before the handle
+
+    @property
+    def ptr(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            for db in list(self._dbs):
+                db.close()
+            lib().sw_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stream(self):
+        return lib().sw_stream(self._h)
+
+    def set_stream(self, hip_stream):
+        _check(lib().sw_set_stream(self._h, hip_stream))
+
+    def timing(self):
+        t = Timing()
+        _check(lib().sw_get_timing(self._h, ctypes.byref(t)))
+        return {"inter_ms": t.inter_ms, "intra_ms": t.intra_ms, "total_ms": t.total_ms,
+                "rescued": t.rescued, "launches": t.launches}
+
+    def timing_reset(self):
+        _check(lib().sw_timing_reset(self._h))
+
+    def timing_total(self):
+        """Kernel ms summed over all scans since timing_reset(); waits."""
+        t = Timing()
+        n = ctypes.c_int32()
+        _check(lib().sw_timing_total(self._h, ctypes.byref(t), ctypes.byref(n)))
+        return {"inter_ms": t.inter_ms, "intra_ms": t.intra_ms, "total_ms": t.total_ms,
+                "launches": t.launches, "scans": n.value}
+
+    def score_pair(self, query_codes, subject_codes, matrix=None, gap_open=2, gap_extend=None):
+        q, qp = _u8(query_codes)
+        s, sp = _u8(subject_codes)
+        sc = _ScoringArg(matrix, gap_open, gap_extend)
+        out = ctypes.c_int32()
+        _check(lib().sw_score_pair(self._h, qp, len(q), sp, len(s), sc.ptr(), ctypes.byref(out)))
+        return out.value
+
+
+class Database:
+    """A device-resident packed database (sw_db_create)."""
+
+    def __init__(self, handle, residues, offsets, ids=None, long_threshold=None):
+        self.handle = handle
+        r, rp = _u8(residues)
+        o = np.ascontiguousarray(offsets, dtype=np.int64)
+        n = len(o) - 1
+        idp = None
+        if ids is not None:
+            self._ids = np.ascontiguousarray(ids, dtype=np.int32)
+            idp = self._ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+            self.n_out = int(self._ids.max()) + 1 if n > 0 else 0
+        else:
+            self.n_out = n
+        d = ctypes.c_void_p()
+        _check(lib().sw_db_create(handle.ptr, rp, o.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                  n, idp, ctypes.byref(d)))
+        self._d = d
+        self.n = n
+        handle._dbs.add(self)
+        if long_threshold is not None:
+            self.set_long_threshold(long_threshold)
+
+    @property
+    def ptr(self):
+        return self._d
+
+    def close(self):
+        if self._d:
+            if self.handle.ptr:  # a closed handle already freed us
+                lib().sw_db_free(self._d)
+            self._d = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_long_threshold(self, t):
+        _check(lib().sw_db_set_long_threshold(self._d, int(t)))
+
+    def stats(self):
+        s = DbStats()
+        _check(lib().sw_db_get_stats(self._d, ctypes.byref(s)))
+        return {k: getattr(s, k) for k, _ in DbStats._fields_}
+
+    def scan(self, query_codes, matrix=None, gap_open=2, gap_extend=None):
+        """Synchronous scan; returns int32 scores indexed by id."""
+        q, qp = _u8(query_codes)
+        sc = _ScoringArg(matrix, gap_open, gap_extend)
+        out = np.zeros(self.n_out, dtype=np.int32)
+        _check(lib().sw_scan(self.handle.ptr, self._d, qp, len(q), sc.ptr(),
+                             out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return out
+
+    def scan_device(self, query_codes, scores_dev_ptr, matrix=None, gap_open=2, gap_extend=None):
+        """Asynchronous scan on the handle's stream into a device int32 buffer."""
+        q, qp = _u8(query_codes)
+        sc = _ScoringArg(matrix, gap_open, gap_extend)
+        _check(lib().sw_scan_device(self.handle.ptr, self._d, qp, len(q), sc.ptr(),
+                                    ctypes.c_void_p(scores_dev_ptr)))
+
+    def scan_batch(self, queries, matrix=None, gap_open=2, gap_extend=None):
+        """queries: list of code arrays; returns [nq, n_out] int32."""
+        cat = np.concatenate([np.asarray(q, dtype=np.uint8) for q in queries]) if queries else \
+            np.zeros(0, dtype=np.uint8)
+        offs = np.zeros(len(queries) + 1, dtype=np.int64)
+        offs[1:] = np.cumsum([len(q) for q in queries])
+        c, cp = _u8(cat)
+        sc = _ScoringArg(matrix, gap_open, gap_extend)
+        out = np.zeros((len(queries), self.n_out), dtype=np.int32)
+        _check(lib().sw_scan_batch(self.handle.ptr, self._d, cp,
+                                   offs.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), len(queries),
+                                   sc.ptr(), out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return out
+
+
+def topk(scores, k):
+    """(ids, scores) of the k best: score descending, id ascending."""
+    s = np.ascontiguousarray(scores, dtype=np.int32)
+    ids = np.empty(k, dtype=np.int32)
+    vals = np.empty(k, dtype=np.int32)
+    _check(lib().sw_topk(s.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(s), k,
+                         ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                         vals.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+    return ids, vals

@@ -1,0 +1,741 @@
+// sw_capi.cpp — host driver behind the C ABI (include/sw_amd.h).
+//
+// What the reference does per query (SWSolver.cu:266-404) and what replaces it:
+//   * pad/encode the query and upload it to __constant__ (:267-299)
+//       -> a 32 x qpad int8 query PROFILE (score of every residue code against
+//          every query row, pre-biased by the gap for the linear kernels),
+//          built on the host and copied once per query (tiny: 32 B/row);
+//   * re-pack the whole database into managed memory on every query,
+//     longest-first, 32 lanes per block (:301-371)
+//       -> sw_db_create packs ONCE into 64-lane blocks of 16-residue groups,
+//          sorted longest-first, and keeps the result resident in HBM;
+//   * launch in chunks with cudaDeviceSynchronize after each (:332-354,379)
+//       -> one asynchronous launch per kernel on the handle's stream;
+//   * read managed scores back in packing order (:383-390)
+//       -> kernels write scores[id] directly.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/sw_amd.h"
+#include "sw_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHECK(expr)                                                                  \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(SW_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+    } while (0)
+
+// ---- built-in matrices (code order ARNDCQEGHILKMFPSTWYVBJZX*) ------------
+// BLOSUM50 exactly as tabulated in the reference, SWSolver.cu:54-81.
+const int8_t kBlosum50Ref[625] = {
+    5, -2, -1, -2, -1, -1, -1, 0, -2, -1, -2, -1, -1, -3, -1, 1, 0, -3, -2, 0, -2, -2, -1, -1, 0,
+    -2, 7, -1, -2, -4, 1, 0, -3, 0, -4, -3, 3, -2, -3, -3, -1, -1, -3, -1, -3, -1, -3, 0, -1, 0,
+    -1, -1, 7, 2, -2, 0, 0, 0, 1, -3, -4, 0, -2, -4, -2, 1, 0, -4, -2, -3, 5, -4, 0, -1, 0,
+    -2, -2, 2, 8, -4, 0, 2, -1, -1, -4, -4, -1, -4, -5, -1, 0, -1, -5, -3, -4, 6, -4, 1, -1, 0,
+    -1, -4, -2, -4, 13, -3, -3, -3, -3, -2, -2, -3, -2, -2, -4, -1, -1, -5, -3, -1, -3, -2, -3, -1, 0,
+    -1, 1, 0, 0, -3, 7, 2, -2, 1, -3, -2, 2, 0, -4, -1, 0, -1, -1, -1, -3, 0, -3, 4, -1, 0,
+    -1, 0, 0, 2, -3, 2, 6, -3, 0, -4, -3, 1, -2, -3, -1, -1, -1, -3, -2, -3, 1, -3, 5, -1, 0,
+    0, -3, 0, -1, -3, -2, -3, 8, -2, -4, -4, -2, -3, -4, -2, 0, -2, -3, -3, -4, -1, -4, -2, -1, 0,
+    -2, 0, 1, -1, -3, 1, 0, -2, 10, -4, -3, 0, -1, -1, -2, -1, -2, -3, 2, -4, 0, -3, 0, -1, 0,
+    -1, -4, -3, -4, -2, -3, -4, -4, -4, 5, 2, -3, 2, 0, -3, -3, -1, -3, -1, 4, -4, 4, -3, -1, 0,
+    -2, -3, -4, -4, -2, -2, -3, -4, -3, 2, 5, -3, 3, 1, -4, -3, -1, -2, -1, 1, -4, 4, -3, -1, 0,
+    -1, 3, 0, -1, -3, 2, 1, -2, 0, -3, -3, 6, -2, -4, -1, 0, -1, -3, -2, -3, 0, -3, 1, -1, 0,
+    -1, -2, -2, -4, -2, 0, -2, -3, -1, 2, 3, -2, 7, 0, -3, -2, -1, -1, 0, 1, -3, 2, -1, -1, 0,
+    -3, -3, -4, -5, -2, -4, -3, -4, -1, 0, 1, -4, 0, 8, -4, -3, -2, 1, 4, -1, -4, 1, -4, -1, 0,
+    -1, -3, -2, -1, -4, -1, -1, -2, -2, -3, -4, -1, -3, -4, 10, -1, -1, -4, -3, -3, -2, -3, -1, -1, 0,
+    1, -1, 1, 0, -1, 0, -1, 0, -1, -3, -3, 0, -2, -3, -1, 5, 2, -4, -2, -2, 0, -3, 0, -1, 0,
+    0, -1, 0, -1, -1, -1, -1, -2, -2, -1, -1, -1, -1, -2, -1, 2, 5, -3, -2, 0, 0, -1, -1, -1, 0,
+    -3, -3, -4, -5, -5, -1, -3, -3, -3, -3, -2, -3, -1, 1, -4, -4, -3, 15, 2, -3, -5, -2, -2, -1, 0,
+    -2, -1, -2, -3, -3, -1, -2, -3, 2, -1, -1, -2, 0, 4, -3, -2, -2, 2, 8, -1, -3, -1, -2, -1, 0,
+    0, -3, -3, -4, -1, -3, -3, -4, -4, 4, 1, -3, 1, -1, -3, -2, 0, -3, -1, 5, -3, 2, -3, -1, 0,
+    -2, -1, 5, 6, -3, 0, 1, -1, 0, -4, -4, 0, -3, -4, -2, 0, 0, -5, -3, -3, 6, -4, 1, -1, 0,
+    -2, -3, -4, -4, -2, -3, -3, -4, -3, 4, 4, -3, 2, 1, -3, -3, -1, -2, -1, 2, -4, 4, -3, -1, 0,
+    -1, 0, 0, 1, -3, 4, 5, -2, 0, -3, -3, 1, -1, -4, -1, 0, -1, -2, -2, -3, 1, -3, 5, -1, 0,
+    -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, 0,
+    0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+};
+
+// NCBI BLOSUM62 with J; an option of this build (the reference has none).
+const int8_t kBlosum62[625] = {
+    4, -1, -2, -2, 0, -1, -1, 0, -2, -1, -1, -1, -1, -2, -1, 1, 0, -3, -2, 0, -2, -1, -1, 0, -4,
+    -1, 5, 0, -2, -3, 1, 0, -2, 0, -3, -2, 2, -1, -3, -2, -1, -1, -3, -2, -3, -1, -2, 0, -1, -4,
+    -2, 0, 6, 1, -3, 0, 0, 0, 1, -3, -3, 0, -2, -3, -2, 1, 0, -4, -2, -3, 3, -3, 0, -1, -4,
+    -2, -2, 1, 6, -3, 0, 2, -1, -1, -3, -4, -1, -3, -3, -1, 0, -1, -4, -3, -3, 4, -3, 1, -1, -4,
+    0, -3, -3, -3, 9, -3, -4, -3, -3, -1, -1, -3, -1, -2, -3, -1, -1, -2, -2, -1, -3, -1, -3, -2, -4,
+    -1, 1, 0, 0, -3, 5, 2, -2, 0, -3, -2, 1, 0, -3, -1, 0, -1, -2, -1, -2, 0, -2, 3, -1, -4,
+    -1, 0, 0, 2, -4, 2, 5, -2, 0, -3, -3, 1, -2, -3, -1, 0, -1, -3, -2, -2, 1, -3, 4, -1, -4,
+    0, -2, 0, -1, -3, -2, -2, 6, -2, -4, -4, -2, -3, -3, -2, 0, -2, -2, -3, -3, -1, -4, -2, -1, -4,
+    -2, 0, 1, -1, -3, 0, 0, -2, 8, -3, -3, -1, -2, -1, -2, -1, -2, -2, 2, -3, 0, -3, 0, -1, -4,
+    -1, -3, -3, -3, -1, -3, -3, -4, -3, 4, 2, -3, 1, 0, -3, -2, -1, -3, -1, 3, -3, 3, -3, -1, -4,
+    -1, -2, -3, -4, -1, -2, -3, -4, -3, 2, 4, -2, 2, 0, -3, -2, -1, -2, -1, 1, -4, 3, -3, -1, -4,
+    -1, 2, 0, -1, -3, 1, 1, -2, -1, -3, -2, 5, -1, -3, -1, 0, -1, -3, -2, -2, 0, -3, 1, -1, -4,
+    -1, -1, -2, -3, -1, 0, -2, -3, -2, 1, 2, -1, 5, 0, -2, -1, -1, -1, -1, 1, -3, 2, -1, -1, -4,
+    -2, -3, -3, -3, -2, -3, -3, -3, -1, 0, 0, -3, 0, 6, -4, -2, -2, 1, 3, -1, -3, 0, -3, -1, -4,
+    -1, -2, -2, -1, -3, -1, -1, -2, -2, -3, -3, -1, -2, -4, 7, -1, -1, -4, -3, -2, -2, -3, -1, -2, -4,
+    1, -1, 1, 0, -1, 0, 0, 0, -1, -2, -2, 0, -1, -2, -1, 4, 1, -3, -2, -2, 0, -2, 0, 0, -4,
+    0, -1, 0, -1, -1, -1, -1, -2, -2, -1, -1, -1, -1, -2, -1, 1, 5, -2, -2, 0, -1, -1, -1, 0, -4,
+    -3, -3, -4, -4, -2, -2, -3, -2, -2, -3, -2, -3, -1, 1, -4, -3, -2, 11, 2, -3, -4, -2, -3, -2, -4,
+    -2, -2, -2, -3, -2, -1, -2, -3, 2, -1, -1, -2, -1, 3, -3, -2, -2, 2, 7, -1, -3, -1, -2, -1, -4,
+    0, -3, -3, -3, -1, -2, -2, -3, -3, 3, 1, -2, 1, -1, -2, -2, 0, -3, -1, 4, -3, 2, -2, -1, -4,
+    -2, -1, 3, 4, -3, 0, 1, -1, 0, -3, -4, 0, -3, -3, -2, 0, -1, -4, -3, -3, 4, -3, 1, -1, -4,
+    -1, -2, -3, -3, -1, -2, -3, -4, -3, 3, 3, -3, 2, 0, -3, -2, -1, -2, -1, 2, -3, 3, -3, -1, -4,
+    -1, 0, 0, 1, -3, 3, 4, -2, 0, -3, -3, 1, -1, -3, -1, 0, -1, -3, -2, -2, 1, -3, 4, -1, -4,
+    0, -1, -1, -1, -2, -1, -1, -1, -1, -1, -1, -1, -1, -1, -2, 0, 0, -2, -1, -1, -1, -1, -1, -1, -4,
+    -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, -4, 1,
+};
+
+int8_t g_encode_lut[256];
+bool g_lut_ready = false;
+
+void init_lut() {
+    if (g_lut_ready) return;
+    static const char letters[] = "ARNDCQEGHILKMFPSTWYVBJZX";  // SWSolver.cu:17-40
+    for (int c = 0; c < 256; ++c) g_encode_lut[c] = SW_CODE_STAR;  // SWSolver.cu:119
+    for (int k = 0; k < 24; ++k) g_encode_lut[static_cast<unsigned char>(letters[k])] = static_cast<int8_t>(k);
+    g_lut_ready = true;
+}
+
+int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+int default_threads() {
+    unsigned n = std::thread::hardware_concurrency();
+    if (n == 0) n = 4;
+    return static_cast<int>(std::min(16u, n));  // GPU boxes expose many more CPUs than our share
+}
+
+template <class F>
+void parallel_for(int64_t n, F&& f) {
+    const int nt = static_cast<int>(std::min<int64_t>(default_threads(), std::max<int64_t>(1, n / 64)));
+    if (nt <= 1) {
+        for (int64_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::atomic<int64_t> next{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&] {
+            for (;;) {
+                const int64_t i0 = next.fetch_add(64);
+                if (i0 >= n) break;
+                const int64_t i1 = std::min(n, i0 + 64);
+                for (int64_t i = i0; i < i1; ++i) f(i);
+            }
+        });
+    for (auto& t : th) t.join();
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+struct ScanEvents {
+    hipEvent_t ev[4] = {};  // start, after intra, after inter, end
+    int launches = 0;
+};
+
+struct sw_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    // One event set per scan since the last sw_timing_reset (grows as needed,
+    // reused after a reset), so a caller can time many back-to-back scans
+    // without synchronising between them.
+    std::vector<ScanEvents> evpool;
+    size_t nscans = 0;
+    hipEvent_t* ev = nullptr;  // event set of the current scan
+    // per-query workspace
+    int8_t* d_prof = nullptr;
+    size_t prof_cap = 0;
+    int32_t* d_scores = nullptr;  // for the synchronous sw_scan
+    size_t scores_cap = 0;
+    std::vector<int8_t> h_prof;
+    bool timed = false;
+    bool had_intra = false;
+    int launches = 0;
+};
+
+struct sw_db {
+    sw_handle* h = nullptr;
+    int64_t n = 0;
+    int64_t residues = 0;
+    int32_t max_len = 0;
+    int32_t max_id = -1;
+    int32_t long_threshold = 0;
+    // inter part
+    int64_t nblocks = 0;
+    int64_t packed_cells = 0;
+    uint8_t* d_res = nullptr;
+    size_t res_bytes = 0;
+    uint64_t* d_blk_off = nullptr;
+    uint32_t* d_blk_groups = nullptr;
+    int32_t* d_lane_ids = nullptr;
+    int32_t* d_bnd_h = nullptr;
+    int32_t* d_bnd_f = nullptr;
+    // intra part (long subjects)
+    int64_t nlong = 0;
+    uint8_t* d_lres = nullptr;
+    size_t lres_bytes = 0;
+    uint64_t* d_loff = nullptr;
+    int32_t* d_llen = nullptr;
+    int32_t* d_lid = nullptr;
+    int32_t* d_lbnd_h = nullptr;
+    int32_t* d_lbnd_f = nullptr;
+    // host copies kept to allow re-partitioning when the threshold changes
+    std::vector<uint8_t> h_residues;
+    std::vector<int64_t> h_offsets;
+    std::vector<int32_t> h_ids;
+    bool built = false;
+    size_t device_bytes = 0;
+};
+
+namespace {
+
+constexpr int32_t kDefaultLongThreshold = 3072;
+
+void free_dev(sw_db* db) {
+    void* ptrs[] = {db->d_res, db->d_blk_off, db->d_blk_groups, db->d_lane_ids, db->d_bnd_h, db->d_bnd_f,
+                    db->d_lres, db->d_loff, db->d_llen, db->d_lid, db->d_lbnd_h, db->d_lbnd_f};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    db->d_res = nullptr; db->d_blk_off = nullptr; db->d_blk_groups = nullptr; db->d_lane_ids = nullptr;
+    db->d_bnd_h = nullptr; db->d_bnd_f = nullptr; db->d_lres = nullptr; db->d_loff = nullptr;
+    db->d_llen = nullptr; db->d_lid = nullptr; db->d_lbnd_h = nullptr; db->d_lbnd_f = nullptr;
+    db->device_bytes = 0;
+    db->built = false;
+}
+
+template <class T>
+int upload(T** dptr, const std::vector<T>& v, hipStream_t s, size_t* acc) {
+    if (v.empty()) { *dptr = nullptr; return SW_OK; }
+    HIPCHECK(hipMalloc(reinterpret_cast<void**>(dptr), v.size() * sizeof(T)));
+    HIPCHECK(hipMemcpyAsync(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+    *acc += v.size() * sizeof(T);
+    return SW_OK;
+}
+
+// Pack: sort by length (descending, stable), route subjects longer than the
+// threshold to the intra kernel, deal the rest into 64-lane blocks of
+// 16-residue groups.  Lanes past a subject's end hold kPadCode.
+int build_db(sw_db* db) {
+    hipStream_t s = db->h->stream;
+    const int64_t n = db->n;
+    std::vector<int64_t> order(n);
+    std::iota(order.begin(), order.end(), 0);
+    auto len = [&](int64_t k) { return db->h_offsets[k + 1] - db->h_offsets[k]; };
+    std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return len(x) > len(y); });
+    int64_t nlong = 0;
+    while (nlong < n && len(order[nlong]) > db->long_threshold) ++nlong;
+
+    // ---- intra (long) part: plain concatenation, 16-byte aligned starts
+    std::vector<uint64_t> loff(nlong);
+    std::vector<int32_t> llen(nlong), lid(nlong);
+    uint64_t ltotal = 0;
+    for (int64_t k = 0; k < nlong; ++k) {
+        const int64_t src = order[k];
+        loff[k] = ltotal;
+        llen[k] = static_cast<int32_t>(len(src));
+        lid[k] = db->h_ids[src];
+        ltotal += round_up(len(src), 64);
+    }
+    std::vector<uint8_t> lres(ltotal, swk::kPadCode);
+    parallel_for(nlong, [&](int64_t k) {
+        const int64_t src = order[k];
+        std::memcpy(lres.data() + loff[k], db->h_residues.data() + db->h_offsets[src], len(src));
+    });
+
+    // ---- inter part
+    const int64_t nshort = n - nlong;
+    const int64_t nblocks = (nshort + swk::kLanes - 1) / swk::kLanes;
+    std::vector<uint64_t> blk_off(nblocks);
+    std::vector<uint32_t> blk_groups(nblocks);
+    std::vector<int32_t> lane_ids(nblocks * swk::kLanes, -1);
+    uint64_t total = 0;
+    for (int64_t b = 0; b < nblocks; ++b) {
+        const int64_t first = nlong + b * swk::kLanes;  // longest subject of the block
+        const int64_t w = round_up(len(order[first]), swk::kGroupCols);
+        blk_off[b] = total;
+        blk_groups[b] = static_cast<uint32_t>(w / swk::kGroupCols);
+        total += static_cast<uint64_t>(blk_groups[b]) * swk::kGroupBytes;
+    }
+    std::vector<uint8_t> res(total, swk::kPadCode);
+    parallel_for(nblocks, [&](int64_t b) {
+        for (int l = 0; l < swk::kLanes; ++l) {
+            const int64_t k = nlong + b * swk::kLanes + l;
+            if (k >= n) break;
+            const int64_t src = order[k];
+            lane_ids[b * swk::kLanes + l] = db->h_ids[src];
+            const uint8_t* p = db->h_residues.data() + db->h_offsets[src];
+            const int64_t L = len(src);
+            for (int64_t j = 0; j < L; ++j)
+                res[blk_off[b] + (j / swk::kGroupCols) * swk::kGroupBytes + l * swk::kGroupCols +
+                    (j % swk::kGroupCols)] = p[j];
+        }
+    });
+
+    size_t acc = 0;
+    int rc;
+    if ((rc = upload(&db->d_res, res, s, &acc))) return rc;
+    if ((rc = upload(&db->d_blk_off, blk_off, s, &acc))) return rc;
+    if ((rc = upload(&db->d_blk_groups, blk_groups, s, &acc))) return rc;
+    if ((rc = upload(&db->d_lane_ids, lane_ids, s, &acc))) return rc;
+    if ((rc = upload(&db->d_lres, lres, s, &acc))) return rc;
+    if ((rc = upload(&db->d_loff, loff, s, &acc))) return rc;
+    if ((rc = upload(&db->d_llen, llen, s, &acc))) return rc;
+    if ((rc = upload(&db->d_lid, lid, s, &acc))) return rc;
+    HIPCHECK(hipStreamSynchronize(s));  // host vectors go out of scope
+    db->res_bytes = total;
+    db->lres_bytes = ltotal;
+    db->nblocks = nblocks;
+    db->nlong = nlong;
+    db->packed_cells = static_cast<int64_t>(total);  // one byte per scanned (lane, column)
+    db->device_bytes = acc;
+    db->built = true;
+    return SW_OK;
+}
+
+// Boundary rows are only needed when the query spans more than one strip;
+// allocate on first need and keep.
+int ensure_bnd(sw_db* db, bool affine) {
+    if (db->res_bytes && !db->d_bnd_h) {
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_bnd_h), db->res_bytes * 4));
+        db->device_bytes += db->res_bytes * 4;
+    }
+    if (affine && db->res_bytes && !db->d_bnd_f) {
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_bnd_f), db->res_bytes * 4));
+        db->device_bytes += db->res_bytes * 4;
+    }
+    if (db->lres_bytes && !db->d_lbnd_h) {
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lbnd_h), db->lres_bytes * 4));
+        db->device_bytes += db->lres_bytes * 4;
+    }
+    if (affine && db->lres_bytes && !db->d_lbnd_f) {
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lbnd_f), db->lres_bytes * 4));
+        db->device_bytes += db->lres_bytes * 4;
+    }
+    return SW_OK;
+}
+
+int check_scoring(const sw_scoring* sc, const int8_t** mat, int* go, int* ge) {
+    *mat = kBlosum50Ref;
+    *go = 2;
+    *ge = 2;
+    if (sc) {
+        if (sc->matrix) *mat = sc->matrix;
+        *go = sc->gap_open;
+        *ge = sc->gap_extend;
+    }
+    if (*go <= 0 || *ge <= 0 || *go > 1000 || *ge > 1000)
+        return fail(SW_E_INVALID, "gap penalties must be in 1..1000");
+    for (int k = 0; k < 625; ++k)
+        if ((*mat)[k] < -100 || (*mat)[k] > 100) return fail(SW_E_INVALID, "matrix entries must be in -100..100");
+    return SW_OK;
+}
+
+// Query profile: prof[c][i] = S[q_i][c] (+ gap for the linear kernels) for
+// residue codes c < 25; rows c >= 25 (the pad code) and columns i >= qlen
+// score 0 (+ gap).  A zero-score pad row/column can never raise the maximum
+// (every such cell is <= max(0, its diagonal, its gap predecessors)).
+int build_profile(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* mat, int go, bool affine,
+                  int32_t stride) {
+    const int bias = affine ? 0 : go;
+    h->h_prof.assign(static_cast<size_t>(swk::kProfileRows) * stride, static_cast<int8_t>(bias));
+    for (int32_t i = 0; i < qlen; ++i) {
+        if (q[i] >= SW_ALPHABET) return fail(SW_E_INVALID, "query residue code out of range (use sw_encode)");
+        const int8_t* row = mat + 25 * q[i];
+        for (int c = 0; c < SW_ALPHABET; ++c)
+            h->h_prof[static_cast<size_t>(c) * stride + i] = static_cast<int8_t>(row[c] + bias);
+    }
+    const size_t bytes = h->h_prof.size();
+    if (bytes > h->prof_cap) {
+        if (h->d_prof) HIPCHECK(hipFree(h->d_prof));
+        h->prof_cap = std::max<size_t>(bytes, 1 << 16);
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&h->d_prof), h->prof_cap));
+    }
+    HIPCHECK(hipMemcpyAsync(h->d_prof, h->h_prof.data(), bytes, hipMemcpyHostToDevice, h->stream));
+    return SW_OK;
+}
+
+int next_events(sw_handle* h) {
+    if (h->nscans >= 4096) h->nscans = 0;  // bound the pool; older sums are dropped
+    if (h->nscans == h->evpool.size()) {
+        ScanEvents se;
+        for (auto& e : se.ev) HIPCHECK(hipEventCreate(&e));
+        h->evpool.push_back(se);
+    }
+    h->ev = h->evpool[h->nscans].ev;
+    h->evpool[h->nscans].launches = 0;
+    ++h->nscans;
+    return SW_OK;
+}
+
+int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen, const sw_scoring* sc,
+              int32_t* scores_dev) {
+    sw_db* db = const_cast<sw_db*>(cdb);
+    if (!h || !db || (!query && qlen > 0) || qlen < 0 || !scores_dev) return fail(SW_E_INVALID, "null argument");
+    const int8_t* mat;
+    int go, ge, rc;
+    if ((rc = check_scoring(sc, &mat, &go, &ge))) return rc;
+    const bool affine = go != ge;
+    if (!db->built && (rc = build_db(db))) return rc;
+    HIPCHECK(hipSetDevice(h->device));
+    h->launches = 0;
+    h->had_intra = false;
+    if ((rc = next_events(h))) return rc;
+
+    const int R = swk::inter_rows(affine);
+    const int CH = swk::kLanes * swk::intra_rows_per_lane(affine);
+    const int32_t qpad_inter = static_cast<int32_t>(round_up(qlen, R));
+    const int32_t qpad_intra = static_cast<int32_t>(round_up(qlen, CH));
+    const int32_t stride = static_cast<int32_t>(round_up(std::max<int32_t>({qpad_inter, qpad_intra, 16}), 16));
+    // Empty query: every score is 0 (the reference's kernel leaves maxScore 0).
+    if (qlen == 0) {
+        HIPCHECK(hipEventRecord(h->ev[0], h->stream));
+        if (db->max_id >= 0)
+            HIPCHECK(hipMemsetAsync(scores_dev, 0, static_cast<size_t>(db->max_id + 1) * 4, h->stream));
+        HIPCHECK(hipEventRecord(h->ev[1], h->stream));
+        HIPCHECK(hipEventRecord(h->ev[2], h->stream));
+        HIPCHECK(hipEventRecord(h->ev[3], h->stream));
+        h->timed = true;
+        return SW_OK;
+    }
+    if ((rc = build_profile(h, query, qlen, mat, go, affine, stride))) return rc;
+    const bool multi_inter = qpad_inter > R;
+    const bool multi_intra = qpad_intra > CH;
+    if ((multi_inter || multi_intra || db->nlong) && (rc = ensure_bnd(db, affine))) return rc;
+
+    HIPCHECK(hipEventRecord(h->ev[0], h->stream));
+    if (db->nlong) {
+        swk::IntraArgs ia{};
+        ia.residues = db->d_lres;
+        ia.subj_off = db->d_loff;
+        ia.subj_len = db->d_llen;
+        ia.subj_id = db->d_lid;
+        ia.nsubj = static_cast<int32_t>(db->nlong);
+        ia.prof = h->d_prof;
+        ia.prof_stride = stride;
+        ia.qpad = qpad_intra;
+        ia.gap_open = go;
+        ia.gap_extend = ge;
+        ia.bnd_h = db->d_lbnd_h;
+        ia.bnd_f = db->d_lbnd_f;
+        ia.scores = scores_dev;
+        HIPCHECK(swk::launch_intra(ia, affine, h->stream));
+        ++h->launches;
+        h->had_intra = true;
+    }
+    HIPCHECK(hipEventRecord(h->ev[1], h->stream));
+    if (db->nblocks) {
+        swk::InterArgs a{};
+        a.residues = db->d_res;
+        a.blk_off = db->d_blk_off;
+        a.blk_groups = db->d_blk_groups;
+        a.lane_ids = db->d_lane_ids;
+        a.nblocks = static_cast<int32_t>(db->nblocks);
+        a.prof = h->d_prof;
+        a.prof_stride = stride;
+        a.qpad = qpad_inter;
+        a.gap_open = go;
+        a.gap_extend = ge;
+        a.bnd_h = db->d_bnd_h;
+        a.bnd_f = db->d_bnd_f;
+        a.scores = scores_dev;
+        HIPCHECK(swk::launch_inter(a, affine, h->stream));
+        ++h->launches;
+    }
+    HIPCHECK(hipEventRecord(h->ev[2], h->stream));
+    HIPCHECK(hipEventRecord(h->ev[3], h->stream));
+    h->evpool[h->nscans - 1].launches = h->launches;
+    h->timed = true;
+    return SW_OK;
+}
+
+int ensure_scores(sw_handle* h, size_t n) {
+    if (n > h->scores_cap) {
+        if (h->d_scores) HIPCHECK(hipFree(h->d_scores));
+        h->scores_cap = std::max<size_t>(n, 1024);
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&h->d_scores), h->scores_cap * 4));
+    }
+    return SW_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+extern "C" {
+
+int32_t sw_version(void) { return 10000 * 0 + 100 * 1 + 0; }
+
+const char* sw_last_error(void) { return g_err.c_str(); }
+
+int sw_encode(const char* ascii, int64_t n, uint8_t* codes) {
+    if ((!ascii || !codes) && n > 0) return fail(SW_E_INVALID, "null argument");
+    init_lut();
+    for (int64_t i = 0; i < n; ++i) codes[i] = static_cast<uint8_t>(g_encode_lut[static_cast<unsigned char>(ascii[i])]);
+    return SW_OK;
+}
+
+int sw_builtin_matrix(int32_t id, int8_t* out625) {
+    if (!out625) return fail(SW_E_INVALID, "null argument");
+    if (id == SW_MATRIX_BLOSUM50_REF) {
+        std::memcpy(out625, kBlosum50Ref, 625);
+    } else if (id == SW_MATRIX_BLOSUM62) {
+        std::memcpy(out625, kBlosum62, 625);
+    } else if (id == SW_MATRIX_IDENTITY3) {
+        for (int a = 0; a < 25; ++a)
+            for (int b = 0; b < 25; ++b) out625[a * 25 + b] = static_cast<int8_t>(a == b ? 3 : -3);
+    } else {
+        return fail(SW_E_INVALID, "unknown matrix id");
+    }
+    return SW_OK;
+}
+
+int sw_create(int32_t device, sw_handle** out) {
+    if (!out) return fail(SW_E_INVALID, "null argument");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SW_E_NODEVICE, "no HIP device visible");
+    if (device < 0 || device >= ndev) return fail(SW_E_INVALID, "device index out of range");
+    HIPCHECK(hipSetDevice(device));
+    auto* h = new (std::nothrow) sw_handle();
+    if (!h) return fail(SW_E_NOMEM, "out of host memory");
+    h->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete h; return fail(SW_E_HIP, hipGetErrorString(e)); }
+    h->own_stream = true;
+    *out = h;
+    return SW_OK;
+}
+
+int sw_destroy(sw_handle* h) {
+    if (!h) return SW_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (auto& se : h->evpool)
+        for (auto& ev : se.ev)
+            if (ev) (void)hipEventDestroy(ev);
+    if (h->d_prof) (void)hipFree(h->d_prof);
+    if (h->d_scores) (void)hipFree(h->d_scores);
+    if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return SW_OK;
+}
+
+void* sw_stream(sw_handle* h) { return h ? reinterpret_cast<void*>(h->stream) : nullptr; }
+
+int sw_set_stream(sw_handle* h, void* hip_stream) {
+    if (!h) return fail(SW_E_INVALID, "null handle");
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    if (h->own_stream) HIPCHECK(hipStreamDestroy(h->stream));
+    if (hip_stream) {
+        h->stream = reinterpret_cast<hipStream_t>(hip_stream);
+        h->own_stream = false;
+    } else {
+        HIPCHECK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        h->own_stream = true;
+    }
+    return SW_OK;
+}
+
+int sw_db_create(sw_handle* h, const uint8_t* residues, const int64_t* offsets, int64_t n, const int32_t* ids,
+                 sw_db** out) {
+    if (!h || !out || n < 0 || (n > 0 && !offsets)) return fail(SW_E_INVALID, "null argument");
+    *out = nullptr;
+    if (n > 0 && offsets[0] != 0) return fail(SW_E_INVALID, "offsets[0] must be 0");
+    for (int64_t k = 0; k < n; ++k)
+        if (offsets[k + 1] < offsets[k]) return fail(SW_E_INVALID, "offsets must be non-decreasing");
+    const int64_t total = n > 0 ? offsets[n] : 0;
+    if (total > 0 && !residues) return fail(SW_E_INVALID, "null residues");
+    for (int64_t k = 0; k < n; ++k)
+        if (offsets[k + 1] - offsets[k] > (int64_t(1) << 30)) return fail(SW_E_INVALID, "subject too long");
+    auto* db = new (std::nothrow) sw_db();
+    if (!db) return fail(SW_E_NOMEM, "out of host memory");
+    db->h = h;
+    db->n = n;
+    try {
+        db->h_residues.assign(residues, residues + total);
+        db->h_offsets.assign(offsets, offsets + n + 1);
+        if (n == 0) db->h_offsets.assign(1, 0);
+        db->h_ids.resize(n);
+        for (int64_t k = 0; k < n; ++k) db->h_ids[k] = ids ? ids[k] : static_cast<int32_t>(k);
+    } catch (...) {
+        delete db;
+        return fail(SW_E_NOMEM, "out of host memory");
+    }
+    for (int64_t k = 0; k < total; ++k)
+        if (db->h_residues[k] >= SW_ALPHABET) {
+            delete db;
+            return fail(SW_E_INVALID, "residue code out of range (use sw_encode)");
+        }
+    db->residues = total;
+    for (int64_t k = 0; k < n; ++k) {
+        db->max_len = std::max<int32_t>(db->max_len, static_cast<int32_t>(offsets[k + 1] - offsets[k]));
+        if (db->h_ids[k] < 0) { delete db; return fail(SW_E_INVALID, "ids must be >= 0"); }
+        db->max_id = std::max(db->max_id, db->h_ids[k]);
+    }
+    db->long_threshold = kDefaultLongThreshold;
+    HIPCHECK(hipSetDevice(h->device));
+    int rc = build_db(db);
+    if (rc) { free_dev(db); delete db; return rc; }
+    *out = db;
+    return SW_OK;
+}
+
+int sw_db_free(sw_db* db) {
+    if (!db) return SW_OK;
+    (void)hipSetDevice(db->h->device);
+    (void)hipStreamSynchronize(db->h->stream);
+    free_dev(db);
+    delete db;
+    return SW_OK;
+}
+
+int sw_db_get_stats(const sw_db* db, sw_db_stats* out) {
+    if (!db || !out) return fail(SW_E_INVALID, "null argument");
+    out->n_subjects = db->n;
+    out->residues = db->residues;
+    out->packed_cells = db->packed_cells;
+    out->n_blocks = db->nblocks;
+    out->n_long = db->nlong;
+    out->device_bytes = static_cast<int64_t>(db->device_bytes);
+    out->max_length = db->max_len;
+    out->long_threshold = db->long_threshold;
+    return SW_OK;
+}
+
+int sw_db_set_long_threshold(sw_db* db, int32_t threshold) {
+    if (!db) return fail(SW_E_INVALID, "null argument");
+    if (threshold < 0) return fail(SW_E_INVALID, "threshold must be >= 0");
+    const int32_t t = threshold == 0 ? kDefaultLongThreshold : threshold;
+    if (t == db->long_threshold && db->built) return SW_OK;
+    HIPCHECK(hipSetDevice(db->h->device));
+    HIPCHECK(hipStreamSynchronize(db->h->stream));
+    free_dev(db);
+    db->long_threshold = t;
+    return build_db(db);
+}
+
+int sw_scan_device(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen, const sw_scoring* sc,
+                   int32_t* scores_dev) {
+    return scan_impl(h, db, query, qlen, sc, scores_dev);
+}
+
+int sw_scan(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen, const sw_scoring* sc,
+            int32_t* scores_host) {
+    if (!h || !db || !scores_host) return fail(SW_E_INVALID, "null argument");
+    const size_t n = static_cast<size_t>(db->max_id + 1);
+    if (n == 0) return SW_OK;
+    int rc;
+    HIPCHECK(hipSetDevice(h->device));
+    if ((rc = ensure_scores(h, n))) return rc;
+    // slots that no subject maps to read 0
+    HIPCHECK(hipMemsetAsync(h->d_scores, 0, n * 4, h->stream));
+    if ((rc = scan_impl(h, db, query, qlen, sc, h->d_scores))) return rc;
+    HIPCHECK(hipMemcpyAsync(scores_host, h->d_scores, n * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    return SW_OK;
+}
+
+int sw_scan_batch(sw_handle* h, const sw_db* db, const uint8_t* queries, const int64_t* qoffsets, int32_t nq,
+                  const sw_scoring* sc, int32_t* scores_host) {
+    if (!h || !db || nq < 0 || (nq > 0 && (!qoffsets || !scores_host))) return fail(SW_E_INVALID, "null argument");
+    const size_t n = static_cast<size_t>(db->max_id + 1);
+    for (int32_t k = 0; k < nq; ++k) {
+        const int64_t ql = qoffsets[k + 1] - qoffsets[k];
+        if (ql < 0 || ql > (int64_t(1) << 24)) return fail(SW_E_INVALID, "bad query offsets");
+        int rc = sw_scan(h, db, queries + qoffsets[k], static_cast<int32_t>(ql), sc, scores_host + k * n);
+        if (rc) return rc;
+    }
+    return SW_OK;
+}
+
+namespace {
+int read_events(const ScanEvents& se, sw_timing* t) {
+    HIPCHECK(hipEventSynchronize(se.ev[3]));
+    float t01 = 0, t12 = 0, t03 = 0;
+    HIPCHECK(hipEventElapsedTime(&t01, se.ev[0], se.ev[1]));
+    HIPCHECK(hipEventElapsedTime(&t12, se.ev[1], se.ev[2]));
+    HIPCHECK(hipEventElapsedTime(&t03, se.ev[0], se.ev[3]));
+    t->intra_ms += t01;
+    t->inter_ms += t12;
+    t->total_ms += t03;
+    t->launches += se.launches;
+    return SW_OK;
+}
+}  // namespace
+
+int sw_get_timing(sw_handle* h, sw_timing* out) {
+    if (!h || !out) return fail(SW_E_INVALID, "null argument");
+    std::memset(out, 0, sizeof(*out));
+    if (!h->timed || h->nscans == 0) return SW_OK;
+    return read_events(h->evpool[h->nscans - 1], out);
+}
+
+int sw_timing_reset(sw_handle* h) {
+    if (!h) return fail(SW_E_INVALID, "null argument");
+    h->nscans = 0;
+    h->timed = false;
+    return SW_OK;
+}
+
+int sw_timing_total(sw_handle* h, sw_timing* out, int32_t* nscans) {
+    if (!h || !out || !nscans) return fail(SW_E_INVALID, "null argument");
+    std::memset(out, 0, sizeof(*out));
+    *nscans = static_cast<int32_t>(h->nscans);
+    for (size_t k = 0; k < h->nscans; ++k) {
+        int rc = read_events(h->evpool[k], out);
+        if (rc) return rc;
+    }
+    return SW_OK;
+}
+
+int sw_topk(const int32_t* scores, int64_t n, int32_t k, int32_t* out_ids, int32_t* out_scores) {
+    if ((!scores && n > 0) || k < 0 || (k > 0 && (!out_ids || !out_scores))) return fail(SW_E_INVALID, "null argument");
+    const int64_t kk = std::min<int64_t>(k, n);
+    std::vector<int32_t> idx(n);
+    std::iota(idx.begin(), idx.end(), 0);
+    auto cmp = [&](int32_t a, int32_t b) { return scores[a] != scores[b] ? scores[a] > scores[b] : a < b; };
+    std::partial_sort(idx.begin(), idx.begin() + kk, idx.end(), cmp);
+    for (int64_t i = 0; i < kk; ++i) {
+        out_ids[i] = idx[i];
+        out_scores[i] = scores[idx[i]];
+    }
+    for (int64_t i = kk; i < k; ++i) {
+        out_ids[i] = -1;
+        out_scores[i] = 0;
+    }
+    return SW_OK;
+}
+
+int sw_score_pair(sw_handle* h, const uint8_t* query, int32_t qlen, const uint8_t* subject, int32_t slen,
+                  const sw_scoring* sc, int32_t* score) {
+    if (!h || !score || slen < 0 || qlen < 0) return fail(SW_E_INVALID, "null argument");
+    const int64_t offs[2] = {0, slen};
+    const int32_t id = 0;
+    sw_db* db = nullptr;
+    int rc = sw_db_create(h, subject, offs, 1, &id, &db);
+    if (rc) return rc;
+    // a single pair takes the wavefront kernel (all subjects longer than 1)
+    if ((rc = sw_db_set_long_threshold(db, 1))) { sw_db_free(db); return rc; }
+    rc = sw_scan(h, db, query, qlen, sc, score);
+    sw_db_free(db);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,69 @@
+// sw_kernels.h — internal interface between the host driver (sw_capi.cpp)
+// and the gfx950 kernels (sw_kernels.hip).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace swk {
+
+constexpr int kLanes = 64;        // one database subject per lane (wave64)
+constexpr int kGroupCols = 16;    // residue columns per packed group
+constexpr int kGroupBytes = kLanes * kGroupCols;  // 1 KiB: [lane][16 residues]
+constexpr int kProfileRows = 32;  // profile codes: 25 residues + PAD (25) + unused
+constexpr int kPadCode = 25;      // residue code used for padding (scores 0)
+constexpr int kWavesPerWG = 4;
+
+// Packed database, inter-sequence part (the layout
+// replaces the reference's [block][col][32-lane] short interleave,
+// SWSolver.cu:316):
+//   residues : for block b, at byte blk_off[b]: ngroups[b] groups, each
+//              [64 lanes][16 residue codes]  (one dwordx4 per lane)
+//   bnd_h/f  : int32 boundary rows in the SAME index space as residues
+//              (4 bytes per residue byte), the DP row handed from one
+//              query strip to the next (replaces the 3.7 GB short
+//              "collapsed" matrix, SWSolver.cu:231-258,288)
+struct InterArgs {
+    const uint8_t* residues;
+    const uint64_t* blk_off;     // byte offset of group 0 of each block
+    const uint32_t* blk_groups;  // number of 16-column groups per block
+    const int32_t* lane_ids;     // [nblocks][64] result slot, -1 = empty lane
+    int32_t nblocks;
+    const int8_t* prof;          // [kProfileRows][prof_stride] query profile (see host)
+    int32_t prof_stride;         // bytes per profile row (>= qpad, multiple of 16)
+    int32_t qpad;                // query length rounded up to the strip height
+    int32_t gap_open;
+    int32_t gap_extend;
+    int32_t* bnd_h;
+    int32_t* bnd_f;
+    int32_t* scores;             // scores[id]
+    int32_t* sat_flags;          // reserved for the int16 path
+};
+
+// Long subjects: one wave per subject, query rows spread over the 64 lanes,
+// anti-diagonal wavefront with wave_shr DPP hand-off between lanes.
+struct IntraArgs {
+    const uint8_t* residues;     // plain concatenated codes of the long subjects
+    const uint64_t* subj_off;    // byte offset of each long subject
+    const int32_t* subj_len;
+    const int32_t* subj_id;
+    int32_t nsubj;
+    const int8_t* prof;          // [kProfileRows][prof_stride]
+    int32_t prof_stride;
+    int32_t qpad;                // multiple of 64 * rows-per-lane
+    int32_t gap_open;
+    int32_t gap_extend;
+    int32_t* bnd_h;              // per subject: subj_off-indexed int32 rows
+    int32_t* bnd_f;
+    int32_t* scores;
+};
+
+// Strip heights (query rows held in registers per lane) the kernels are
+// instantiated for.
+int inter_rows(bool affine);
+int intra_rows_per_lane(bool affine);
+
+hipError_t launch_inter(const InterArgs& a, bool affine, hipStream_t s);
+hipError_t launch_intra(const IntraArgs& a, bool affine, hipStream_t s);
+
+}  // namespace swk

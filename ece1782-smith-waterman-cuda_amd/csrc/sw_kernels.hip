@@ -1,0 +1,445 @@
+// sw_kernels.hip — gfx950 (CDNA4) Smith-Waterman score-only kernels.
+//
+// Recurrence (the reference's, SWSolver.cu:246; cpu.cpp:43-74), linear gap g:
+//     H(i,j) = max(0, H(i-1,j-1) + S[q_i][s_j], H(i,j-1) - g, H(i-1,j) - g)
+// and its affine generalisation (Gotoh; go == ge reduces to the above):
+//     E(i,j) = max(E(i,j-1) - ge, H(i,j-1) - go)
+//     F(i,j) = max(F(i-1,j) - ge, H(i-1,j) - go)
+//     H(i,j) = max(0, H(i-1,j-1) + S, E(i,j), F(i,j))
+// score = max over all cells.  Integer max/add DP: no MFMA anywhere.
+//
+// Two kernels:
+//  * inter   — one database subject per lane (the reference's parallelism,
+//              SWSolver.cu:201-264, re-designed for wave64): the lane keeps R
+//              query rows of its DP column in VGPRs, walks its subject left to
+//              right, and hands the strip's bottom row to the next strip
+//              through an int32 boundary row in HBM.  The query profile for
+//              the strip (32 codes x R rows, int8) is staged in a wave-private
+//              LDS slice; per column a lane reads its R scores with
+//              ds_read_b128 at its own residue's row.  The per-cell sequence
+//              is v_add_u32_sdwa (sign-extended profile byte) + v_max3_i32 +
+//              v_sub_u32 clamp (+ half a v_max3 for the running maximum).
+//  * intra   — one long subject per wave: lane t owns query rows
+//              [t*RI, (t+1)*RI) of a 64*RI-row chunk and processes column
+//              j = k - t at step k (anti-diagonal wavefront).  The bottom-row
+//              H (and F) of lane t-1 and the residue code reach lane t through
+//              DPP wave_shr:1; lane 0 is fed from the previous chunk's
+//              boundary row, lane 63's output becomes the next chunk's.
+//
+// Profile bias: for the linear kernels the host stores S + g in the profile,
+// so a cell is  h = usat(max3(H_left, H_up, H_diag + S + g) - g)  (the
+// saturating subtract supplies the 0 floor; H_left, H_up >= 0).  For affine
+// the profile holds S, and E/F are kept clamped at 0 (exact: a negative E or F
+// can never win the max against the 0 floor, and clamping commutes with the
+// "- ge" step because ge > 0).
+#include "sw_kernels.h"
+
+#ifndef SW_INTER_SG
+#define SW_INTER_SG 16
+#endif
+
+namespace swk {
+
+// LDS row stride (bytes) of the inter profile slice: >= R+16, a multiple of
+// 16 with an odd number of 16-byte slots so that ds_read_b128 of different
+// residue rows lands in different bank slots (MI355X_MICROARCH.md §LDS).
+__host__ __device__ constexpr int inter_stride(int R) {
+    return ((R + 16 + 15) / 16) % 2 == 1 ? ((R + 16 + 15) / 16) * 16
+                                         : ((R + 16 + 15) / 16 + 1) * 16;
+}
+
+__device__ __forceinline__ int sx8(uint32_t w, int b) {
+    return static_cast<int>(static_cast<int8_t>(w >> (8 * b)));
+}
+
+__device__ __forceinline__ int usub(int m, uint32_t g) {
+    return static_cast<int>(__builtin_elementwise_sub_sat(static_cast<uint32_t>(m), g));
+}
+
+template <int N>
+__device__ __forceinline__ uint32_t pword(const int4 (&v)[N], int w) {
+    const int4 q = v[w >> 2];
+    switch (w & 3) {
+        case 0: return static_cast<uint32_t>(q.x);
+        case 1: return static_cast<uint32_t>(q.y);
+        case 2: return static_cast<uint32_t>(q.z);
+        default: return static_cast<uint32_t>(q.w);
+    }
+}
+
+// Stage rows [s0, s0+R) of the profile into the wave's LDS slice:
+// 32 codes x R bytes = 2R chunks of 16 B, spread over the 64 lanes.
+template <int R>
+__device__ __forceinline__ void stage_profile(uint8_t* lp, const int8_t* __restrict__ prof,
+                                              int stride, int s0, int lane) {
+    constexpr int kChunks = kProfileRows * (R / 16);
+    constexpr int S = inter_stride(R);
+#pragma unroll
+    for (int t = lane; t < kChunks; t += kLanes) {
+        const int c = t / (R / 16);
+        const int k = t % (R / 16);
+        const int4 v = *reinterpret_cast<const int4*>(prof + static_cast<size_t>(c) * stride + s0 + 16 * k);
+        *reinterpret_cast<int4*>(lp + c * S + 16 * k) = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// inter-sequence kernels (linear and affine share one body)
+// ---------------------------------------------------------------------------
+// Per wave: one 64-subject block.  Per strip of R query rows: stage the
+// profile slice, then walk the block's columns in sub-groups of SG columns.
+// Software pipeline (the compiler would otherwise hoist every column's LDS
+// reads and spill): the NEXT column's profile rows are read before the
+// current column is computed, and the next sub-group's residues and boundary
+// values are loaded at the top of the current sub-group; a sched_barrier
+// closes each column.
+template <int SG>
+struct Residues {
+    uint32_t w[SG / 4];
+    __device__ __forceinline__ void load(const uint8_t* p) {
+        if constexpr (SG == 16) {
+            const int4 v = *reinterpret_cast<const int4*>(p);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else if constexpr (SG == 8) {
+            const int2 v = *reinterpret_cast<const int2*>(p);
+            w[0] = v.x; w[1] = v.y;
+        } else {
+            w[0] = *reinterpret_cast<const uint32_t*>(p);
+        }
+    }
+    __device__ __forceinline__ uint32_t code(int jj) const { return (w[jj >> 2] >> (8 * (jj & 3))) & 0xffu; }
+};
+
+template <int SG>
+__device__ __forceinline__ void load_row(int (&v)[SG], const int32_t* p) {
+#pragma unroll
+    for (int q = 0; q < SG / 4; ++q) {
+        const int4 t = *reinterpret_cast<const int4*>(p + 4 * q);
+        v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+    }
+}
+
+template <int SG>
+__device__ __forceinline__ void store_row(int32_t* p, const int (&v)[SG]) {
+#pragma unroll
+    for (int q = 0; q < SG / 4; ++q)
+        *reinterpret_cast<int4*>(p + 4 * q) = make_int4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+
+// `dep` ties the read to a value produced by the previous column: without it
+// the IR scheduler hoists every unrolled column's LDS reads to the top of the
+// body (sched_barrier only binds the machine scheduler) and the kernel
+// balloons to 256+ VGPRs.
+template <int R>
+__device__ __forceinline__ void read_prof(int4 (&pv)[R / 16], const uint8_t* lp, uint32_t c, int dep) {
+    constexpr int S = inter_stride(R);
+    uint32_t off = c * S;
+    asm volatile("" : "+v"(off) : "v"(dep));
+    const int4* pp = reinterpret_cast<const int4*>(lp + off);
+#pragma unroll
+    for (int q = 0; q < R / 16; ++q) pv[q] = pp[q];
+}
+
+template <int R, int SG, bool AFFINE>
+__global__ __launch_bounds__(256) void sw_inter(InterArgs a) {
+    constexpr int S = inter_stride(R);
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerWG * kProfileRows * S];
+    // threadIdx.x >> 6 is wave-uniform, but the compiler cannot prove it:
+    // without readfirstlane every bound below would be a divergent VGPR value.
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int blk = blockIdx.x * kWavesPerWG + wave;
+    if (blk >= a.nblocks) return;  // wave-uniform
+    uint8_t* lp = lds + wave * (kProfileRows * S);
+
+    const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
+    const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
+    const uint32_t go = static_cast<uint32_t>(a.gap_open);
+    const uint32_t ge = static_cast<uint32_t>(a.gap_extend);
+    int best = 0;
+    if (ncols == 0) goto done;
+
+    for (int s0 = 0; s0 < a.qpad; s0 += R) {
+        const bool first = (s0 == 0);
+        const bool last = (s0 + R >= a.qpad);
+        stage_profile<R>(lp, a.prof, a.prof_stride, s0, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+
+        int H[R];
+        int E[AFFINE ? R : 1];
+#pragma unroll
+        for (int r = 0; r < R; ++r) H[r] = 0;
+#pragma unroll
+        for (int r = 0; r < (AFFINE ? R : 1); ++r) E[r] = 0;
+        int dtop = 0;  // H(s0-1, j-1)
+
+        Residues<SG> rs, rs_next;
+        int bh[SG], bh_next[SG];
+        int bf[AFFINE ? SG : 1], bf_next[AFFINE ? SG : 1];
+        rs.load(a.residues + base);
+        if (!first) {
+            load_row<SG>(bh, a.bnd_h + base);
+            if constexpr (AFFINE) load_row<SG>(bf, a.bnd_f + base);
+        } else {
+#pragma unroll
+            for (int q = 0; q < SG; ++q) bh[q] = 0;
+#pragma unroll
+            for (int q = 0; q < (AFFINE ? SG : 1); ++q) bf[q] = 0;
+        }
+        int4 pcur[R / 16], pnext[R / 16];
+        read_prof<R>(pcur, lp, rs.code(0), 0);
+
+        for (uint32_t col0 = 0; col0 < ncols; col0 += SG) {
+            const uint64_t idx = base + (col0 >> 4) * kGroupBytes + (col0 & 15);
+            const bool more = col0 + SG < ncols;
+            const uint64_t nidx = base + ((col0 + SG) >> 4) * kGroupBytes + ((col0 + SG) & 15);
+            if (more) {
+                rs_next.load(a.residues + nidx);
+                if (!first) {
+                    load_row<SG>(bh_next, a.bnd_h + nidx);
+                    if constexpr (AFFINE) load_row<SG>(bf_next, a.bnd_f + nidx);
+                }
+            }
+#pragma unroll
+            for (int jj = 0; jj < SG; ++jj) {
+                // prefetch the next column's profile rows
+                if (jj + 1 < SG) {
+                    read_prof<R>(pnext, lp, rs.code(jj + 1), H[R - 1]);
+                } else if (more) {
+                    read_prof<R>(pnext, lp, rs_next.code(0), H[R - 1]);
+                }
+                int up = bh[jj];
+                int diag = dtop;
+                dtop = up;
+                if constexpr (!AFFINE) {
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int sc = sx8(pword(pcur, r >> 2), r & 3);
+                        const int h = usub(max(max(H[r], up), diag + sc), go);
+                        diag = H[r];
+                        H[r] = h;
+                        up = h;
+                        best = max(best, h);
+                    }
+                } else {
+                    int f = bf[jj];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int sc = sx8(pword(pcur, r >> 2), r & 3);
+                        const int e = max(usub(E[r], ge), usub(H[r], go));
+                        f = max(usub(f, ge), usub(up, go));
+                        const int h = max(max(e, f), diag + sc);
+                        diag = H[r];
+                        H[r] = h;
+                        E[r] = e;
+                        up = h;
+                        best = max(best, h);
+                    }
+                    bf[jj] = f;
+                }
+                bh[jj] = up;
+#pragma unroll
+                for (int q = 0; q < R / 16; ++q) pcur[q] = pnext[q];
+                // Stop LLVM from reassociating the running max across the
+                // unrolled columns (it would keep every column's H alive).
+                asm volatile("" : "+v"(best));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (!last) {
+                store_row<SG>(a.bnd_h + idx, bh);
+                if constexpr (AFFINE) store_row<SG>(a.bnd_f + idx, bf);
+            }
+            if (more) {
+                rs = rs_next;
+                if (!first) {
+#pragma unroll
+                    for (int q = 0; q < SG; ++q) bh[q] = bh_next[q];
+                    if constexpr (AFFINE) {
+#pragma unroll
+                        for (int q = 0; q < SG; ++q) bf[q] = bf_next[q];
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < SG; ++q) bh[q] = 0;
+                    if constexpr (AFFINE) {
+#pragma unroll
+                        for (int q = 0; q < SG; ++q) bf[q] = 0;
+                    }
+                }
+            }
+        }
+    }
+done:
+    const int id = a.lane_ids[static_cast<size_t>(blk) * kLanes + lane];
+    if (id >= 0) a.scores[id] = best;
+}
+
+// ---------------------------------------------------------------------------
+// intra-sequence wavefront (one long subject per wave)
+// ---------------------------------------------------------------------------
+// DPP controls (GFX9 family): wave_shr:1 moves lane t-1's value to lane t;
+// lane 0 keeps `old`.
+constexpr int kDppWaveShr1 = 0x138;
+
+__device__ __forceinline__ int shr1(int old, int src) {
+    return __builtin_amdgcn_update_dpp(old, src, kDppWaveShr1, 0xf, 0xf, false);
+}
+
+__host__ __device__ constexpr int intra_stride(int RI) { return kLanes * RI + 8; }
+
+template <int RI, bool AFFINE>
+__global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
+    const int prof_stride = a.prof_stride;
+    constexpr int CH = kLanes * RI;  // query rows per chunk
+    constexpr int S = intra_stride(RI);
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kProfileRows * S];
+    const int lane = threadIdx.x;
+    const int sid = blockIdx.x;
+    if (sid >= a.nsubj) return;
+    const int L = a.subj_len[sid];
+    const uint8_t* __restrict__ res = a.residues + a.subj_off[sid];
+    int32_t* bnd_h = a.bnd_h + a.subj_off[sid];
+    int32_t* bnd_f = AFFINE ? a.bnd_f + a.subj_off[sid] : nullptr;
+    const uint32_t go = static_cast<uint32_t>(a.gap_open);
+    const uint32_t ge = static_cast<uint32_t>(a.gap_extend);
+    int best = 0;
+
+    for (int c0 = 0; c0 < a.qpad; c0 += CH) {
+        const bool first = (c0 == 0);
+        const bool last = (c0 + CH >= a.qpad);
+        __syncthreads();  // previous chunk's LDS reads are done
+        // stage profile rows [c0, c0+CH) for all 32 codes: 32*CH bytes
+        for (int t = lane; t < kProfileRows * (CH / 16); t += kLanes) {
+            const int c = t / (CH / 16);
+            const int k = t % (CH / 16);
+            const int4 v = *reinterpret_cast<const int4*>(a.prof + static_cast<size_t>(c) * prof_stride + c0 + 16 * k);
+            int* d = reinterpret_cast<int*>(lds + c * S + 16 * k);  // S is only 8-byte aligned
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
+        __syncthreads();
+
+        int H[RI], E[RI];
+#pragma unroll
+        for (int r = 0; r < RI; ++r) { H[r] = 0; E[r] = 0; }
+        int hl = 0, fl = 0;         // this lane's bottom row H, F at its last column
+        int up_prev = 0;            // H of the row above at column j-1 (diag of row 0)
+        int rc = kPadCode;          // residue code of this lane's current column
+        int in_res = kPadCode, in_bh = 0, in_bf = 0, out_h = 0, out_f = 0;
+        const int nsteps = L + kLanes - 1;
+        const uint8_t* lrow = lds + lane * RI;
+
+        for (int k0 = 0; k0 < nsteps; k0 += kLanes) {
+            // refill lane-0 conveyors for steps k0..k0+63 (column k = step)
+            {
+                const int col = k0 + lane;
+                in_res = col < L ? res[col] : kPadCode;
+                in_bh = (!first && col < L) ? bnd_h[col] : 0;
+                if (AFFINE) in_bf = (!first && col < L) ? bnd_f[col] : 0;
+            }
+            const int mend = min(kLanes, nsteps - k0);
+            for (int m = 0; m < mend; ++m) {
+                const int sres = __builtin_amdgcn_readlane(in_res, m);
+                const int sbh = __builtin_amdgcn_readlane(in_bh, m);
+                rc = shr1(sres, rc);
+                const int up0 = shr1(sbh, hl);
+                int f = 0;
+                if (AFFINE) {
+                    const int sbf = __builtin_amdgcn_readlane(in_bf, m);
+                    f = shr1(sbf, fl);
+                }
+                const uint8_t* pp = lrow + rc * S;
+                uint32_t pw[RI / 4];
+#pragma unroll
+                for (int q = 0; q < RI / 8; ++q) {
+                    const uint2 v = *reinterpret_cast<const uint2*>(pp + 8 * q);
+                    pw[2 * q] = v.x;
+                    pw[2 * q + 1] = v.y;
+                }
+                int up = up0;
+                int diag = up_prev;
+                up_prev = up0;
+                const uint32_t g = go;
+#pragma unroll
+                for (int r = 0; r < RI; ++r) {
+                    const int sc = sx8(pw[r >> 2], r & 3);
+                    int h;
+                    if (AFFINE) {
+                        const int e = max(usub(E[r], ge), usub(H[r], go));
+                        f = max(usub(f, ge), usub(up, go));
+                        h = max(max(e, f), diag + sc);
+                        E[r] = e;
+                    } else {
+                        h = usub(max(max(H[r], up), diag + sc), g);
+                    }
+                    diag = H[r];
+                    H[r] = h;
+                    up = h;
+                    best = max(best, h);
+                }
+                hl = up;
+                fl = f;
+                if (!last) {
+                    // lane 63 finished column k - 63: collect it for the next chunk
+                    const int k = k0 + m;
+                    const int oc = k - (kLanes - 1);
+                    if (oc >= 0) {
+                        const int slot = oc & (kLanes - 1);
+                        const bool mine = (lane == slot);
+                        const int vh = __builtin_amdgcn_readlane(hl, kLanes - 1);
+                        out_h = mine ? vh : out_h;
+                        if (AFFINE) {
+                            const int vf = __builtin_amdgcn_readlane(fl, kLanes - 1);
+                            out_f = mine ? vf : out_f;
+                        }
+                        if (slot == kLanes - 1 || oc == L - 1) {
+                            const int col = (oc & ~(kLanes - 1)) + lane;
+                            if (col <= oc) {
+                                bnd_h[col] = out_h;
+                                if (AFFINE) bnd_f[col] = out_f;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+    // wave max-reduction of best
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) best = max(best, __shfl_xor(best, off));
+    if (lane == 0) a.scores[a.subj_id[sid]] = best;
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+constexpr int kInterRowsLinear = 32;
+constexpr int kInterRowsAffine = 32;
+constexpr int kIntraRows = 8;
+constexpr int kInterSG = SW_INTER_SG;
+
+int inter_rows(bool affine) { return affine ? kInterRowsAffine : kInterRowsLinear; }
+int intra_rows_per_lane(bool) { return kIntraRows; }
+
+hipError_t launch_inter(const InterArgs& a, bool affine, hipStream_t s) {
+    if (a.nblocks <= 0 || a.qpad <= 0) return hipSuccess;
+    const dim3 grid((a.nblocks + kWavesPerWG - 1) / kWavesPerWG);
+    const dim3 block(kWavesPerWG * kLanes);
+    if (affine)
+        hipLaunchKernelGGL((sw_inter<kInterRowsAffine, kInterSG, true>), grid, block, 0, s, a);
+    else
+        hipLaunchKernelGGL((sw_inter<kInterRowsLinear, kInterSG, false>), grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_intra(const IntraArgs& a, bool affine, hipStream_t s) {
+    if (a.nsubj <= 0 || a.qpad <= 0) return hipSuccess;
+    if (affine)
+        hipLaunchKernelGGL((sw_intra<kIntraRows, true>), dim3(a.nsubj), dim3(kLanes), 0, s, a);
+    else
+        hipLaunchKernelGGL((sw_intra<kIntraRows, false>), dim3(a.nsubj), dim3(kLanes), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace swk

@@ -1,0 +1,69 @@
+"""Deterministic synthetic protein databases.
+
+Residues are i.i.d. from Swiss-Prot background amino-acid frequencies over
+the 20 standard residues; lengths are log-normal with median 290 and mean
+~360 (mu = ln 290, sigma = 0.657), clipped to [5, 35213] (the shortest and
+longest Swiss-Prot entries).  Everything is a function of (seed, shard), so
+any rank can regenerate any shard.  Data are synthetic: there is no network
+and Swiss-Prot itself is not shipped.
+"""
+import numpy as np
+
+# UniProtKB/Swiss-Prot amino-acid composition (percent), code order
+# A R N D C Q E G H I L K M F P S T W Y V  (codes 0..19)
+SWISSPROT_FREQ = np.array([8.25, 5.53, 4.06, 5.45, 1.37, 3.93, 6.75, 7.07, 2.27, 5.96,
+                           9.66, 5.84, 2.42, 3.86, 4.70, 6.56, 5.34, 1.08, 2.92, 6.87])
+LEN_MEDIAN = 290.0
+LEN_SIGMA = 0.657
+LEN_MIN, LEN_MAX = 5, 35213
+SEED = 1782
+
+_LUT = None
+
+
+def _lut():
+    """65536-entry table: uniform u16 -> residue code with the target mix."""
+    global _LUT
+    if _LUT is None:
+        p = SWISSPROT_FREQ / SWISSPROT_FREQ.sum()
+        edges = np.round(np.cumsum(p) * 65536).astype(np.int64)
+        edges[-1] = 65536
+        _LUT = np.searchsorted(edges, np.arange(65536), side="right").astype(np.uint8)
+    return _LUT
+
+
+def lengths(n, seed=SEED, shard=0, median=LEN_MEDIAN, sigma=LEN_SIGMA, lo=LEN_MIN, hi=LEN_MAX):
+    rng = np.random.Generator(np.random.PCG64([seed, shard, 1]))
+    L = np.exp(rng.normal(np.log(median), sigma, size=n))
+    return np.clip(np.rint(L), lo, hi).astype(np.int64)
+
+
+def residues(total, seed=SEED, shard=0, chunk=1 << 24):
+    rng = np.random.Generator(np.random.PCG64([seed, shard, 2]))
+    lut = _lut()
+    out = np.empty(total, dtype=np.uint8)
+    for k in range(0, total, chunk):
+        m = min(chunk, total - k)
+        out[k:k + m] = lut[rng.integers(0, 65536, size=m, dtype=np.uint16)]
+    return out
+
+
+def database(n, seed=SEED, shard=0, **len_kw):
+    """(residues uint8, offsets int64[n+1]) for a synthetic shard."""
+    L = lengths(n, seed, shard, **len_kw)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    offs[1:] = np.cumsum(L)
+    return residues(int(offs[-1]), seed, shard), offs
+
+
+def fixed_length_database(n, mean, sd, seed=SEED, shard=0, lo=1):
+    """Normal lengths N(mean, sd) (config C5: 2k-residue subjects)."""
+    rng = np.random.Generator(np.random.PCG64([seed, shard, 3]))
+    L = np.clip(np.rint(rng.normal(mean, sd, size=n)), lo, None).astype(np.int64)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    offs[1:] = np.cumsum(L)
+    return residues(int(offs[-1]), seed, shard), offs
+
+
+def query(length, seed=SEED, shard=99):
+    return residues(length, seed, shard)

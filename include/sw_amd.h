@@ -1,0 +1,166 @@
+/*
+ * sw_amd.h — C ABI of the MI355X Smith-Waterman database-scan library
+ * (libswamd.so).  Plain pointers and sizes only; no C++ or torch types.
+ *
+ * This is the boundary the reference's scan path crosses.  The reference has
+ * no FFI of its own: its one entry point is the C++ function
+ *
+ *     void smith_waterman_cuda(FASTAQuery&, FASTADatabase&,
+ *                              std::vector<seqid_score>&);     SWSolver.h:9
+ *
+ * implemented at SWSolver.cu:266-404, plus the (uncompilable) char variant
+ * SWSolver_char.h:9 / SWSolver_char.cu:193-280.  Those C++ signatures are
+ * kept unchanged in include/SWSolver.h and include/SWSolver_char.h; they are
+ * thin shims over the calls below.  Each call names the part of the
+ * reference it replaces.
+ *
+ * Conventions
+ *   - Residues are ENCODED bytes: codes 0..24 for A R N D C Q E G H I L K M F
+ *     P S T W Y V B J Z X * (SWSolver.cu:17-41); every other input byte is
+ *     '*' = 24 (convertStringToFloat, SWSolver.cu:91-120).  sw_encode()
+ *     performs that mapping.
+ *   - Scores are int32 (the reference's int16 storage overflows for the
+ *     self-hits of the longest shipped queries).
+ *   - Every call returns SW_OK (0) or a negative SW_E* code; a HIP failure
+ *     is returned as SW_E_HIP and its text is kept for sw_last_error().
+ *     Nothing fails silently (the reference checks no CUDA error,
+ *     SWSolver.cu:276).
+ *   - A handle is bound to one device and owns one HIP stream; calls on one
+ *     handle are not re-entrant (neither is the reference: it keeps its
+ *     query in __constant__ memory, SWSolver.cu:85-89).
+ */
+#ifndef SW_AMD_H
+#define SW_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SW_OK 0
+#define SW_E_INVALID -1   /* bad argument */
+#define SW_E_HIP -2       /* HIP runtime error (see sw_last_error) */
+#define SW_E_NOMEM -3     /* host allocation failed */
+#define SW_E_NODEVICE -4  /* no HIP device / kernel image for this GPU */
+
+#define SW_ALPHABET 25    /* residue codes 0..24 */
+#define SW_CODE_STAR 24
+
+/* Built-in substitution matrices (25x25 int8, code order). */
+#define SW_MATRIX_BLOSUM50_REF 0  /* SWSolver.cu:54-81 exactly ('*' = 0) */
+#define SW_MATRIX_BLOSUM62 1      /* NCBI BLOSUM62 (option, not in the reference) */
+#define SW_MATRIX_IDENTITY3 2     /* +3/-3, the cpu.cpp:6-8 scheme */
+
+typedef struct sw_scoring {
+    const int8_t* matrix;  /* 625 int8 (row = query code, col = subject code);
+                              NULL = SW_MATRIX_BLOSUM50_REF */
+    int32_t gap_open;      /* cost of the first residue of a gap (> 0) */
+    int32_t gap_extend;    /* cost of each further residue (> 0); equal to
+                              gap_open = the reference's linear gap
+                              (GAP_PENALTY 2, SWSolver.cu:7) */
+} sw_scoring;
+
+typedef struct sw_db_stats {
+    int64_t n_subjects;      /* records in the database */
+    int64_t residues;        /* sum of unpadded subject lengths */
+    int64_t packed_cells;    /* residue columns actually scanned (64 lanes x
+                                padded block widths) */
+    int64_t n_blocks;        /* 64-subject blocks scanned by the inter-sequence kernel */
+    int64_t n_long;          /* subjects routed to the intra-sequence kernel */
+    int64_t device_bytes;    /* HBM held by the packed database */
+    int32_t max_length;      /* longest subject */
+    int32_t long_threshold;  /* subjects longer than this use the intra kernel */
+} sw_db_stats;
+
+typedef struct sw_timing {
+    float inter_ms;     /* inter-sequence kernel(s), HIP events on the handle's stream */
+    float intra_ms;     /* intra-sequence kernel(s) */
+    float total_ms;     /* first launch to last completion of the last scan */
+    int32_t rescued;    /* subjects re-scored at int32 after an int16 saturation */
+    int32_t launches;   /* kernel launches in the last scan */
+} sw_timing;
+
+typedef struct sw_handle sw_handle;
+typedef struct sw_db sw_db;
+
+/* ---- housekeeping ---------------------------------------------------- */
+int32_t sw_version(void);                         /* 10000*major + 100*minor + patch */
+const char* sw_last_error(void);                  /* thread-local text of the last failure */
+int sw_encode(const char* ascii, int64_t n, uint8_t* codes);    /* SWSolver.cu:91-120 */
+int sw_builtin_matrix(int32_t id, int8_t* out625);               /* SWSolver.cu:54-81 */
+
+/* ---- device context ---------------------------------------------------
+ * Replaces the reference's implicit CUDA context + default stream
+ * (SWSolver.cu:282-288 allocations, :349/:381 synchronisations).        */
+int sw_create(int32_t device, sw_handle** out);
+int sw_destroy(sw_handle* h);
+/* The handle's HIP stream (hipStream_t), e.g. to record events on it. */
+void* sw_stream(sw_handle* h);
+/* Use an external stream (e.g. torch's current stream); NULL = own stream. */
+int sw_set_stream(sw_handle* h, void* hip_stream);
+
+/* ---- database -----------------------------------------------------------
+ * Replaces the per-call packing loop SWSolver.cu:301-371 (longest-first
+ * 32-lane interleave into managed memory, re-done on every query): the
+ * database is sorted, packed and uploaded ONCE and stays resident in HBM.
+ *   residues : encoded subject residues, concatenated
+ *   offsets  : n+1 offsets into residues (offsets[0] = 0)
+ *   ids      : n result ids (NULL = 0..n-1); sw_scan writes scores[id]   */
+int sw_db_create(sw_handle* h, const uint8_t* residues, const int64_t* offsets,
+                 int64_t n, const int32_t* ids, sw_db** out);
+int sw_db_free(sw_db* db);
+int sw_db_get_stats(const sw_db* db, sw_db_stats* out);
+/* Subjects longer than `threshold` go to the intra-sequence kernel
+ * (default chosen at sw_db_create; 0 = library default).  Must be called
+ * before the first scan. */
+int sw_db_set_long_threshold(sw_db* db, int32_t threshold);
+
+/* ---- scans ---------------------------------------------------------------
+ * Replaces smith_waterman_cuda (SWSolver.cu:266-404): score the encoded
+ * query against every subject; scores[id] = best local score.  The output
+ * array must hold max(id)+1 int32; slots no subject maps to are set to 0.
+ * Synchronous.                                                            */
+int sw_scan(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen,
+            const sw_scoring* sc, int32_t* scores_host);
+
+/* Same, asynchronous on the handle's stream, scores written to DEVICE memory
+ * (scores_dev; only slots that some subject maps to are written).  Used by
+ * bench.py with the database already resident.  The handle must outlive the
+ * database: sw_db_free uses the handle's stream.                          */
+int sw_scan_device(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen,
+                   const sw_scoring* sc, int32_t* scores_dev);
+
+/* Batch of nq queries (concatenated encoded residues, nq+1 offsets);
+ * scores_host is [nq][max(id)+1].  Consecutive queries overlap on the
+ * device (main.cpp handles one query per run).     */
+int sw_scan_batch(sw_handle* h, const sw_db* db, const uint8_t* queries,
+                  const int64_t* qoffsets, int32_t nq, const sw_scoring* sc,
+                  int32_t* scores_host);
+
+/* Timing of the most recent scan on this handle (waits for it). */
+int sw_get_timing(sw_handle* h, sw_timing* out);
+/* Kernel times summed over every scan since the last reset (waits for them);
+ * *nscans = number of scans summed.  Lets a caller time many back-to-back
+ * scans with HIP events on the stream they ran on, without synchronising
+ * between them (bench.py).                                               */
+int sw_timing_reset(sw_handle* h);
+int sw_timing_total(sw_handle* h, sw_timing* out, int32_t* nscans);
+
+/* ---- ranking ---------------------------------------------------------------
+ * Top-k of a score vector (score descending, id ascending on ties).
+ * Host-side helper for the multi-GPU top-K exchange.     */
+int sw_topk(const int32_t* scores, int64_t n, int32_t k, int32_t* out_ids,
+            int32_t* out_scores);
+
+/* ---- single pair ---------------------------------------------------------
+ * One query against one subject on the GPU (wavefront kernel); the GPU
+ * analogue of the cpu.cpp pair program's score (cpu.cpp:43-74).         */
+int sw_score_pair(sw_handle* h, const uint8_t* query, int32_t qlen,
+                  const uint8_t* subject, int32_t slen, const sw_scoring* sc,
+                  int32_t* score);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SW_AMD_H */

@@ -1,0 +1,44 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+for p in (REPO, os.path.join(REPO, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP library)")
+
+
+@pytest.fixture(scope="session")
+def sw():
+    import _swpkg
+    return _swpkg.load()
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import sw_oracle
+    sw_oracle.lib()
+    return sw_oracle
+
+
+@pytest.fixture(scope="session")
+def handle(sw):
+    h = sw.Handle(0)
+    yield h
+    h.close()
+
+
+def read_query(name):
+    with open(os.path.join(GOLDEN, "queries", name + ".fasta")) as f:
+        return "".join(f.read().split("\n")[1:])
+
+
+def read_golden(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return [int(x) for x in f.read().split()]

@@ -1,0 +1,130 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden
+scores and against the CPU oracle, bit-exact (integer DP)."""
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, read_golden, read_query
+
+pytestmark = pytest.mark.gpu
+
+QUERIES = ["P02232", "P05013", "P14942", "P07327", "P01008", "P03435", "P42357", "P21177",
+           "Q38941", "P27895", "P07756", "P04775", "P19096", "P28167", "P0C6B8", "P20930",
+           "P08519", "Q7TMA5", "P33450", "Q9UKN1"]
+
+
+def subset(oracle):
+    recs = oracle.read_fasta_records(GOLDEN + "/subset111.fasta")
+    seqs = [s for _, s in recs]
+    res = np.concatenate([oracle.encode(s) for s in seqs])
+    offs = np.zeros(len(seqs) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(s) for s in seqs])
+    return res, offs
+
+
+@pytest.mark.parametrize("qname", ["P01008", "P02232"])
+@pytest.mark.parametrize("long_threshold", [None, 300, 1])
+def test_golden_subset111(sw, oracle, handle, qname, long_threshold):
+    """Swissprot records 0..110 vs test/reference/<q>.txt lines 0..110."""
+    res, offs = subset(oracle)
+    db = sw.Database(handle, res, offs, long_threshold=long_threshold)
+    got = db.scan(sw.encode(read_query(qname)))
+    want = np.array(read_golden(qname + ".subset111.scores"), dtype=np.int32)
+    assert np.array_equal(got, want), np.nonzero(got != want)
+
+
+@pytest.mark.parametrize("qname", QUERIES)
+def test_all_shipped_queries_vs_oracle(sw, oracle, handle, qname):
+    """Every data/queries FASTA (144..5478 aa: no 1024 cap) on the subset."""
+    res, offs = subset(oracle)
+    db = sw.Database(handle, res, offs)
+    q = sw.encode(read_query(qname))
+    got = db.scan(q)
+    want = oracle.scan(q, res, offs)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("n,qlen,thr", [(1000, 144, None), (777, 375, None), (300, 1100, None),
+                                        (130, 33, 200), (257, 600, 500), (64, 2100, 64)])
+def test_synthetic_vs_oracle(sw, oracle, handle, n, qlen, thr):
+    r, o = sw.synth.database(n, shard=n)
+    q = sw.synth.query(qlen, shard=qlen)
+    db = sw.Database(handle, r, o, long_threshold=thr)
+    got = db.scan(q)
+    want = oracle.scan(q, r, o)
+    assert np.array_equal(got, want), (np.nonzero(got != want)[0][:10], got[:5], want[:5])
+
+
+@pytest.mark.parametrize("go,ge", [(10, 1), (11, 1), (5, 2), (3, 3)])
+@pytest.mark.parametrize("mid", [0, 1])
+def test_affine_vs_oracle(sw, oracle, handle, go, ge, mid):
+    r, o = sw.synth.database(400, shard=7)
+    q = sw.synth.query(250, shard=8)
+    mat = oracle.matrix(mid)
+    db = sw.Database(handle, r, o)
+    got = db.scan(q, matrix=mat, gap_open=go, gap_extend=ge)
+    want = oracle.scan(q, r, o, mat=mat, gap_open=go, gap_extend=ge)
+    assert np.array_equal(got, want)
+    db.set_long_threshold(100)
+    got2 = db.scan(q, matrix=mat, gap_open=go, gap_extend=ge)
+    assert np.array_equal(got2, want)
+
+
+def test_edge_cases(sw, oracle, handle):
+    """Empty and ragged subjects, an empty query, custom ids."""
+    seqs = ["", "A", "W", "WW", "", "ACDEFGHIKLMNPQRSTVWY" * 7, "X*UO/", "M" * 17]
+    res = np.concatenate([oracle.encode(s) for s in seqs if s] or [np.zeros(0, np.uint8)])
+    offs = np.zeros(len(seqs) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(s) for s in seqs])
+    ids = np.array([5, 0, 3, 9, 1, 2, 4, 7], dtype=np.int32)
+    db = sw.Database(handle, res, offs, ids=ids)
+    q = sw.encode("MKWVTFISLLFLFSSAYSW")
+    got = db.scan(q)
+    want_k = oracle.scan(q, res, offs)
+    want = np.zeros(10, dtype=np.int32)
+    want[ids] = want_k
+    assert np.array_equal(got, want)
+    assert np.all(db.scan(np.zeros(0, np.uint8)) == 0)
+    db.set_long_threshold(1)
+    assert np.array_equal(db.scan(q), want)
+
+
+def test_identity_matrix_vs_cpu_cpp_pairs(sw, oracle, handle):
+    """cpu.cpp's own +3/-3 scheme: GPU pair scores = maxima cpu.cpp printed."""
+    import json
+    pairs = json.load(open(GOLDEN + "/cpu_pairs.json"))["pairs"]
+    mat = sw.builtin_matrix(sw.MATRIX_IDENTITY3)
+    for p in pairs:
+        got = handle.score_pair(sw.encode(p["a"]), sw.encode(p["b"]), matrix=mat)
+        assert got == p["max"], p
+
+
+def test_batch_and_solver_api(sw, oracle, handle, tmp_path):
+    res, offs = subset(oracle)
+    db = sw.Database(handle, res, offs)
+    qs = [sw.encode(read_query(n)) for n in ("P02232", "P01008", "P07327")]
+    out = db.scan_batch(qs)
+    for k, q in enumerate(qs):
+        assert np.array_equal(out[k], oracle.scan(q, res, offs))
+    # the reference's interface: (id, score) appended in descending padded length
+    query = sw.FASTAQuery(GOLDEN + "/queries/P01008.fasta", True)
+    fdb = sw.FASTADatabase(GOLDEN + "/subset111.fasta")
+    result = []
+    sw.smith_waterman_cuda(query, fdb, result)
+    golden = read_golden("P01008.subset111.scores")
+    assert len(result) == 111
+    assert all(score == golden[i] for i, score in result)
+    lens = [len(s) for i, s in sorted(fdb.records())]
+    order = [lens[i] for i, _ in result]
+    assert order == sorted(order, reverse=True)
+    chars = sw.smith_waterman_cuda_char(query, fdb)
+    assert [s for _, s in chars] == golden
+
+
+def test_long_query_self_hit_int32(sw, oracle, handle):
+    """Q9UKN1 (5478 aa) against itself: > int16 range."""
+    q = sw.encode(read_query("Q9UKN1"))
+    offs = np.array([0, len(q)], dtype=np.int64)
+    db = sw.Database(handle, q, offs)
+    got = int(db.scan(q)[0])
+    want = int(oracle.scan(q, q, offs)[0])
+    assert got == want and got > 32767
