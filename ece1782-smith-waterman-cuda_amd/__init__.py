@@ -8,7 +8,7 @@ Python face.  There is no CPU fallback: if the library is missing, calls raise.
 Load with `import sw_amd` after `_swpkg.load()` (the directory name carries
 hyphens, so it is registered under the module name `sw_amd`).
 """
-from . import capi, fasta, solver, synth  # noqa: F401
+from . import capi, dist, fasta, solver, synth  # noqa: F401
 from .capi import Database, Handle, SWError, builtin_matrix, encode, topk  # noqa: F401
 from .fasta import FASTADatabase, FASTAQuery, SubjectSequence  # noqa: F401
 from .solver import smith_waterman_cuda, smith_waterman_cuda_char  # noqa: F401

@@ -85,13 +85,14 @@ def encode(seq):
     return out
 
 
-def score(q, s, mat=None, gap_open=2, gap_extend=2):
-    """One pair, encoded inputs."""
+def score(q, s, mat=None, gap_open=2, gap_extend=2, force_affine=False):
+    """One pair, encoded inputs (go == ge uses the linear recurrence unless
+    force_affine)."""
     mat = matrix() if mat is None else mat
     q, qp = _u8(q)
     s, sp = _u8(s)
     m, mp = _mat_ptr(mat)
-    if gap_open == gap_extend:
+    if gap_open == gap_extend and not force_affine:
         return lib().swo_score_linear(qp, len(q), sp, len(s), mp, gap_open)
     return lib().swo_score_affine(qp, len(q), sp, len(s), mp, gap_open, gap_extend)
 

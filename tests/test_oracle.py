@@ -1,0 +1,116 @@
+"""CPU: the oracle itself, pinned to the reference's own golden data."""
+import json
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, read_golden, read_query
+
+
+def subset(oracle):
+    recs = oracle.read_fasta_records(GOLDEN + "/subset111.fasta")
+    seqs = [s for _, s in recs]
+    res = np.concatenate([oracle.encode(s) for s in seqs])
+    offs = np.zeros(len(seqs) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(s) for s in seqs])
+    return res, offs
+
+
+@pytest.mark.parametrize("qname", ["P01008", "P02232"])
+def test_oracle_matches_reference_golden(oracle, qname):
+    """test/reference/<q>.txt lines 0..110 = the 111 records of uniprot_subset.dat."""
+    res, offs = subset(oracle)
+    got = oracle.scan(oracle.encode(read_query(qname)), res, offs)
+    assert got.tolist() == read_golden(qname + ".subset111.scores")
+
+
+def test_golden_full_files_consistent():
+    """The full golden files: 559,228 scores; their first 111 are the subset
+    fixtures; maxima are the self-hits."""
+    import gzip
+    for q, mx in (("P01008", 3037), ("P02232", 910)):
+        with gzip.open(GOLDEN + "/%s.full.txt.gz" % q, "rt") as f:
+            vals = [int(x) for x in f.read().split()]
+        assert len(vals) == 559228
+        assert vals[:111] == read_golden(q + ".subset111.scores")
+        assert max(vals) == mx
+
+
+def test_oracle_matches_cpu_cpp(oracle):
+    """Maxima printed by the reference's own cpu.cpp (oracle/_ref/cpu_ref)."""
+    pairs = json.load(open(GOLDEN + "/cpu_pairs.json"))["pairs"]
+    assert len(pairs) >= 40
+    for p in pairs:
+        assert oracle.score_raw_identity(p["a"], p["b"]) == p["max"], p
+        # the same scheme through the encoded path + identity matrix
+        m = oracle.matrix(oracle.MATRIX_IDENTITY3)
+        assert oracle.score(oracle.encode(p["a"]), oracle.encode(p["b"]), m) == p["max"]
+
+
+def _render(a, b, al):
+    """Alignment rows as cpu.cpp prints them (cpu.cpp:80-108)."""
+    i, j = al["q_begin"] - 1, al["s_begin"] - 1
+    ra, rb = [], []
+    for op in al["ops"]:
+        if op == "M":
+            ra.append(a[i]); rb.append(b[j]); i += 1; j += 1
+        elif op == "I":
+            ra.append(a[i]); rb.append("-"); i += 1
+        else:
+            ra.append("-"); rb.append(b[j]); j += 1
+    return "".join(ra), "".join(rb)
+
+
+def test_traceback_matches_cpu_cpp(oracle):
+    """Traceback tie rules of cpu.cpp:47-70 reproduce its printed alignments."""
+    pairs = json.load(open(GOLDEN + "/cpu_pairs.json"))["pairs"]
+    m = oracle.matrix(oracle.MATRIX_IDENTITY3)
+    for p in pairs:
+        al = oracle.align(oracle.encode(p["a"]), oracle.encode(p["b"]), m)
+        assert al["score"] == p["max"]
+        assert _render(p["a"], p["b"], al) == (p["aln_a"], p["aln_b"]), p
+
+
+def test_python_restatement_agrees(oracle):
+    rng = np.random.default_rng(5)
+    for mid in (0, 1, 2):
+        mat = oracle.matrix(mid)
+        for _ in range(20):
+            q = rng.integers(0, 25, size=rng.integers(1, 40)).astype(np.uint8)
+            s = rng.integers(0, 25, size=rng.integers(1, 40)).astype(np.uint8)
+            assert oracle.score(q, s, mat) == oracle.score_linear_py(q, s, mat, 2)
+
+
+def test_affine_reduces_to_linear(oracle):
+    """Gotoh with open == extend == g is the reference's linear gap g."""
+    rng = np.random.default_rng(6)
+    m = oracle.matrix()
+    for _ in range(30):
+        q = rng.integers(0, 25, size=rng.integers(1, 60)).astype(np.uint8)
+        s = rng.integers(0, 25, size=rng.integers(1, 60)).astype(np.uint8)
+        for g in (1, 2, 5):
+            assert oracle.score(q, s, m, g, g) == oracle.score(q, s, m, g, g, force_affine=True)
+
+
+def test_matrices(oracle):
+    b50 = oracle.matrix(0)
+    assert (b50 == b50.T).all() and b50.max() == 15 and b50.min() == -5
+    assert (b50[24] == 0).all() and (b50[:, 24] == 0).all()   # SWSolver.cu:80
+    assert (b50[23, :24] == -1).all()                          # X row
+    b62 = oracle.matrix(1)
+    assert (b62 == b62.T).all() and b62[17, 17] == 11
+
+
+def test_encoding(oracle):
+    codes = oracle.encode("ARNDCQEGHILKMFPSTWYVBJZX")
+    assert codes.tolist() == list(range(24))
+    assert oracle.encode("UOarnd/\r*").tolist() == [24] * 9   # SWSolver.cu:119
+
+
+def test_edge_cases(oracle):
+    m = oracle.matrix()
+    e = np.zeros(0, np.uint8)
+    assert oracle.score(e, oracle.encode("AAA"), m) == 0
+    assert oracle.score(oracle.encode("W"), oracle.encode("W"), m) == 15
+    out = oracle.scan(oracle.encode("WW"), e, np.zeros(3, np.int64))
+    assert out.tolist() == [0, 0]
