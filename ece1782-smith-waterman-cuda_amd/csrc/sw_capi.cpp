@@ -160,12 +160,19 @@ struct sw_handle {
     std::vector<ScanEvents> evpool;
     size_t nscans = 0;
     hipEvent_t* ev = nullptr;  // event set of the current scan
-    // per-query workspace
+    // The intra kernel runs on a side stream, concurrently with the inter
+    // kernel (fork/join through ev[0] and ev[1]).
+    hipStream_t side = nullptr;
+    // per-query workspace: profiles (inter: [32][stride]; intra: lane-slotted
+    // chunks) built in pinned host buffers, copied once per query
     int8_t* d_prof = nullptr;
     size_t prof_cap = 0;
+    int8_t* h_prof = nullptr;
+    size_t h_prof_cap = 0;
+    hipEvent_t prof_copied = nullptr;  // the staging buffer may be rewritten after this
+    bool prof_pending = false;
     int32_t* d_scores = nullptr;  // for the synchronous sw_scan
     size_t scores_cap = 0;
-    std::vector<int8_t> h_prof;
     bool timed = false;
     bool had_intra = false;
     int launches = 0;
@@ -190,6 +197,7 @@ struct sw_db {
     int32_t* d_bnd_f = nullptr;
     // intra part (long subjects)
     int64_t nlong = 0;
+    int32_t long_max = 0;
     uint8_t* d_lres = nullptr;
     size_t lres_bytes = 0;
     uint64_t* d_loff = nullptr;
@@ -207,7 +215,18 @@ struct sw_db {
 
 namespace {
 
-constexpr int32_t kDefaultLongThreshold = 3072;
+// Subjects longer than this go to the wavefront kernel.  A 64-lane block of
+// the inter kernel takes time proportional to its longest subject, so very
+// long subjects would become the kernel's critical path; measured on the C2
+// workload (mean length 360): 1536 beats 3072 by 1.3x and 1024 by 1.03x
+// (profiles/r01_tune_inter.jsonl).  Default: 4.25 x mean length, clamped.
+
+int32_t default_long_threshold(const sw_db* db) {
+    if (db->n == 0) return 1536;
+    const double mean = static_cast<double>(db->residues) / static_cast<double>(db->n);
+    const double t = 4.25 * mean;
+    return static_cast<int32_t>(std::min(8192.0, std::max(1024.0, t)));
+}
 
 void free_dev(sw_db* db) {
     void* ptrs[] = {db->d_res, db->d_blk_off, db->d_blk_groups, db->d_lane_ids, db->d_bnd_h, db->d_bnd_f,
@@ -304,6 +323,7 @@ int build_db(sw_db* db) {
     db->lres_bytes = ltotal;
     db->nblocks = nblocks;
     db->nlong = nlong;
+    db->long_max = nlong ? static_cast<int32_t>(len(order[0])) : 0;
     db->packed_cells = static_cast<int64_t>(total);  // one byte per scanned (lane, column)
     db->device_bytes = acc;
     db->built = true;
@@ -348,27 +368,67 @@ int check_scoring(const sw_scoring* sc, const int8_t** mat, int* go, int* ge) {
     return SW_OK;
 }
 
-// Query profile: prof[c][i] = S[q_i][c] (+ gap for the linear kernels) for
-// residue codes c < 25; rows c >= 25 (the pad code) and columns i >= qlen
-// score 0 (+ gap).  A zero-score pad row/column can never raise the maximum
-// (every such cell is <= max(0, its diagonal, its gap predecessors)).
-int build_profile(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* mat, int go, bool affine,
-                  int32_t stride) {
-    const int bias = affine ? 0 : go;
-    h->h_prof.assign(static_cast<size_t>(swk::kProfileRows) * stride, static_cast<int8_t>(bias));
-    for (int32_t i = 0; i < qlen; ++i) {
+// Query profiles.  Inter kernel: prof[c][i] = S[q_i][c] (+ gap for the
+// linear kernels) for residue codes c < 25; rows c >= 25 (the pad code) and
+// columns i >= qlen score 0 (+ gap).  A zero-score pad row/column can never
+// raise the maximum (every such cell is <= max(0, its diagonal, its gap
+// predecessors)).  Intra kernel: the same values laid out per chunk of
+// 64*ri query rows as [code][lane][RIP] so each lane's ri rows are contiguous.
+struct Profiles {
+    int32_t stride = 0;      // inter: bytes per code row
+    size_t inter_bytes = 0;
+    size_t intra_off = 0;    // byte offset of the intra profile in the buffer
+    size_t total = 0;
+};
+
+int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* mat, int go, bool affine,
+                   int32_t qpad_inter, int ri, int32_t qpad_intra, Profiles* P) {
+    for (int32_t i = 0; i < qlen; ++i)
         if (q[i] >= SW_ALPHABET) return fail(SW_E_INVALID, "query residue code out of range (use sw_encode)");
-        const int8_t* row = mat + 25 * q[i];
-        for (int c = 0; c < SW_ALPHABET; ++c)
-            h->h_prof[static_cast<size_t>(c) * stride + i] = static_cast<int8_t>(row[c] + bias);
+    const int bias = affine ? 0 : go;
+    P->stride = static_cast<int32_t>(round_up(std::max<int32_t>(qpad_inter, 16), 16));
+    P->inter_bytes = static_cast<size_t>(swk::kProfileRows) * P->stride;
+    P->intra_off = round_up(static_cast<int64_t>(P->inter_bytes), 256);
+    const int rip = swk::intra_rip(ri);
+    const size_t intra_bytes = ri ? static_cast<size_t>(qpad_intra / (swk::kLanes * ri)) * swk::intra_chunk_bytes(ri) : 0;
+    P->total = P->intra_off + intra_bytes;
+    if (P->total > h->h_prof_cap) {
+        if (h->prof_pending) HIPCHECK(hipEventSynchronize(h->prof_copied));
+        h->prof_pending = false;
+        if (h->h_prof) HIPCHECK(hipHostFree(h->h_prof));
+        h->h_prof_cap = std::max<size_t>(P->total, 1 << 16);
+        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h->h_prof), h->h_prof_cap, hipHostMallocDefault));
     }
-    const size_t bytes = h->h_prof.size();
-    if (bytes > h->prof_cap) {
-        if (h->d_prof) HIPCHECK(hipFree(h->d_prof));
-        h->prof_cap = std::max<size_t>(bytes, 1 << 16);
+    if (P->total > h->prof_cap) {
+        if (h->d_prof) {
+            HIPCHECK(hipStreamSynchronize(h->stream));
+            HIPCHECK(hipFree(h->d_prof));
+        }
+        h->prof_cap = std::max<size_t>(P->total, 1 << 16);
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&h->d_prof), h->prof_cap));
     }
-    HIPCHECK(hipMemcpyAsync(h->d_prof, h->h_prof.data(), bytes, hipMemcpyHostToDevice, h->stream));
+    if (h->prof_pending) HIPCHECK(hipEventSynchronize(h->prof_copied));  // previous copy consumed the buffer
+    int8_t* hp = h->h_prof;
+    auto value = [&](int c, int64_t row) -> int8_t {
+        if (c >= SW_ALPHABET || row >= qlen) return static_cast<int8_t>(bias);
+        return static_cast<int8_t>(mat[25 * q[row] + c] + bias);
+    };
+    for (int c = 0; c < swk::kProfileRows; ++c)
+        for (int32_t i = 0; i < P->stride; ++i) hp[static_cast<size_t>(c) * P->stride + i] = value(c, i);
+    if (ri) {
+        const int64_t CH = static_cast<int64_t>(swk::kLanes) * ri;
+        int8_t* ip = hp + P->intra_off;
+        const int64_t nch = qpad_intra / CH;
+        for (int64_t ch = 0; ch < nch; ++ch)
+            for (int c = 0; c < swk::kProfileRows; ++c)
+                for (int t = 0; t < swk::kLanes; ++t) {
+                    int8_t* d = ip + ((ch * swk::kProfileRows + c) * swk::kLanes + t) * rip;
+                    for (int r = 0; r < rip; ++r) d[r] = r < ri ? value(c, ch * CH + t * ri + r) : 0;
+                }
+    }
+    HIPCHECK(hipMemcpyAsync(h->d_prof, hp, P->total, hipMemcpyHostToDevice, h->stream));
+    HIPCHECK(hipEventRecord(h->prof_copied, h->stream));
+    h->prof_pending = true;
     return SW_OK;
 }
 
@@ -400,10 +460,9 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     if ((rc = next_events(h))) return rc;
 
     const int R = swk::inter_rows(affine);
-    const int CH = swk::kLanes * swk::intra_rows_per_lane(affine);
     const int32_t qpad_inter = static_cast<int32_t>(round_up(qlen, R));
-    const int32_t qpad_intra = static_cast<int32_t>(round_up(qlen, CH));
-    const int32_t stride = static_cast<int32_t>(round_up(std::max<int32_t>({qpad_inter, qpad_intra, 16}), 16));
+    const int ri = db->nlong ? swk::intra_rows_for(qlen, db->long_max) : 0;
+    const int32_t qpad_intra = ri ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri)) : 0;
     // Empty query: every score is 0 (the reference's kernel leaves maxScore 0).
     if (qlen == 0) {
         HIPCHECK(hipEventRecord(h->ev[0], h->stream));
@@ -415,32 +474,34 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         h->timed = true;
         return SW_OK;
     }
-    if ((rc = build_profile(h, query, qlen, mat, go, affine, stride))) return rc;
+    Profiles P;
+    if ((rc = build_profiles(h, query, qlen, mat, go, affine, qpad_inter, ri, qpad_intra, &P))) return rc;
     const bool multi_inter = qpad_inter > R;
-    const bool multi_intra = qpad_intra > CH;
-    if ((multi_inter || multi_intra || db->nlong) && (rc = ensure_bnd(db, affine))) return rc;
+    const bool multi_intra = ri && qpad_intra > swk::kLanes * ri;
+    if ((multi_inter || multi_intra) && (rc = ensure_bnd(db, affine))) return rc;
 
+    // fork: the side stream starts when the main stream reaches ev[0]
     HIPCHECK(hipEventRecord(h->ev[0], h->stream));
     if (db->nlong) {
+        HIPCHECK(hipStreamWaitEvent(h->side, h->ev[0], 0));
         swk::IntraArgs ia{};
         ia.residues = db->d_lres;
         ia.subj_off = db->d_loff;
         ia.subj_len = db->d_llen;
         ia.subj_id = db->d_lid;
         ia.nsubj = static_cast<int32_t>(db->nlong);
-        ia.prof = h->d_prof;
-        ia.prof_stride = stride;
+        ia.prof = h->d_prof + P.intra_off;
         ia.qpad = qpad_intra;
         ia.gap_open = go;
         ia.gap_extend = ge;
         ia.bnd_h = db->d_lbnd_h;
         ia.bnd_f = db->d_lbnd_f;
         ia.scores = scores_dev;
-        HIPCHECK(swk::launch_intra(ia, affine, h->stream));
+        HIPCHECK(swk::launch_intra(ia, ri, affine, h->side));
         ++h->launches;
         h->had_intra = true;
     }
-    HIPCHECK(hipEventRecord(h->ev[1], h->stream));
+    HIPCHECK(hipEventRecord(h->ev[1], db->nlong ? h->side : h->stream));
     if (db->nblocks) {
         swk::InterArgs a{};
         a.residues = db->d_res;
@@ -449,7 +510,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         a.lane_ids = db->d_lane_ids;
         a.nblocks = static_cast<int32_t>(db->nblocks);
         a.prof = h->d_prof;
-        a.prof_stride = stride;
+        a.prof_stride = P.stride;
         a.qpad = qpad_inter;
         a.gap_open = go;
         a.gap_extend = ge;
@@ -460,6 +521,8 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         ++h->launches;
     }
     HIPCHECK(hipEventRecord(h->ev[2], h->stream));
+    // join
+    if (db->nlong) HIPCHECK(hipStreamWaitEvent(h->stream, h->ev[1], 0));
     HIPCHECK(hipEventRecord(h->ev[3], h->stream));
     h->evpool[h->nscans - 1].launches = h->launches;
     h->timed = true;
@@ -519,6 +582,9 @@ int sw_create(int32_t device, sw_handle** out) {
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete h; return fail(SW_E_HIP, hipGetErrorString(e)); }
     h->own_stream = true;
+    e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->prof_copied, hipEventDisableTiming);
+    if (e != hipSuccess) { delete h; return fail(SW_E_HIP, hipGetErrorString(e)); }
     *out = h;
     return SW_OK;
 }
@@ -530,8 +596,12 @@ int sw_destroy(sw_handle* h) {
     for (auto& se : h->evpool)
         for (auto& ev : se.ev)
             if (ev) (void)hipEventDestroy(ev);
+    if (h->side) (void)hipStreamSynchronize(h->side);
     if (h->d_prof) (void)hipFree(h->d_prof);
+    if (h->h_prof) (void)hipHostFree(h->h_prof);
+    if (h->prof_copied) (void)hipEventDestroy(h->prof_copied);
     if (h->d_scores) (void)hipFree(h->d_scores);
+    if (h->side) (void)hipStreamDestroy(h->side);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return SW_OK;
@@ -589,7 +659,7 @@ int sw_db_create(sw_handle* h, const uint8_t* residues, const int64_t* offsets, 
         if (db->h_ids[k] < 0) { delete db; return fail(SW_E_INVALID, "ids must be >= 0"); }
         db->max_id = std::max(db->max_id, db->h_ids[k]);
     }
-    db->long_threshold = kDefaultLongThreshold;
+    db->long_threshold = default_long_threshold(db);
     HIPCHECK(hipSetDevice(h->device));
     int rc = build_db(db);
     if (rc) { free_dev(db); delete db; return rc; }
@@ -601,6 +671,7 @@ int sw_db_free(sw_db* db) {
     if (!db) return SW_OK;
     (void)hipSetDevice(db->h->device);
     (void)hipStreamSynchronize(db->h->stream);
+    (void)hipStreamSynchronize(db->h->side);
     free_dev(db);
     delete db;
     return SW_OK;
@@ -622,10 +693,11 @@ int sw_db_get_stats(const sw_db* db, sw_db_stats* out) {
 int sw_db_set_long_threshold(sw_db* db, int32_t threshold) {
     if (!db) return fail(SW_E_INVALID, "null argument");
     if (threshold < 0) return fail(SW_E_INVALID, "threshold must be >= 0");
-    const int32_t t = threshold == 0 ? kDefaultLongThreshold : threshold;
+    const int32_t t = threshold == 0 ? default_long_threshold(db) : threshold;
     if (t == db->long_threshold && db->built) return SW_OK;
     HIPCHECK(hipSetDevice(db->h->device));
     HIPCHECK(hipStreamSynchronize(db->h->stream));
+    HIPCHECK(hipStreamSynchronize(db->h->side));
     free_dev(db);
     db->long_threshold = t;
     return build_db(db);
@@ -668,12 +740,14 @@ int sw_scan_batch(sw_handle* h, const sw_db* db, const uint8_t* queries, const i
 namespace {
 int read_events(const ScanEvents& se, sw_timing* t) {
     HIPCHECK(hipEventSynchronize(se.ev[3]));
-    float t01 = 0, t12 = 0, t03 = 0;
+    // intra runs on the side stream from the fork (ev0) to ev1; inter on the
+    // main stream from ev0 to ev2; they overlap.
+    float t01 = 0, t02 = 0, t03 = 0;
     HIPCHECK(hipEventElapsedTime(&t01, se.ev[0], se.ev[1]));
-    HIPCHECK(hipEventElapsedTime(&t12, se.ev[1], se.ev[2]));
+    HIPCHECK(hipEventElapsedTime(&t02, se.ev[0], se.ev[2]));
     HIPCHECK(hipEventElapsedTime(&t03, se.ev[0], se.ev[3]));
     t->intra_ms += t01;
-    t->inter_ms += t12;
+    t->inter_ms += t02;
     t->total_ms += t03;
     t->launches += se.launches;
     return SW_OK;

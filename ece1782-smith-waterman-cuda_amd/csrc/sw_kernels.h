@@ -48,8 +48,7 @@ struct IntraArgs {
     const int32_t* subj_len;
     const int32_t* subj_id;
     int32_t nsubj;
-    const int8_t* prof;          // [kProfileRows][prof_stride]
-    int32_t prof_stride;
+    const int8_t* prof;          // [chunk][kProfileRows][64 lanes][RIP] (host-built)
     int32_t qpad;                // multiple of 64 * rows-per-lane
     int32_t gap_open;
     int32_t gap_extend;
@@ -61,9 +60,13 @@ struct IntraArgs {
 // Strip heights (query rows held in registers per lane) the kernels are
 // instantiated for.
 int inter_rows(bool affine);
-int intra_rows_per_lane(bool affine);
+// Query rows per lane the intra kernel uses for this query (2..16, even).
+int intra_rows_for(int qlen, int longest);
+// Bytes of one intra profile chunk (64*ri query rows, 32 codes).
+int intra_chunk_bytes(int ri);
+__host__ __device__ constexpr int intra_rip(int RI) { return (RI + 3) / 4 * 4; }
 
 hipError_t launch_inter(const InterArgs& a, bool affine, hipStream_t s);
-hipError_t launch_intra(const IntraArgs& a, bool affine, hipStream_t s);
+hipError_t launch_intra(const IntraArgs& a, int ri, bool affine, hipStream_t s);
 
 }  // namespace swk

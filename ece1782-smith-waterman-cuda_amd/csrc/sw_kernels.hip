@@ -34,9 +34,8 @@
 // "- ge" step because ge > 0).
 #include "sw_kernels.h"
 
-#ifndef SW_INTER_SG
-#define SW_INTER_SG 16
-#endif
+#include <cstdio>
+#include <cstdlib>
 
 namespace swk {
 
@@ -287,13 +286,18 @@ __device__ __forceinline__ int shr1(int old, int src) {
     return __builtin_amdgcn_update_dpp(old, src, kDppWaveShr1, 0xf, 0xf, false);
 }
 
-__host__ __device__ constexpr int intra_stride(int RI) { return kLanes * RI + 8; }
+// Per-lane slot of RIP = RI rounded up to 4 bytes (intra_rip, sw_kernels.h);
+// the host lays the intra profile out as [chunk][code][lane][RIP] so staging
+// is a straight copy.
+// +4 bytes per code row: lanes reading different codes start on different banks
+__host__ __device__ constexpr int intra_stride(int RI) { return kLanes * intra_rip(RI) + 4; }
 
 template <int RI, bool AFFINE>
 __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
-    const int prof_stride = a.prof_stride;
     constexpr int CH = kLanes * RI;  // query rows per chunk
+    constexpr int RIP = intra_rip(RI);
     constexpr int S = intra_stride(RI);
+    constexpr int CHUNK_BYTES = kProfileRows * kLanes * RIP;  // one chunk of the host profile
     __shared__ __attribute__((aligned(16))) uint8_t lds[kProfileRows * S];
     const int lane = threadIdx.x;
     const int sid = blockIdx.x;
@@ -306,29 +310,32 @@ __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
     const uint32_t ge = static_cast<uint32_t>(a.gap_extend);
     int best = 0;
 
-    for (int c0 = 0; c0 < a.qpad; c0 += CH) {
+    for (int c0 = 0, ch = 0; c0 < a.qpad; c0 += CH, ++ch) {
         const bool first = (c0 == 0);
         const bool last = (c0 + CH >= a.qpad);
         __syncthreads();  // previous chunk's LDS reads are done
-        // stage profile rows [c0, c0+CH) for all 32 codes: 32*CH bytes
-        for (int t = lane; t < kProfileRows * (CH / 16); t += kLanes) {
-            const int c = t / (CH / 16);
-            const int k = t % (CH / 16);
-            const int4 v = *reinterpret_cast<const int4*>(a.prof + static_cast<size_t>(c) * prof_stride + c0 + 16 * k);
-            int* d = reinterpret_cast<int*>(lds + c * S + 16 * k);  // S is only 8-byte aligned
+        // stage this chunk's profile: [code][lane][RIP] -> rows of S bytes
+        const int8_t* src = a.prof + static_cast<size_t>(ch) * CHUNK_BYTES;
+        for (int t = lane; t < CHUNK_BYTES / 16; t += kLanes) {
+            const int c = t / (kLanes * RIP / 16);
+            const int k = t % (kLanes * RIP / 16);
+            const int4 v = *reinterpret_cast<const int4*>(src + 16 * t);
+            int* d = reinterpret_cast<int*>(lds + c * S + 16 * k);  // S is 4-byte aligned only
             d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
         }
         __syncthreads();
 
-        int H[RI], E[RI];
+        int H[RI], E[AFFINE ? RI : 1];
 #pragma unroll
-        for (int r = 0; r < RI; ++r) { H[r] = 0; E[r] = 0; }
+        for (int r = 0; r < RI; ++r) H[r] = 0;
+#pragma unroll
+        for (int r = 0; r < (AFFINE ? RI : 1); ++r) E[r] = 0;
         int hl = 0, fl = 0;         // this lane's bottom row H, F at its last column
         int up_prev = 0;            // H of the row above at column j-1 (diag of row 0)
         int rc = kPadCode;          // residue code of this lane's current column
         int in_res = kPadCode, in_bh = 0, in_bf = 0, out_h = 0, out_f = 0;
         const int nsteps = L + kLanes - 1;
-        const uint8_t* lrow = lds + lane * RI;
+        const uint8_t* lrow = lds + lane * RIP;
 
         for (int k0 = 0; k0 < nsteps; k0 += kLanes) {
             // refill lane-0 conveyors for steps k0..k0+63 (column k = step)
@@ -349,18 +356,13 @@ __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
                     const int sbf = __builtin_amdgcn_readlane(in_bf, m);
                     f = shr1(sbf, fl);
                 }
-                const uint8_t* pp = lrow + rc * S;
-                uint32_t pw[RI / 4];
+                const uint32_t* pp = reinterpret_cast<const uint32_t*>(lrow + rc * S);
+                uint32_t pw[RIP / 4];
 #pragma unroll
-                for (int q = 0; q < RI / 8; ++q) {
-                    const uint2 v = *reinterpret_cast<const uint2*>(pp + 8 * q);
-                    pw[2 * q] = v.x;
-                    pw[2 * q + 1] = v.y;
-                }
+                for (int q = 0; q < RIP / 4; ++q) pw[q] = pp[q];
                 int up = up0;
                 int diag = up_prev;
                 up_prev = up0;
-                const uint32_t g = go;
 #pragma unroll
                 for (int r = 0; r < RI; ++r) {
                     const int sc = sx8(pw[r >> 2], r & 3);
@@ -371,7 +373,7 @@ __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
                         h = max(max(e, f), diag + sc);
                         E[r] = e;
                     } else {
-                        h = usub(max(max(H[r], up), diag + sc), g);
+                        h = usub(max(max(H[r], up), diag + sc), go);
                     }
                     diag = H[r];
                     H[r] = h;
@@ -414,31 +416,84 @@ __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-constexpr int kInterRowsLinear = 32;
-constexpr int kInterRowsAffine = 32;
-constexpr int kIntraRows = 8;
-constexpr int kInterSG = SW_INTER_SG;
+// Inter-kernel shape: R query rows per strip x SG columns per software-
+// pipelined sub-group.  SW_INTER_VARIANT="RxSG" overrides (tuning only).
+struct InterShape { int R, SG; };
+static InterShape inter_shape(bool affine) {
+    // measured on MI355X (scripts/tune_inter.py, profiles/r01_tune_inter.jsonl):
+    // 64x8 is fastest for the linear kernel (170 VGPRs, 2 waves/SIMD, half
+    // the boundary traffic of 32-row strips); affine keeps 32x8.
+    InterShape v = affine ? InterShape{32, 8} : InterShape{64, 8};
+    if (const char* e = std::getenv("SW_INTER_VARIANT")) {
+        int r = 0, g = 0;
+        if (std::sscanf(e, "%dx%d", &r, &g) == 2 &&
+            ((r == 32 && (g == 8 || g == 16)) || (r == 48 && g == 8) || (r == 64 && g == 8) || (r == 16 && g == 16)))
+            v = InterShape{r, g};
+    }
+    return v;
+}
 
-int inter_rows(bool affine) { return affine ? kInterRowsAffine : kInterRowsLinear; }
-int intra_rows_per_lane(bool) { return kIntraRows; }
+int inter_rows(bool affine) { return inter_shape(affine).R; }
+
+// Rows per lane for the intra kernel: minimise
+//   chunks * (steps per chunk) * (ops per step)
+// with ops per step ~ RI * 3.7 (cells) + 8 (hand-off overhead); RI is even
+// and at most 16 (register budget).
+int intra_rows_for(int qlen, int longest) {
+    int best_ri = 16;
+    double best_cost = 1e300;
+    for (int ri = 2; ri <= 16; ri += 2) {
+        const int chunk = kLanes * ri;
+        const int nch = (qlen + chunk - 1) / chunk;
+        const double cost = static_cast<double>(nch) * (longest + kLanes - 1) * (ri * 3.7 + 8.0);
+        if (cost < best_cost) { best_cost = cost; best_ri = ri; }
+    }
+    return best_ri;
+}
+
+int intra_chunk_bytes(int ri) { return kProfileRows * kLanes * intra_rip(ri); }
 
 hipError_t launch_inter(const InterArgs& a, bool affine, hipStream_t s) {
     if (a.nblocks <= 0 || a.qpad <= 0) return hipSuccess;
     const dim3 grid((a.nblocks + kWavesPerWG - 1) / kWavesPerWG);
     const dim3 block(kWavesPerWG * kLanes);
-    if (affine)
-        hipLaunchKernelGGL((sw_inter<kInterRowsAffine, kInterSG, true>), grid, block, 0, s, a);
-    else
-        hipLaunchKernelGGL((sw_inter<kInterRowsLinear, kInterSG, false>), grid, block, 0, s, a);
-    return hipGetLastError();
+    const InterShape v = inter_shape(affine);
+#define SW_LAUNCH_INTER(R_, SG_)                                                             \
+    if (v.R == R_ && v.SG == SG_) {                                                          \
+        if (affine) hipLaunchKernelGGL((sw_inter<R_, SG_, true>), grid, block, 0, s, a);     \
+        else hipLaunchKernelGGL((sw_inter<R_, SG_, false>), grid, block, 0, s, a);           \
+        return hipGetLastError();                                                            \
+    }
+    SW_LAUNCH_INTER(32, 8)
+    SW_LAUNCH_INTER(32, 16)
+    SW_LAUNCH_INTER(48, 8)
+    SW_LAUNCH_INTER(64, 8)
+    SW_LAUNCH_INTER(16, 16)
+#undef SW_LAUNCH_INTER
+    return hipErrorInvalidValue;
 }
 
-hipError_t launch_intra(const IntraArgs& a, bool affine, hipStream_t s) {
-    if (a.nsubj <= 0 || a.qpad <= 0) return hipSuccess;
+template <int RI>
+static void launch_intra_ri(const IntraArgs& a, bool affine, hipStream_t s) {
     if (affine)
-        hipLaunchKernelGGL((sw_intra<kIntraRows, true>), dim3(a.nsubj), dim3(kLanes), 0, s, a);
+        hipLaunchKernelGGL((sw_intra<RI, true>), dim3(a.nsubj), dim3(kLanes), 0, s, a);
     else
-        hipLaunchKernelGGL((sw_intra<kIntraRows, false>), dim3(a.nsubj), dim3(kLanes), 0, s, a);
+        hipLaunchKernelGGL((sw_intra<RI, false>), dim3(a.nsubj), dim3(kLanes), 0, s, a);
+}
+
+hipError_t launch_intra(const IntraArgs& a, int ri, bool affine, hipStream_t s) {
+    if (a.nsubj <= 0 || a.qpad <= 0) return hipSuccess;
+    switch (ri) {
+        case 2: launch_intra_ri<2>(a, affine, s); break;
+        case 4: launch_intra_ri<4>(a, affine, s); break;
+        case 6: launch_intra_ri<6>(a, affine, s); break;
+        case 8: launch_intra_ri<8>(a, affine, s); break;
+        case 10: launch_intra_ri<10>(a, affine, s); break;
+        case 12: launch_intra_ri<12>(a, affine, s); break;
+        case 14: launch_intra_ri<14>(a, affine, s); break;
+        case 16: launch_intra_ri<16>(a, affine, s); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
