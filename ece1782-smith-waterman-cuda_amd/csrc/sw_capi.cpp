@@ -195,6 +195,7 @@ struct sw_db {
     int32_t* d_lane_ids = nullptr;
     int32_t* d_bnd_h = nullptr;
     int32_t* d_bnd_f = nullptr;
+    int32_t* d_rescue = nullptr;  // [count, block ids...] for the 16-bit kernel
     // intra part (long subjects)
     int64_t nlong = 0;
     int32_t long_max = 0;
@@ -230,11 +231,11 @@ int32_t default_long_threshold(const sw_db* db) {
 
 void free_dev(sw_db* db) {
     void* ptrs[] = {db->d_res, db->d_blk_off, db->d_blk_groups, db->d_lane_ids, db->d_bnd_h, db->d_bnd_f,
-                    db->d_lres, db->d_loff, db->d_llen, db->d_lid, db->d_lbnd_h, db->d_lbnd_f};
+                    db->d_rescue, db->d_lres, db->d_loff, db->d_llen, db->d_lid, db->d_lbnd_h, db->d_lbnd_f};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     db->d_res = nullptr; db->d_blk_off = nullptr; db->d_blk_groups = nullptr; db->d_lane_ids = nullptr;
-    db->d_bnd_h = nullptr; db->d_bnd_f = nullptr; db->d_lres = nullptr; db->d_loff = nullptr;
+    db->d_bnd_h = nullptr; db->d_bnd_f = nullptr; db->d_rescue = nullptr; db->d_lres = nullptr; db->d_loff = nullptr;
     db->d_llen = nullptr; db->d_lid = nullptr; db->d_lbnd_h = nullptr; db->d_lbnd_f = nullptr;
     db->device_bytes = 0;
     db->built = false;
@@ -375,23 +376,34 @@ int check_scoring(const sw_scoring* sc, const int8_t** mat, int* go, int* ge) {
 // predecessors)).  Intra kernel: the same values laid out per chunk of
 // 64*ri query rows as [code][lane][RIP] so each lane's ri rows are contiguous.
 struct Profiles {
-    int32_t stride = 0;      // inter: bytes per code row
-    size_t inter_bytes = 0;
-    size_t intra_off = 0;    // byte offset of the intra profile in the buffer
+    int32_t stride = 0;      // inter profiles: entries per code row
+    size_t off8 = 0;         // int8 inter profile (biased for linear)
+    size_t off16 = 0;        // int16 inter profile (16-bit kernel)
+    size_t off32 = 0;        // int32 inter profile (p32 kernel)
+    size_t intra_off = 0;    // lane-slotted intra profile
     size_t total = 0;
 };
 
 int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* mat, int go, bool affine,
-                   int32_t qpad_inter, int ri, int32_t qpad_intra, Profiles* P) {
+                   int32_t qpad_inter, bool want16, bool want32, int ri, int32_t qpad_intra, Profiles* P) {
     for (int32_t i = 0; i < qlen; ++i)
         if (q[i] >= SW_ALPHABET) return fail(SW_E_INVALID, "query residue code out of range (use sw_encode)");
     const int bias = affine ? 0 : go;
     P->stride = static_cast<int32_t>(round_up(std::max<int32_t>(qpad_inter, 16), 16));
-    P->inter_bytes = static_cast<size_t>(swk::kProfileRows) * P->stride;
-    P->intra_off = round_up(static_cast<int64_t>(P->inter_bytes), 256);
+    const size_t n = static_cast<size_t>(swk::kProfileRows) * P->stride;
+    size_t at = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = at;
+        at = round_up(static_cast<int64_t>(at + bytes), 256);
+        return o;
+    };
+    P->off8 = take(n);
+    P->off16 = want16 ? take(2 * n) : 0;
+    P->off32 = want32 ? take(4 * n) : 0;
     const int rip = swk::intra_rip(ri);
     const size_t intra_bytes = ri ? static_cast<size_t>(qpad_intra / (swk::kLanes * ri)) * swk::intra_chunk_bytes(ri) : 0;
-    P->total = P->intra_off + intra_bytes;
+    P->intra_off = take(intra_bytes);
+    P->total = at;
     if (P->total > h->h_prof_cap) {
         if (h->prof_pending) HIPCHECK(hipEventSynchronize(h->prof_copied));
         h->prof_pending = false;
@@ -409,12 +421,21 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     }
     if (h->prof_pending) HIPCHECK(hipEventSynchronize(h->prof_copied));  // previous copy consumed the buffer
     int8_t* hp = h->h_prof;
-    auto value = [&](int c, int64_t row) -> int8_t {
-        if (c >= SW_ALPHABET || row >= qlen) return static_cast<int8_t>(bias);
-        return static_cast<int8_t>(mat[25 * q[row] + c] + bias);
+    auto value = [&](int c, int64_t row) -> int {
+        if (c >= SW_ALPHABET || row >= qlen) return bias;
+        return mat[25 * q[row] + c] + bias;
     };
+    int8_t* p8 = hp + P->off8;
+    int16_t* p16 = reinterpret_cast<int16_t*>(hp + P->off16);
+    int32_t* p32 = reinterpret_cast<int32_t*>(hp + P->off32);
     for (int c = 0; c < swk::kProfileRows; ++c)
-        for (int32_t i = 0; i < P->stride; ++i) hp[static_cast<size_t>(c) * P->stride + i] = value(c, i);
+        for (int32_t i = 0; i < P->stride; ++i) {
+            const int v = value(c, i);
+            const size_t k = static_cast<size_t>(c) * P->stride + i;
+            p8[k] = static_cast<int8_t>(v);
+            if (want16) p16[k] = static_cast<int16_t>(v);
+            if (want32) p32[k] = v;
+        }
     if (ri) {
         const int64_t CH = static_cast<int64_t>(swk::kLanes) * ri;
         int8_t* ip = hp + P->intra_off;
@@ -423,7 +444,7 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
             for (int c = 0; c < swk::kProfileRows; ++c)
                 for (int t = 0; t < swk::kLanes; ++t) {
                     int8_t* d = ip + ((ch * swk::kProfileRows + c) * swk::kLanes + t) * rip;
-                    for (int r = 0; r < rip; ++r) d[r] = r < ri ? value(c, ch * CH + t * ri + r) : 0;
+                    for (int r = 0; r < rip; ++r) d[r] = static_cast<int8_t>(r < ri ? value(c, ch * CH + t * ri + r) : 0);
                 }
     }
     HIPCHECK(hipMemcpyAsync(h->d_prof, hp, P->total, hipMemcpyHostToDevice, h->stream));
@@ -452,7 +473,12 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     const int8_t* mat;
     int go, ge, rc;
     if ((rc = check_scoring(sc, &mat, &go, &ge))) return rc;
-    const bool affine = go != ge;
+    // The linear kernels keep S + gap in an int8 profile; if that does not
+    // fit, score with the affine kernels (open == extend is the same DP).
+    bool biased_fits = true;
+    for (int k = 0; k < 625; ++k)
+        if (mat[k] + go > 127) biased_fits = false;
+    const bool affine = go != ge || !biased_fits;
     if (!db->built && (rc = build_db(db))) return rc;
     HIPCHECK(hipSetDevice(h->device));
     h->launches = 0;
@@ -475,7 +501,13 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         return SW_OK;
     }
     Profiles P;
-    if ((rc = build_profiles(h, query, qlen, mat, go, affine, qpad_inter, ri, qpad_intra, &P))) return rc;
+    const bool p32 = swk::inter_profile32(affine);
+    const bool i16 = swk::inter_uses_16bit(affine);
+    if ((rc = build_profiles(h, query, qlen, mat, go, affine, qpad_inter, i16, p32, ri, qpad_intra, &P))) return rc;
+    if (i16 && db->nblocks && !db->d_rescue) {
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rescue), (db->nblocks + 1) * sizeof(int32_t)));
+        db->device_bytes += (db->nblocks + 1) * sizeof(int32_t);
+    }
     const bool multi_inter = qpad_inter > R;
     const bool multi_intra = ri && qpad_intra > swk::kLanes * ri;
     if ((multi_inter || multi_intra) && (rc = ensure_bnd(db, affine))) return rc;
@@ -509,7 +541,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         a.blk_groups = db->d_blk_groups;
         a.lane_ids = db->d_lane_ids;
         a.nblocks = static_cast<int32_t>(db->nblocks);
-        a.prof = h->d_prof;
+        a.prof = h->d_prof + (i16 ? P.off16 : p32 ? P.off32 : P.off8);
         a.prof_stride = P.stride;
         a.qpad = qpad_inter;
         a.gap_open = go;
@@ -517,8 +549,25 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         a.bnd_h = db->d_bnd_h;
         a.bnd_f = db->d_bnd_f;
         a.scores = scores_dev;
+        if (i16) {
+            a.rescue_count = db->d_rescue;
+            a.rescue_list = db->d_rescue + 1;
+            HIPCHECK(hipMemsetAsync(a.rescue_count, 0, sizeof(int32_t), h->stream));
+        }
         HIPCHECK(swk::launch_inter(a, affine, h->stream));
         ++h->launches;
+        if (i16) {
+            // int32 re-scoring of any block the 16-bit kernel flagged (rare:
+            // scores near 32767); the list and its count stay on the device
+            swk::InterArgs r = a;
+            r.prof = h->d_prof + P.off8;
+            r.blk_list = db->d_rescue + 1;
+            r.blk_count = db->d_rescue;
+            r.rescue_list = nullptr;
+            r.rescue_count = nullptr;
+            HIPCHECK(swk::launch_inter_rescue(r, h->stream));
+            ++h->launches;
+        }
     }
     HIPCHECK(hipEventRecord(h->ev[2], h->stream));
     // join

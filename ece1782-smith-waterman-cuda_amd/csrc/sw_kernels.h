@@ -14,6 +14,24 @@ constexpr int kProfileRows = 32;  // profile codes: 25 residues + PAD (25) + unu
 constexpr int kPadCode = 25;      // residue code used for padding (scores 0)
 constexpr int kWavesPerWG = 4;
 
+// Shared by the inter kernels: one wave's residues for SG columns.
+template <int SG>
+struct Residues {
+    uint32_t w[SG / 4];
+    __device__ __forceinline__ void load(const uint8_t* p) {
+        if constexpr (SG == 16) {
+            const int4 v = *reinterpret_cast<const int4*>(p);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else if constexpr (SG == 8) {
+            const int2 v = *reinterpret_cast<const int2*>(p);
+            w[0] = v.x; w[1] = v.y;
+        } else {
+            w[0] = *reinterpret_cast<const uint32_t*>(p);
+        }
+    }
+    __device__ __forceinline__ uint32_t code(int jj) const { return (w[jj >> 2] >> (8 * (jj & 3))) & 0xffu; }
+};
+
 // Packed database, inter-sequence part (the layout
 // replaces the reference's [block][col][32-lane] short interleave,
 // SWSolver.cu:316):
@@ -37,7 +55,13 @@ struct InterArgs {
     int32_t* bnd_h;
     int32_t* bnd_f;
     int32_t* scores;             // scores[id]
-    int32_t* sat_flags;          // reserved for the int16 path
+    // int16 kernel: blocks with a lane near int16 saturation are appended
+    // here (count at rescue_count) and re-scored by the int32 kernel, which
+    // in list mode (blk_list != nullptr) walks only the listed blocks.
+    int32_t* rescue_list;
+    int32_t* rescue_count;
+    const int32_t* blk_list;
+    const int32_t* blk_count;
 };
 
 // Long subjects: one wave per subject, query rows spread over the 64 lanes,
@@ -60,6 +84,8 @@ struct IntraArgs {
 // Strip heights (query rows held in registers per lane) the kernels are
 // instantiated for.
 int inter_rows(bool affine);
+// true: the inter kernel takes an int32 profile [kProfileRows][prof_stride] int32
+bool inter_profile32(bool affine);
 // Query rows per lane the intra kernel uses for this query (2..16, even).
 int intra_rows_for(int qlen, int longest);
 // Bytes of one intra profile chunk (64*ri query rows, 32 codes).
@@ -67,6 +93,14 @@ int intra_chunk_bytes(int ri);
 __host__ __device__ constexpr int intra_rip(int RI) { return (RI + 3) / 4 * 4; }
 
 hipError_t launch_inter(const InterArgs& a, bool affine, hipStream_t s);
+// Linear gap: true if the 16-bit inter kernel is used (profile int16 [32][stride]).
+bool inter_uses_16bit(bool affine);
+// The 16-bit inter kernel (sw_inter16.hip, its own translation unit).
+hipError_t launch_inter16(const InterArgs& a, int R, int SG, hipStream_t s);
+// Lanes whose 16-bit running maximum reaches this may have overflowed.
+constexpr int kSat16 = 32767 - 1152;
+// int32 re-scoring of the blocks the 16-bit kernel listed (device-side count).
+hipError_t launch_inter_rescue(const InterArgs& a, hipStream_t s);
 hipError_t launch_intra(const IntraArgs& a, int ri, bool affine, hipStream_t s);
 
 }  // namespace swk

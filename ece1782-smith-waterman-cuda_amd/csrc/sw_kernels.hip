@@ -92,22 +92,6 @@ __device__ __forceinline__ void stage_profile(uint8_t* lp, const int8_t* __restr
 // current column is computed, and the next sub-group's residues and boundary
 // values are loaded at the top of the current sub-group; a sched_barrier
 // closes each column.
-template <int SG>
-struct Residues {
-    uint32_t w[SG / 4];
-    __device__ __forceinline__ void load(const uint8_t* p) {
-        if constexpr (SG == 16) {
-            const int4 v = *reinterpret_cast<const int4*>(p);
-            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-        } else if constexpr (SG == 8) {
-            const int2 v = *reinterpret_cast<const int2*>(p);
-            w[0] = v.x; w[1] = v.y;
-        } else {
-            w[0] = *reinterpret_cast<const uint32_t*>(p);
-        }
-    }
-    __device__ __forceinline__ uint32_t code(int jj) const { return (w[jj >> 2] >> (8 * (jj & 3))) & 0xffu; }
-};
 
 template <int SG>
 __device__ __forceinline__ void load_row(int (&v)[SG], const int32_t* p) {
@@ -140,16 +124,30 @@ __device__ __forceinline__ void read_prof(int4 (&pv)[R / 16], const uint8_t* lp,
 }
 
 template <int R, int SG, bool AFFINE>
+__device__ __forceinline__ void inter_block(const InterArgs& a, int blk, uint8_t* lp, int lane);
+
+template <int R, int SG, bool AFFINE>
 __global__ __launch_bounds__(256) void sw_inter(InterArgs a) {
-    constexpr int S = inter_stride(R);
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerWG * kProfileRows * S];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerWG * kProfileRows * inter_stride(R)];
     // threadIdx.x >> 6 is wave-uniform, but the compiler cannot prove it:
     // without readfirstlane every bound below would be a divergent VGPR value.
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
+    uint8_t* lp = lds + wave * (kProfileRows * inter_stride(R));
+    if (a.blk_list) {  // rescue mode: the listed blocks only (count on the device)
+        const int n = __builtin_amdgcn_readfirstlane(*a.blk_count);
+        for (int i = blockIdx.x * kWavesPerWG + wave; i < n; i += gridDim.x * kWavesPerWG)
+            inter_block<R, SG, AFFINE>(a, __builtin_amdgcn_readfirstlane(a.blk_list[i]), lp, lane);
+        return;
+    }
     const int blk = blockIdx.x * kWavesPerWG + wave;
     if (blk >= a.nblocks) return;  // wave-uniform
-    uint8_t* lp = lds + wave * (kProfileRows * S);
+    inter_block<R, SG, AFFINE>(a, blk, lp, lane);
+}
+
+template <int R, int SG, bool AFFINE>
+__device__ __forceinline__ void inter_block(const InterArgs& a, int blk, uint8_t* lp, int lane) {
+    constexpr int S = inter_stride(R);
 
     const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
     const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
@@ -266,6 +264,149 @@ __global__ __launch_bounds__(256) void sw_inter(InterArgs a) {
 #pragma unroll
                         for (int q = 0; q < SG; ++q) bf[q] = 0;
                     }
+                }
+            }
+        }
+    }
+done:
+    const int id = a.lane_ids[static_cast<size_t>(blk) * kLanes + lane];
+    if (id >= 0) a.scores[id] = best;
+}
+
+// ---------------------------------------------------------------------------
+// inter-sequence, linear gap, int32 profile ("p32")
+// ---------------------------------------------------------------------------
+// Same scheme as sw_inter, but the profile slice in LDS holds int32 scores so
+// the per-cell add is the fast-rate v_add_u32 instead of the slow SDWA form
+// (profiles/r01_valu_rate_*.txt).  Per column a lane reads R*4 bytes; the
+// reads are pipelined one 16-row chunk ahead over a flat (column, chunk)
+// schedule with ping-pong buffers.
+__host__ __device__ constexpr int inter32_stride(int R) {
+    // R*4 bytes + 16, with an odd number of 16-byte slots (bank spread)
+    return ((R * 4 + 16) / 16) % 2 == 1 ? R * 4 + 16 : R * 4 + 32;
+}
+
+template <int R>
+__device__ __forceinline__ void stage_profile32(uint8_t* lp, const int32_t* __restrict__ prof, int stride,
+                                                int s0, int lane) {
+    constexpr int kChunks = kProfileRows * (R / 4);  // 16-byte chunks
+    constexpr int S = inter32_stride(R);
+#pragma unroll
+    for (int t = lane; t < kChunks; t += kLanes) {
+        const int c = t / (R / 4);
+        const int k = t % (R / 4);
+        const int4 v = *reinterpret_cast<const int4*>(prof + static_cast<size_t>(c) * stride + s0 + 4 * k);
+        *reinterpret_cast<int4*>(lp + c * S + 16 * k) = v;
+    }
+}
+
+__device__ __forceinline__ void read_chunk(int4 (&p)[4], const uint8_t* lp, uint32_t off, int dep) {
+    asm volatile("" : "+v"(off) : "v"(dep));
+    const int4* pp = reinterpret_cast<const int4*>(lp + off);
+    p[0] = pp[0];
+    p[1] = pp[1];
+    p[2] = pp[2];
+    p[3] = pp[3];
+}
+
+template <int R, int SG>
+__global__ __launch_bounds__(256) void sw_inter_p32(InterArgs a) {
+    constexpr int S = inter32_stride(R);
+    constexpr int NCH = R / 16;          // 16-row chunks per column
+    constexpr int STEPS = SG * NCH;      // (column, chunk) steps per sub-group
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerWG * kProfileRows * S];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int blk = blockIdx.x * kWavesPerWG + wave;
+    if (blk >= a.nblocks) return;
+    uint8_t* lp = lds + wave * (kProfileRows * S);
+    const int32_t* prof32 = reinterpret_cast<const int32_t*>(a.prof);
+
+    const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
+    const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
+    const uint32_t go = static_cast<uint32_t>(a.gap_open);
+    int best = 0;
+    if (ncols == 0) goto done;
+
+    for (int s0 = 0; s0 < a.qpad; s0 += R) {
+        const bool first = (s0 == 0);
+        const bool last = (s0 + R >= a.qpad);
+        stage_profile32<R>(lp, prof32, a.prof_stride, s0, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+
+        int H[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) H[r] = 0;
+        int dtop = 0;
+
+        Residues<SG> rs, rs_next;
+        int bh[SG], bh_next[SG];
+        rs.load(a.residues + base);
+        if (!first) {
+            load_row<SG>(bh, a.bnd_h + base);
+        } else {
+#pragma unroll
+            for (int q = 0; q < SG; ++q) bh[q] = 0;
+        }
+        int4 P[2][4];
+        read_chunk(P[0], lp, rs.code(0) * S, 0);
+
+        for (uint32_t col0 = 0; col0 < ncols; col0 += SG) {
+            const uint64_t idx = base + (col0 >> 4) * kGroupBytes + (col0 & 15);
+            const bool more = col0 + SG < ncols;
+            const uint64_t nidx = base + ((col0 + SG) >> 4) * kGroupBytes + ((col0 + SG) & 15);
+            if (more) {
+                rs_next.load(a.residues + nidx);
+                if (!first) load_row<SG>(bh_next, a.bnd_h + nidx);
+            }
+            int up = 0, diag = 0;
+#pragma unroll
+            for (int t = 0; t < STEPS; ++t) {
+                const int jj = t / NCH;
+                const int k = t % NCH;
+                // prefetch the next step's chunk (next column's first chunk at a column end)
+                if (t + 1 < STEPS) {
+                    const int jn = (t + 1) / NCH, kn = (t + 1) % NCH;
+                    read_chunk(P[(t + 1) & 1], lp, rs.code(jn) * S + 64 * kn, k == 0 ? H[R - 1] : H[16 * k - 1]);
+                } else if (more) {
+                    read_chunk(P[(t + 1) & 1], lp, rs_next.code(0) * S, H[16 * k - 1]);
+                }
+                if (k == 0) {
+                    up = bh[jj];
+                    diag = dtop;
+                    dtop = up;
+                }
+                const int4(&pc)[4] = P[t & 1];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int sv[4] = {pc[q].x, pc[q].y, pc[q].z, pc[q].w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int r = 16 * k + 4 * q + e;
+                        const int h = usub(max(max(H[r], up), diag + sv[e]), go);
+                        diag = H[r];
+                        H[r] = h;
+                        up = h;
+                        best = max(best, h);
+                    }
+                }
+                if (k == NCH - 1) {
+                    bh[jj] = up;
+                    asm volatile("" : "+v"(best));
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            if (!last) store_row<SG>(a.bnd_h + idx, bh);
+            if (more) {
+                rs = rs_next;
+                if (!first) {
+#pragma unroll
+                    for (int q = 0; q < SG; ++q) bh[q] = bh_next[q];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < SG; ++q) bh[q] = 0;
                 }
             }
         }
@@ -418,22 +559,40 @@ __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
 // ---------------------------------------------------------------------------
 // Inter-kernel shape: R query rows per strip x SG columns per software-
 // pipelined sub-group.  SW_INTER_VARIANT="RxSG" overrides (tuning only).
-struct InterShape { int R, SG; };
+struct InterShape { int R, SG; bool p32; bool i16; };
 static InterShape inter_shape(bool affine) {
     // measured on MI355X (scripts/tune_inter.py, profiles/r01_tune_inter.jsonl):
     // 64x8 is fastest for the linear kernel (170 VGPRs, 2 waves/SIMD, half
     // the boundary traffic of 32-row strips); affine keeps 32x8.
-    InterShape v = affine ? InterShape{32, 8} : InterShape{64, 8};
+    // measured on MI355X: 64x8 int32 beats the 16-bit-value (h*) and int32-
+    // profile (p*) variants on C2 (profiles/r01_tune_inter*.jsonl)
+    InterShape v = affine ? InterShape{32, 8, false, false} : InterShape{64, 8, false, false};
     if (const char* e = std::getenv("SW_INTER_VARIANT")) {
         int r = 0, g = 0;
-        if (std::sscanf(e, "%dx%d", &r, &g) == 2 &&
+        if (std::sscanf(e, "h%dx%d", &r, &g) == 2 && !affine &&
+            ((r == 64 && (g == 8 || g == 16)) || (r == 32 && (g == 8 || g == 16)) || (r == 48 && g == 8)))
+            v = InterShape{r, g, false, true};
+        else if (std::sscanf(e, "p%dx%d", &r, &g) == 2 && !affine &&
+            ((r == 64 && (g == 8 || g == 4)) || (r == 32 && g == 8) || (r == 48 && g == 8)))
+            v = InterShape{r, g, true, false};
+        else if (std::sscanf(e, "%dx%d", &r, &g) == 2 &&
             ((r == 32 && (g == 8 || g == 16)) || (r == 48 && g == 8) || (r == 64 && g == 8) || (r == 16 && g == 16)))
-            v = InterShape{r, g};
+            v = InterShape{r, g, false, false};
     }
     return v;
 }
 
 int inter_rows(bool affine) { return inter_shape(affine).R; }
+bool inter_profile32(bool affine) { return inter_shape(affine).p32; }
+bool inter_uses_16bit(bool affine) { return inter_shape(affine).i16; }
+
+// int32 re-scoring of the blocks the 16-bit kernel put on the rescue list.
+hipError_t launch_inter_rescue(const InterArgs& a, hipStream_t s) {
+    // A few hundred waves walk the device-side list; an empty list costs one
+    // tiny launch and no host synchronisation.
+    hipLaunchKernelGGL((sw_inter<64, 8, false>), dim3(64), dim3(kWavesPerWG * kLanes), 0, s, a);
+    return hipGetLastError();
+}
 
 // Rows per lane for the intra kernel: minimise
 //   chunks * (steps per chunk) * (ops per step)
@@ -458,6 +617,20 @@ hipError_t launch_inter(const InterArgs& a, bool affine, hipStream_t s) {
     const dim3 grid((a.nblocks + kWavesPerWG - 1) / kWavesPerWG);
     const dim3 block(kWavesPerWG * kLanes);
     const InterShape v = inter_shape(affine);
+    if (v.i16) return launch_inter16(a, v.R, v.SG, s);
+    if (v.p32) {
+#define SW_LAUNCH_P32(R_, SG_)                                                               \
+        if (v.R == R_ && v.SG == SG_) {                                                      \
+            hipLaunchKernelGGL((sw_inter_p32<R_, SG_>), grid, block, 0, s, a);               \
+            return hipGetLastError();                                                        \
+        }
+        SW_LAUNCH_P32(64, 8)
+        SW_LAUNCH_P32(64, 4)
+        SW_LAUNCH_P32(32, 8)
+        SW_LAUNCH_P32(48, 8)
+#undef SW_LAUNCH_P32
+        return hipErrorInvalidValue;
+    }
 #define SW_LAUNCH_INTER(R_, SG_)                                                             \
     if (v.R == R_ && v.SG == SG_) {                                                          \
         if (affine) hipLaunchKernelGGL((sw_inter<R_, SG_, true>), grid, block, 0, s, a);     \

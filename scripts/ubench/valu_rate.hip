@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 
 #define CHAINS 8
 #define ITERS 4096
@@ -76,6 +77,14 @@ BODY(max_u32) BODY(min_i32) BODY(max_f32) BODY(add_u16) BODY(sub_u16_clamp) BODY
 #define INSTR_mad_u16(x) asm volatile("v_mad_u16 %0, %0, %1, %2" : "+v"(x) : "v"(y), "v"(z))
 BODY(max3_i16) BODY(max3_u16) BODY(med3_i16) BODY(add_u16_opsel_hi) BODY(max_i16_opsel_hi) BODY(max3_i16_opsel) BODY(sub_u16_clamp_e64) BODY(add_u16_e32) BODY(mad_u16)
 
+
+// per-"cell" instruction mixes (8 independent chains so latency is hidden)
+#define INSTR_mix_cell_i32(x) asm volatile("v_add_u32_sdwa %0, %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n v_max3_i32 %0, %0, %1, %2\n v_sub_u32 %0, %0, %1 clamp\n v_max3_i32 %2, %2, %0, %1" : "+v"(x), "+v"(z) : "v"(y))
+#define INSTR_mix_cell_p32(x) asm volatile("v_add_u32 %0, %0, %1\n v_max3_i32 %0, %0, %1, %2\n v_sub_u32 %0, %0, %1 clamp\n v_max3_i32 %2, %2, %0, %1" : "+v"(x), "+v"(z) : "v"(y))
+#define INSTR_mix_cell_16(x) asm volatile("v_add_u16 %0, %0, %1\n v_max_i16 %0, %0, %1\n v_max_i16 %0, %0, %2\n v_sub_u16_e64 %0, %0, %1 clamp\n v_max_i16 %2, %2, %0" : "+v"(x), "+v"(z) : "v"(y))
+#define INSTR_mix_pk_dualq(x) asm volatile("v_pk_add_u16 %0, %0, %1\n v_pk_max_i16 %0, %0, %1\n v_pk_max_i16 %0, %0, %2\n v_pk_sub_u16 %0, %0, %1 clamp\n v_pk_max_i16 %2, %2, %0" : "+v"(x), "+v"(z) : "v"(y))
+BODY(mix_cell_i32) BODY(mix_cell_p32) BODY(mix_cell_16) BODY(mix_pk_dualq)
+
 // v_pk_fma_f32 / v_pk_add_f32 need 64-bit register pairs
 __global__ __launch_bounds__(256) void k_pk_add_f32(uint32_t* out, uint32_t seed) {
     double v[CHAINS];
@@ -110,13 +119,17 @@ typedef void (*kfn)(uint32_t*, uint32_t);
 
 int main() {
     struct { const char* name; kfn f; } ks[] = {
-        {"v_add_u32", k_add_u32}, {"v_max3_i32", k_max3_i32}, {"v_max_i16", k_max_i16}, {"max3_i16", k_max3_i16}, {"max3_u16", k_max3_u16}, {"med3_i16", k_med3_i16}, {"add_u16_opsel_hi", k_add_u16_opsel_hi}, {"max_i16_opsel_hi", k_max_i16_opsel_hi}, {"max3_i16_opsel", k_max3_i16_opsel}, {"sub_u16_clamp_e64", k_sub_u16_clamp_e64}, {"add_u16_e32", k_add_u16_e32}, {"mad_u16", k_mad_u16}
+        {"v_add_u32", k_add_u32}, {"v_sub_u32 clamp", k_sub_clamp}, {"v_max_i16", k_max_i16},
+        {"sub_u16_clamp", k_sub_u16_clamp}, {"v_max3_i32", k_max3_i32}, {"v_pk_max_i16", k_pk_max_i16},
+        {"mix_cell_i32", k_mix_cell_i32}, {"mix_cell_p32", k_mix_cell_p32}, {"mix_cell_16", k_mix_cell_16},
+        {"mix_pk_dualq", k_mix_pk_dualq},
     };
     int dev = 0;
     hipDeviceProp_t p;
     hipGetDeviceProperties(&p, dev);
     const int cus = p.multiProcessorCount;
-    const int blocks = cus * 8;  // 8 x 256 threads per CU = 32 waves/CU
+    const int wpc = getenv("WAVES_PER_SIMD") ? atoi(getenv("WAVES_PER_SIMD")) : 8;
+    const int blocks = cus * wpc;  // wpc x 256 threads per CU = wpc waves per SIMD
     uint32_t* out;
     hipMalloc(&out, blocks * 256 * 4);
     hipEvent_t a, b;

@@ -128,3 +128,22 @@ def test_long_query_self_hit_int32(sw, oracle, handle):
     got = int(db.scan(q)[0])
     want = int(oracle.scan(q, q, offs)[0])
     assert got == want and got > 32767
+
+
+@pytest.mark.parametrize("reps", [2100, 2190, 2300])
+def test_int16_saturation_rescue(sw, oracle, handle, reps):
+    """Scores at/above the 16-bit kernel's saturation guard are re-scored at
+    int32 (block-level rescue), next to ordinary subjects in the same block."""
+    rng = np.random.default_rng(reps)
+    q = sw.encode("W" * reps)
+    seqs = [rng.integers(0, 20, size=rng.integers(50, 400)).astype(np.uint8) for _ in range(150)]
+    seqs[37] = sw.encode("W" * reps)            # 15 * reps: 31500 .. 34500
+    seqs[90] = sw.encode("W" * (reps // 2) + "A" * 30 + "W" * (reps // 2))
+    res = np.concatenate(seqs)
+    offs = np.zeros(len(seqs) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(x) for x in seqs])
+    db = sw.Database(handle, res, offs, long_threshold=4096)
+    got = db.scan(q)
+    want = oracle.scan(q, res, offs)
+    assert got[37] == 15 * reps
+    assert np.array_equal(got, want)
