@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -163,6 +164,8 @@ struct sw_handle {
     // The intra kernel runs on a side stream, concurrently with the inter
     // kernel (fork/join through ev[0] and ev[1]).
     hipStream_t side = nullptr;
+    hipStream_t side2 = nullptr;  // the cooperative wide-block kernel
+    hipEvent_t coop_done = nullptr;
     // per-query workspace: profiles (inter: [32][stride]; intra: lane-slotted
     // chunks) built in pinned host buffers, copied once per query
     int8_t* d_prof = nullptr;
@@ -196,6 +199,7 @@ struct sw_db {
     int32_t* d_bnd_h = nullptr;
     int32_t* d_bnd_f = nullptr;
     int32_t* d_rescue = nullptr;  // [count, block ids...] for the 16-bit kernel
+    std::vector<uint32_t> h_blk_groups;  // block widths (16-column groups), widest first
     // intra part (long subjects)
     int64_t nlong = 0;
     int32_t long_max = 0;
@@ -220,12 +224,14 @@ namespace {
 // the inter kernel takes time proportional to its longest subject, so very
 // long subjects would become the kernel's critical path; measured on the C2
 // workload (mean length 360): 1536 beats 3072 by 1.3x and 1024 by 1.03x
-// (profiles/r01_tune_inter.jsonl).  Default: 4.25 x mean length, clamped.
+// (profiles/r01_tune_inter.jsonl); with the cooperative kernel for wide
+// blocks the best is ~2048 (profiles/r01_tune_coop.jsonl).  Default: 5.7 x
+// mean length, clamped.
 
 int32_t default_long_threshold(const sw_db* db) {
     if (db->n == 0) return 1536;
     const double mean = static_cast<double>(db->residues) / static_cast<double>(db->n);
-    const double t = 4.25 * mean;
+    const double t = 5.7 * mean;
     return static_cast<int32_t>(std::min(8192.0, std::max(1024.0, t)));
 }
 
@@ -320,6 +326,7 @@ int build_db(sw_db* db) {
     if ((rc = upload(&db->d_llen, llen, s, &acc))) return rc;
     if ((rc = upload(&db->d_lid, lid, s, &acc))) return rc;
     HIPCHECK(hipStreamSynchronize(s));  // host vectors go out of scope
+    db->h_blk_groups = blk_groups;
     db->res_bytes = total;
     db->lres_bytes = ltotal;
     db->nblocks = nblocks;
@@ -453,6 +460,24 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     return SW_OK;
 }
 
+// Leading (widest) blocks handled by the cooperative kernel: blocks whose
+// one-wave time is a large share of the whole scan.  One wave of a W-column
+// block costs ~W*qpad*3.5 VALU instructions at ~8.4 cycles each (2 waves per
+// SIMD); the scan costs ~16 cycles per 64 cells over 1024 SIMDs.  Measured on
+// C2 (2.05e8 residues, profiles/r01_tune_coop.jsonl): width 384 with long
+// threshold 2048 is best, i.e. W ~ sum(residues) / 530000.  SW_COOP_WIDTH
+// overrides (tuning); 0 disables.
+int32_t coop_blocks(const sw_db* db) {
+    int64_t wmin = std::max<int64_t>(128, db->residues / 530000);
+    if (const char* e = std::getenv("SW_COOP_WIDTH")) wmin = std::atoll(e);
+    if (wmin <= 0) return 0;
+    int32_t n = 0;
+    while (n < static_cast<int32_t>(db->h_blk_groups.size()) &&
+           static_cast<int64_t>(db->h_blk_groups[n]) * swk::kGroupCols >= wmin)
+        ++n;
+    return n;
+}
+
 int next_events(sw_handle* h) {
     if (h->nscans >= 4096) h->nscans = 0;  // bound the pool; older sums are dropped
     if (h->nscans == h->evpool.size()) {
@@ -503,12 +528,16 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     Profiles P;
     const bool p32 = swk::inter_profile32(affine);
     const bool i16 = swk::inter_uses_16bit(affine);
-    if ((rc = build_profiles(h, query, qlen, mat, go, affine, qpad_inter, i16, p32, ri, qpad_intra, &P))) return rc;
+    // the int32 rescue pass after a 16-bit kernel walks 64-row strips
+    const int32_t qpad_rescue = i16 ? static_cast<int32_t>(round_up(qlen, 64)) : 0;
+    if ((rc = build_profiles(h, query, qlen, mat, go, affine, std::max(qpad_inter, qpad_rescue), i16, p32, ri,
+                             qpad_intra, &P)))
+        return rc;
     if (i16 && db->nblocks && !db->d_rescue) {
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rescue), (db->nblocks + 1) * sizeof(int32_t)));
         db->device_bytes += (db->nblocks + 1) * sizeof(int32_t);
     }
-    const bool multi_inter = qpad_inter > R;
+    const bool multi_inter = qpad_inter > R || qpad_rescue > 64;
     const bool multi_intra = ri && qpad_intra > swk::kLanes * ri;
     if ((multi_inter || multi_intra) && (rc = ensure_bnd(db, affine))) return rc;
 
@@ -554,13 +583,27 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             a.rescue_list = db->d_rescue + 1;
             HIPCHECK(hipMemsetAsync(a.rescue_count, 0, sizeof(int32_t), h->stream));
         }
+        // widest blocks first, one cooperative workgroup each (linear int32 path)
+        const int32_t ncoop = (!affine && !i16 && !p32) ? coop_blocks(db) : 0;
+        if (ncoop) {
+            // on its own stream, so the per-wave kernel fills the GPU beside it
+            swk::InterArgs c = a;
+            c.qpad = static_cast<int32_t>(round_up(qlen, swk::inter_coop_rows()));
+            HIPCHECK(hipStreamWaitEvent(h->side2, h->ev[0], 0));
+            HIPCHECK(swk::launch_inter_coop(c, ncoop, h->side2));
+            HIPCHECK(hipEventRecord(h->coop_done, h->side2));
+            ++h->launches;
+            a.blk_first = ncoop;
+        }
         HIPCHECK(swk::launch_inter(a, affine, h->stream));
         ++h->launches;
+        if (ncoop) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
         if (i16) {
             // int32 re-scoring of any block the 16-bit kernel flagged (rare:
             // scores near 32767); the list and its count stay on the device
             swk::InterArgs r = a;
             r.prof = h->d_prof + P.off8;
+            r.qpad = qpad_rescue;
             r.blk_list = db->d_rescue + 1;
             r.blk_count = db->d_rescue;
             r.rescue_list = nullptr;
@@ -632,7 +675,9 @@ int sw_create(int32_t device, sw_handle** out) {
     if (e != hipSuccess) { delete h; return fail(SW_E_HIP, hipGetErrorString(e)); }
     h->own_stream = true;
     e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side2, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->prof_copied, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->coop_done, hipEventDisableTiming);
     if (e != hipSuccess) { delete h; return fail(SW_E_HIP, hipGetErrorString(e)); }
     *out = h;
     return SW_OK;
@@ -646,11 +691,14 @@ int sw_destroy(sw_handle* h) {
         for (auto& ev : se.ev)
             if (ev) (void)hipEventDestroy(ev);
     if (h->side) (void)hipStreamSynchronize(h->side);
+    if (h->side2) (void)hipStreamSynchronize(h->side2);
     if (h->d_prof) (void)hipFree(h->d_prof);
     if (h->h_prof) (void)hipHostFree(h->h_prof);
     if (h->prof_copied) (void)hipEventDestroy(h->prof_copied);
     if (h->d_scores) (void)hipFree(h->d_scores);
     if (h->side) (void)hipStreamDestroy(h->side);
+    if (h->side2) (void)hipStreamDestroy(h->side2);
+    if (h->coop_done) (void)hipEventDestroy(h->coop_done);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return SW_OK;

@@ -62,6 +62,9 @@ struct InterArgs {
     int32_t* rescue_count;
     const int32_t* blk_list;
     const int32_t* blk_count;
+    // blocks [0, blk_first) are handled by the cooperative kernel; the
+    // one-block-per-wave kernels start at blk_first
+    int32_t blk_first;
 };
 
 // Long subjects: one wave per subject, query rows spread over the 64 lanes,
@@ -93,10 +96,16 @@ int intra_chunk_bytes(int ri);
 __host__ __device__ constexpr int intra_rip(int RI) { return (RI + 3) / 4 * 4; }
 
 hipError_t launch_inter(const InterArgs& a, bool affine, hipStream_t s);
+// Wide blocks [0, ncoop): one 4-wave workgroup per block, the waves pipelined
+// over query strips (linear gap).  Returns the strip height it uses.
+hipError_t launch_inter_coop(const InterArgs& a, int ncoop, hipStream_t s);
+int inter_coop_rows();
 // Linear gap: true if the 16-bit inter kernel is used (profile int16 [32][stride]).
 bool inter_uses_16bit(bool affine);
 // The 16-bit inter kernel (sw_inter16.hip, its own translation unit).
 hipError_t launch_inter16(const InterArgs& a, int R, int SG, hipStream_t s);
+// The packed two-subjects-per-lane kernel (sw_inter_pk.hip).
+hipError_t launch_inter_pk(const InterArgs& a, int R, int SG, hipStream_t s);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.
 constexpr int kSat16 = 32767 - 1152;
 // int32 re-scoring of the blocks the 16-bit kernel listed (device-side count).

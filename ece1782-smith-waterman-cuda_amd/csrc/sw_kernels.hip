@@ -140,14 +140,13 @@ __global__ __launch_bounds__(256) void sw_inter(InterArgs a) {
             inter_block<R, SG, AFFINE>(a, __builtin_amdgcn_readfirstlane(a.blk_list[i]), lp, lane);
         return;
     }
-    const int blk = blockIdx.x * kWavesPerWG + wave;
+    const int blk = a.blk_first + blockIdx.x * kWavesPerWG + wave;
     if (blk >= a.nblocks) return;  // wave-uniform
     inter_block<R, SG, AFFINE>(a, blk, lp, lane);
 }
 
 template <int R, int SG, bool AFFINE>
 __device__ __forceinline__ void inter_block(const InterArgs& a, int blk, uint8_t* lp, int lane) {
-    constexpr int S = inter_stride(R);
 
     const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
     const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
@@ -271,6 +270,124 @@ __device__ __forceinline__ void inter_block(const InterArgs& a, int blk, uint8_t
 done:
     const int id = a.lane_ids[static_cast<size_t>(blk) * kLanes + lane];
     if (id >= 0) a.scores[id] = best;
+}
+
+// ---------------------------------------------------------------------------
+// inter-sequence, linear gap, cooperative: one workgroup per WIDE block
+// ---------------------------------------------------------------------------
+// With one block per wave, the widest blocks (subjects near the long
+// threshold) are the kernel's critical path: a 1536-column block is ~7 ms of
+// one wave's work at 2 waves/SIMD.  Here the 4 waves of a workgroup share one
+// block: in pass p wave w computes query strip 4p+w, one 8-column chunk behind
+// wave w-1, and receives that wave's strip-bottom row for the chunk through an
+// LDS double buffer (one workgroup barrier per chunk step).  Only the last
+// strip of a pass hands its bottom row to the next pass through HBM.  The
+// block's latency drops ~4x.
+template <int R>
+__global__ __launch_bounds__(256) void sw_inter_coop(InterArgs a) {
+    constexpr int SG = 8;
+    constexpr int S = inter_stride(R);
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerWG * kProfileRows * S];
+    __shared__ __attribute__((aligned(16))) int4 ring[kWavesPerWG - 1][2][kLanes][SG / 4];
+    __shared__ int red[kWavesPerWG][kLanes];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int blk = blockIdx.x;  // the widest blocks come first
+    uint8_t* lp = lds + wave * (kProfileRows * S);
+    const int nchunks = static_cast<int>(a.blk_groups[blk] * (kGroupCols / SG));
+    const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
+    const uint32_t go = static_cast<uint32_t>(a.gap_open);
+    const int nstrips = a.qpad / R;
+    const int passes = (nstrips + kWavesPerWG - 1) / kWavesPerWG;
+    int best = 0;
+
+    for (int p = 0; p < passes; ++p) {
+        const int strip = p * kWavesPerWG + wave;
+        const bool valid = strip < nstrips;
+        const bool first = (strip == 0);
+        const bool last = (strip == nstrips - 1);
+        const int s0 = strip * R;
+        if (valid) stage_profile<R>(lp, a.prof, a.prof_stride, s0, lane);
+        int H[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) H[r] = 0;
+        int dtop = 0;
+        __syncthreads();  // profile staged; the previous pass's HBM boundary rows are visible
+
+        for (int t = 0; t < nchunks + kWavesPerWG - 1; ++t) {
+            const int c = t - wave;
+            if (valid && c >= 0 && c < nchunks) {
+                const int col0 = c * SG;
+                const uint64_t idx = base + (col0 >> 4) * kGroupBytes + (col0 & 15);
+                Residues<SG> rs;
+                rs.load(a.residues + idx);
+                int bv[SG];
+                if (first) {
+#pragma unroll
+                    for (int q = 0; q < SG; ++q) bv[q] = 0;
+                } else if (wave == 0) {
+                    load_row<SG>(bv, a.bnd_h + idx);
+                } else {
+                    const int4* rp = ring[wave - 1][(t - 1) & 1][lane];
+#pragma unroll
+                    for (int q = 0; q < SG / 4; ++q) {
+                        const int4 v = rp[q];
+                        bv[4 * q] = v.x; bv[4 * q + 1] = v.y; bv[4 * q + 2] = v.z; bv[4 * q + 3] = v.w;
+                    }
+                }
+                int4 pcur[R / 16], pnext[R / 16];
+                read_prof<R>(pcur, lp, rs.code(0), 0);
+#pragma unroll
+                for (int jj = 0; jj < SG; ++jj) {
+                    if (jj + 1 < SG) read_prof<R>(pnext, lp, rs.code(jj + 1), H[R - 1]);
+                    int up = bv[jj];
+                    int diag = dtop;
+                    dtop = up;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int sc = sx8(pword(pcur, r >> 2), r & 3);
+                        const int h = usub(max(max(H[r], up), diag + sc), go);
+                        diag = H[r];
+                        H[r] = h;
+                        up = h;
+                        best = max(best, h);
+                    }
+                    bv[jj] = up;
+#pragma unroll
+                    for (int q = 0; q < R / 16; ++q) pcur[q] = pnext[q];
+                    asm volatile("" : "+v"(best));
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (!last) {
+                    if (wave == kWavesPerWG - 1) {
+                        store_row<SG>(a.bnd_h + idx, bv);
+                    } else {
+                        int4* wp = ring[wave][t & 1][lane];
+#pragma unroll
+                        for (int q = 0; q < SG / 4; ++q)
+                            wp[q] = make_int4(bv[4 * q], bv[4 * q + 1], bv[4 * q + 2], bv[4 * q + 3]);
+                    }
+                }
+            }
+            __syncthreads();  // chunk step: ring slots written at t are read at t + 1
+        }
+    }
+    red[wave][lane] = best;
+    __syncthreads();
+    if (wave == 0) {
+        const int b = max(max(red[0][lane], red[1][lane]), max(red[2][lane], red[3][lane]));
+        const int id = a.lane_ids[static_cast<size_t>(blk) * kLanes + lane];
+        if (id >= 0) a.scores[id] = b;
+    }
+}
+
+constexpr int kCoopRows = 32;
+int inter_coop_rows() { return kCoopRows; }
+
+hipError_t launch_inter_coop(const InterArgs& a, int ncoop, hipStream_t s) {
+    if (ncoop <= 0 || a.qpad <= 0) return hipSuccess;
+    hipLaunchKernelGGL((sw_inter_coop<kCoopRows>), dim3(ncoop), dim3(kWavesPerWG * kLanes), 0, s, a);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -559,25 +676,28 @@ __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
 // ---------------------------------------------------------------------------
 // Inter-kernel shape: R query rows per strip x SG columns per software-
 // pipelined sub-group.  SW_INTER_VARIANT="RxSG" overrides (tuning only).
-struct InterShape { int R, SG; bool p32; bool i16; };
+struct InterShape { int R, SG; bool p32; bool i16; bool pk; };
 static InterShape inter_shape(bool affine) {
     // measured on MI355X (scripts/tune_inter.py, profiles/r01_tune_inter.jsonl):
     // 64x8 is fastest for the linear kernel (170 VGPRs, 2 waves/SIMD, half
     // the boundary traffic of 32-row strips); affine keeps 32x8.
     // measured on MI355X: 64x8 int32 beats the 16-bit-value (h*) and int32-
     // profile (p*) variants on C2 (profiles/r01_tune_inter*.jsonl)
-    InterShape v = affine ? InterShape{32, 8, false, false} : InterShape{64, 8, false, false};
+    InterShape v = affine ? InterShape{32, 8, false, false, false} : InterShape{64, 8, false, false, false};
     if (const char* e = std::getenv("SW_INTER_VARIANT")) {
         int r = 0, g = 0;
-        if (std::sscanf(e, "h%dx%d", &r, &g) == 2 && !affine &&
+        if (std::sscanf(e, "k%dx%d", &r, &g) == 2 && !affine &&
+            ((r == 16 && (g == 8 || g == 16 || g == 9)) || (r == 32 && g == 8)))
+            v = InterShape{r, g, false, true, true};
+        else if (std::sscanf(e, "h%dx%d", &r, &g) == 2 && !affine &&
             ((r == 64 && (g == 8 || g == 16)) || (r == 32 && (g == 8 || g == 16)) || (r == 48 && g == 8)))
-            v = InterShape{r, g, false, true};
+            v = InterShape{r, g, false, true, false};
         else if (std::sscanf(e, "p%dx%d", &r, &g) == 2 && !affine &&
             ((r == 64 && (g == 8 || g == 4)) || (r == 32 && g == 8) || (r == 48 && g == 8)))
-            v = InterShape{r, g, true, false};
+            v = InterShape{r, g, true, false, false};
         else if (std::sscanf(e, "%dx%d", &r, &g) == 2 &&
             ((r == 32 && (g == 8 || g == 16)) || (r == 48 && g == 8) || (r == 64 && g == 8) || (r == 16 && g == 16)))
-            v = InterShape{r, g, false, false};
+            v = InterShape{r, g, false, false, false};
     }
     return v;
 }
@@ -613,10 +733,11 @@ int intra_rows_for(int qlen, int longest) {
 int intra_chunk_bytes(int ri) { return kProfileRows * kLanes * intra_rip(ri); }
 
 hipError_t launch_inter(const InterArgs& a, bool affine, hipStream_t s) {
-    if (a.nblocks <= 0 || a.qpad <= 0) return hipSuccess;
-    const dim3 grid((a.nblocks + kWavesPerWG - 1) / kWavesPerWG);
+    if (a.nblocks - a.blk_first <= 0 || a.qpad <= 0) return hipSuccess;
+    const dim3 grid((a.nblocks - a.blk_first + kWavesPerWG - 1) / kWavesPerWG);
     const dim3 block(kWavesPerWG * kLanes);
     const InterShape v = inter_shape(affine);
+    if (v.pk) return launch_inter_pk(a, v.R, v.SG, s);
     if (v.i16) return launch_inter16(a, v.R, v.SG, s);
     if (v.p32) {
 #define SW_LAUNCH_P32(R_, SG_)                                                               \
