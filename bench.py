@@ -93,6 +93,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r01_pmc_traffic.json"))
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo = rehearse the multi-rank path on one GPU (CPU collectives)")
+    ap.add_argument("--device", type=int, default=None, help="override the GPU index (rehearsal)")
     args = ap.parse_args()
 
     import torch
@@ -103,10 +106,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = local if args.device is None else args.device
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     import _swpkg
     sw = _swpkg.load()
@@ -118,7 +125,7 @@ def main():
     q = sw.encode(read_query(args.query))
     log("rank %d: shard %d subjects, %d residues, generated in %.1fs" % (rank, n, residues, time.perf_counter() - t0))
 
-    handle = sw.Handle(local)
+    handle = sw.Handle(gpu)
     # The library launches on a torch stream (not the legacy null stream,
     # whose handle is 0 = "library-owned stream" for sw_set_stream), so the
     # scan is stream-ordered with the top-K ops that read its scores.
@@ -131,19 +138,25 @@ def main():
     log("rank %d: packed + uploaded in %.1fs: %s" % (rank, time.perf_counter() - t0, st))
 
     scores = torch.zeros(n, dtype=torch.int32, device=dev)
-    gid = torch.arange(n, dtype=torch.int64, device=dev) + rank * n
     K = min(args.topk, n)
+    top = torch.empty(K, dtype=torch.int64, device=dev)
     gathered = torch.empty(world * K, dtype=torch.int64, device=dev)
+    final = torch.empty(K, dtype=torch.int64, device=dev)
 
     def step():
         db.scan_device(q, scores.data_ptr())
-        # key orders (score desc, global id asc); ids < 2^31
-        key = (scores.to(torch.int64) << 32) | ((1 << 31) - 1 - gid)
-        top = torch.topk(key, K, sorted=False).values
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, top)
-            return torch.topk(gathered, K).values
-        return torch.topk(top, K).values
+        # device top-K: int64 keys (score << 32 | 2^31-1-global id), best first
+        handle.topk_device(scores.data_ptr(), n, K, top.data_ptr(), id_base=rank * n)
+        if world == 1:
+            return top
+        if args.backend == "nccl":
+            dist.all_gather_into_tensor(gathered, top)  # RCCL over xGMI: K x 8 B per rank
+        else:
+            parts = [torch.empty(K, dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(parts, top.cpu())
+            gathered.copy_(torch.cat(parts))
+        handle.topk_keys_device(gathered.data_ptr(), world * K, K, final.data_ptr())
+        return final
 
     for _ in range(args.warmup):
         step()
@@ -164,7 +177,8 @@ def main():
 
     cells_rank = float(len(q)) * residues
     if world > 1:
-        t = torch.tensor([elapsed, cells_rank], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, cells_rank], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -172,9 +186,7 @@ def main():
     else:
         elapsed_max, cells_all = elapsed, cells_rank
 
-    # check one step's scores against themselves across the run (determinism)
-    top_ids = ((1 << 31) - 1 - (final & 0xFFFFFFFF)).cpu().numpy()
-    top_scores = (final >> 32).cpu().numpy()
+    top_ids, top_scores = sw.capi.decode_keys(final.cpu().numpy())
 
     if rank == 0:
         value = cells_all * args.steps / elapsed_max / 1e9
@@ -233,7 +245,7 @@ def main():
                               "peak": round(VALU_PEAK_TOPS, 2), "unit": "T lane-ops/s",
                               "frac": round(inter_gcups * INTER_OPS_PER_CELL / 1e3 / VALU_PEAK_TOPS, 4),
                               "inter_gcups": round(inter_gcups, 1), "ops_per_cell": INTER_OPS_PER_CELL},
-            "top_hit": {"id": int(top_ids[np.argmax(top_scores)]), "score": int(top_scores.max())},
+            "top_hit": {"id": int(top_ids[0]), "score": int(top_scores[0])},
         }
         if not args.no_cpu_baseline and world == 1:
             gs = scores.cpu().numpy()

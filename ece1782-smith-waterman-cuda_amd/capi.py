@@ -26,7 +26,7 @@ EXPORTED = (
     "sw_db_create", "sw_db_free", "sw_db_get_stats", "sw_db_set_long_threshold",
     "sw_scan", "sw_scan_device", "sw_scan_batch", "sw_get_timing",
     "sw_timing_reset", "sw_timing_total",
-    "sw_topk", "sw_score_pair",
+    "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_score_pair",
 )
 
 
@@ -64,6 +64,16 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise SWError("HIP library %s not built; run __graft_entry__.build() "
                       "or make -C ece1782-smith-waterman-cuda_amd/csrc" % LIB_PATH)
+    # One HIP runtime per process: PyTorch-ROCm bundles its own
+    # libamdhip64.so with the same SONAME (libamdhip64.so.7) as /opt/rocm's.
+    # Imported first, it is the runtime our library binds to, and streams can
+    # be shared; loaded after us it would start a second runtime that cannot
+    # see the GPU.  (PyTorch is plumbing here, not a dependency: without it
+    # the library uses the system runtime.)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -89,6 +99,8 @@ def lib():
         "sw_timing_reset": (ctypes.c_int, [vp]),
         "sw_timing_total": (ctypes.c_int, [vp, ctypes.POINTER(Timing), i32p]),
         "sw_topk": (ctypes.c_int, [i32p, i64, i32, i32p, i32p]),
+        "sw_topk_device": (ctypes.c_int, [vp, vp, i64, i64, i32, vp]),
+        "sw_topk_keys_device": (ctypes.c_int, [vp, vp, i64, i32, vp]),
         "sw_score_pair": (ctypes.c_int, [vp, u8p, i32, u8p, i32, ctypes.POINTER(Scoring), i32p]),
     }
     for name, (res, args) in sig.items():
@@ -189,6 +201,15 @@ class Handle:
         return {"inter_ms": t.inter_ms, "intra_ms": t.intra_ms, "total_ms": t.total_ms,
                 "launches": t.launches, "scans": n.value}
 
+    def topk_device(self, scores_dev_ptr, n, k, keys_out_dev_ptr, id_base=0):
+        """Asynchronous device top-k into an int64 key buffer (best first)."""
+        _check(lib().sw_topk_device(self._h, ctypes.c_void_p(scores_dev_ptr), n, id_base, k,
+                                    ctypes.c_void_p(keys_out_dev_ptr)))
+
+    def topk_keys_device(self, keys_dev_ptr, n, k, keys_out_dev_ptr):
+        _check(lib().sw_topk_keys_device(self._h, ctypes.c_void_p(keys_dev_ptr), n, k,
+                                         ctypes.c_void_p(keys_out_dev_ptr)))
+
     def score_pair(self, query_codes, subject_codes, matrix=None, gap_open=2, gap_extend=None):
         q, qp = _u8(query_codes)
         s, sp = _u8(subject_codes)
@@ -286,3 +307,12 @@ def topk(scores, k):
                          ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
                          vals.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
     return ids, vals
+
+
+def decode_keys(keys):
+    """int64 top-k keys -> (ids, scores); INT64_MIN padding -> id -1, score 0."""
+    keys = np.asarray(keys, dtype=np.int64)
+    valid = keys != np.iinfo(np.int64).min
+    ids = np.where(valid, ((1 << 31) - 1) - (keys & 0xFFFFFFFF), -1)
+    scores = np.where(valid, keys >> 32, 0)
+    return ids.astype(np.int64), scores.astype(np.int64)

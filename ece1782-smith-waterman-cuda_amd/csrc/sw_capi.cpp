@@ -176,6 +176,8 @@ struct sw_handle {
     bool prof_pending = false;
     int32_t* d_scores = nullptr;  // for the synchronous sw_scan
     size_t scores_cap = 0;
+    int64_t* d_topk_work = nullptr;  // device top-K workspace
+    size_t topk_cap = 0;
     bool timed = false;
     bool had_intra = false;
     int launches = 0;
@@ -632,6 +634,27 @@ int ensure_scores(sw_handle* h, size_t n) {
 
 }  // namespace
 
+namespace {
+int topk_impl(sw_handle* h, const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, int32_t k,
+              int64_t* out) {
+    if (!h || !out || n < 0 || k <= 0 || k > 4096 || (n > 0 && !scores && !keys))
+        return fail(SW_E_INVALID, "bad top-k arguments (1 <= k <= 4096)");
+    if (id_base < 0 || id_base + n > (int64_t(1) << 31)) return fail(SW_E_INVALID, "ids must fit in 31 bits");
+    HIPCHECK(hipSetDevice(h->device));
+    const size_t need = swk::topk_workspace_bytes(n, k);
+    if (need > h->topk_cap) {
+        if (h->d_topk_work) {
+            HIPCHECK(hipStreamSynchronize(h->stream));
+            HIPCHECK(hipFree(h->d_topk_work));
+        }
+        h->topk_cap = std::max<size_t>(need, 1 << 20);
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&h->d_topk_work), h->topk_cap));
+    }
+    HIPCHECK(swk::launch_topk(scores, keys, n, id_base, k, out, h->d_topk_work, h->stream));
+    return SW_OK;
+}
+}  // namespace
+
 // ===========================================================================
 extern "C" {
 
@@ -696,6 +719,7 @@ int sw_destroy(sw_handle* h) {
     if (h->h_prof) (void)hipHostFree(h->h_prof);
     if (h->prof_copied) (void)hipEventDestroy(h->prof_copied);
     if (h->d_scores) (void)hipFree(h->d_scores);
+    if (h->d_topk_work) (void)hipFree(h->d_topk_work);
     if (h->side) (void)hipStreamDestroy(h->side);
     if (h->side2) (void)hipStreamDestroy(h->side2);
     if (h->coop_done) (void)hipEventDestroy(h->coop_done);
@@ -892,6 +916,15 @@ int sw_topk(const int32_t* scores, int64_t n, int32_t k, int32_t* out_ids, int32
         out_scores[i] = 0;
     }
     return SW_OK;
+}
+
+int sw_topk_device(sw_handle* h, const int32_t* scores_dev, int64_t n, int64_t id_base, int32_t k,
+                   int64_t* keys_out_dev) {
+    return topk_impl(h, scores_dev, nullptr, n, id_base, k, keys_out_dev);
+}
+
+int sw_topk_keys_device(sw_handle* h, const int64_t* keys_dev, int64_t n, int32_t k, int64_t* keys_out_dev) {
+    return topk_impl(h, nullptr, keys_dev, n, 0, k, keys_out_dev);
 }
 
 int sw_score_pair(sw_handle* h, const uint8_t* query, int32_t qlen, const uint8_t* subject, int32_t slen,

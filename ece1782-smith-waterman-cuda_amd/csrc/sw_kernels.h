@@ -112,4 +112,9 @@ constexpr int kSat16 = 32767 - 1152;
 hipError_t launch_inter_rescue(const InterArgs& a, hipStream_t s);
 hipError_t launch_intra(const IntraArgs& a, int ri, bool affine, hipStream_t s);
 
+// Device top-K (sw_topk.hip): keys = score << 32 | (2^31 - 1 - id), best first.
+size_t topk_workspace_bytes(int64_t n, int k);
+hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, int k,
+                       int64_t* out, int64_t* work, hipStream_t s);
+
 }  // namespace swk

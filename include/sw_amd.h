@@ -38,6 +38,13 @@
 extern "C" {
 #endif
 
+/* libswamd.so is built with -fvisibility=hidden; only these are exported. */
+#if defined(SW_AMD_BUILD)
+#define SW_API __attribute__((visibility("default")))
+#else
+#define SW_API
+#endif
+
 #define SW_OK 0
 #define SW_E_INVALID -1   /* bad argument */
 #define SW_E_HIP -2       /* HIP runtime error (see sw_last_error) */
@@ -85,20 +92,20 @@ typedef struct sw_handle sw_handle;
 typedef struct sw_db sw_db;
 
 /* ---- housekeeping ---------------------------------------------------- */
-int32_t sw_version(void);                         /* 10000*major + 100*minor + patch */
-const char* sw_last_error(void);                  /* thread-local text of the last failure */
-int sw_encode(const char* ascii, int64_t n, uint8_t* codes);    /* SWSolver.cu:91-120 */
-int sw_builtin_matrix(int32_t id, int8_t* out625);               /* SWSolver.cu:54-81 */
+SW_API int32_t sw_version(void);                         /* 10000*major + 100*minor + patch */
+SW_API const char* sw_last_error(void);                  /* thread-local text of the last failure */
+SW_API int sw_encode(const char* ascii, int64_t n, uint8_t* codes);    /* SWSolver.cu:91-120 */
+SW_API int sw_builtin_matrix(int32_t id, int8_t* out625);               /* SWSolver.cu:54-81 */
 
 /* ---- device context ---------------------------------------------------
  * Replaces the reference's implicit CUDA context + default stream
  * (SWSolver.cu:282-288 allocations, :349/:381 synchronisations).        */
-int sw_create(int32_t device, sw_handle** out);
-int sw_destroy(sw_handle* h);
+SW_API int sw_create(int32_t device, sw_handle** out);
+SW_API int sw_destroy(sw_handle* h);
 /* The handle's HIP stream (hipStream_t), e.g. to record events on it. */
-void* sw_stream(sw_handle* h);
+SW_API void* sw_stream(sw_handle* h);
 /* Use an external stream (e.g. torch's current stream); NULL = own stream. */
-int sw_set_stream(sw_handle* h, void* hip_stream);
+SW_API int sw_set_stream(sw_handle* h, void* hip_stream);
 
 /* ---- database -----------------------------------------------------------
  * Replaces the per-call packing loop SWSolver.cu:301-371 (longest-first
@@ -107,56 +114,66 @@ int sw_set_stream(sw_handle* h, void* hip_stream);
  *   residues : encoded subject residues, concatenated
  *   offsets  : n+1 offsets into residues (offsets[0] = 0)
  *   ids      : n result ids (NULL = 0..n-1); sw_scan writes scores[id]   */
-int sw_db_create(sw_handle* h, const uint8_t* residues, const int64_t* offsets,
+SW_API int sw_db_create(sw_handle* h, const uint8_t* residues, const int64_t* offsets,
                  int64_t n, const int32_t* ids, sw_db** out);
-int sw_db_free(sw_db* db);
-int sw_db_get_stats(const sw_db* db, sw_db_stats* out);
+SW_API int sw_db_free(sw_db* db);
+SW_API int sw_db_get_stats(const sw_db* db, sw_db_stats* out);
 /* Subjects longer than `threshold` go to the intra-sequence kernel
  * (default chosen at sw_db_create; 0 = library default).  Must be called
  * before the first scan. */
-int sw_db_set_long_threshold(sw_db* db, int32_t threshold);
+SW_API int sw_db_set_long_threshold(sw_db* db, int32_t threshold);
 
 /* ---- scans ---------------------------------------------------------------
  * Replaces smith_waterman_cuda (SWSolver.cu:266-404): score the encoded
  * query against every subject; scores[id] = best local score.  The output
  * array must hold max(id)+1 int32; slots no subject maps to are set to 0.
  * Synchronous.                                                            */
-int sw_scan(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen,
+SW_API int sw_scan(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen,
             const sw_scoring* sc, int32_t* scores_host);
 
 /* Same, asynchronous on the handle's stream, scores written to DEVICE memory
  * (scores_dev; only slots that some subject maps to are written).  Used by
  * bench.py with the database already resident.  The handle must outlive the
  * database: sw_db_free uses the handle's stream.                          */
-int sw_scan_device(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen,
+SW_API int sw_scan_device(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen,
                    const sw_scoring* sc, int32_t* scores_dev);
 
 /* Batch of nq queries (concatenated encoded residues, nq+1 offsets);
  * scores_host is [nq][max(id)+1].  Consecutive queries overlap on the
  * device (main.cpp handles one query per run).     */
-int sw_scan_batch(sw_handle* h, const sw_db* db, const uint8_t* queries,
+SW_API int sw_scan_batch(sw_handle* h, const sw_db* db, const uint8_t* queries,
                   const int64_t* qoffsets, int32_t nq, const sw_scoring* sc,
                   int32_t* scores_host);
 
 /* Timing of the most recent scan on this handle (waits for it). */
-int sw_get_timing(sw_handle* h, sw_timing* out);
+SW_API int sw_get_timing(sw_handle* h, sw_timing* out);
 /* Kernel times summed over every scan since the last reset (waits for them);
  * *nscans = number of scans summed.  Lets a caller time many back-to-back
  * scans with HIP events on the stream they ran on, without synchronising
  * between them (bench.py).                                               */
-int sw_timing_reset(sw_handle* h);
-int sw_timing_total(sw_handle* h, sw_timing* out, int32_t* nscans);
+SW_API int sw_timing_reset(sw_handle* h);
+SW_API int sw_timing_total(sw_handle* h, sw_timing* out, int32_t* nscans);
 
 /* ---- ranking ---------------------------------------------------------------
  * Top-k of a score vector (score descending, id ascending on ties).
  * Host-side helper for the multi-GPU top-K exchange.     */
-int sw_topk(const int32_t* scores, int64_t n, int32_t k, int32_t* out_ids,
+SW_API int sw_topk(const int32_t* scores, int64_t n, int32_t k, int32_t* out_ids,
             int32_t* out_scores);
+
+/* Device top-k, asynchronous on the handle's stream: the k best of
+ * scores_dev[0..n) as int64 keys  score << 32 | (2^31 - 1 - (id_base + i)),
+ * best first (score descending, id ascending); missing entries (n < k) are
+ * INT64_MIN.  1 <= k <= 4096.  sw_topk_keys_device merges key vectors
+ * (e.g. the all-gathered per-rank top-k of the multi-GPU exchange).        */
+SW_API int sw_topk_device(sw_handle* h, const int32_t* scores_dev, int64_t n, int64_t id_base,
+                   int32_t k, int64_t* keys_out_dev);
+SW_API int sw_topk_keys_device(sw_handle* h, const int64_t* keys_dev, int64_t n, int32_t k,
+                        int64_t* keys_out_dev);
 
 /* ---- single pair ---------------------------------------------------------
  * One query against one subject on the GPU (wavefront kernel); the GPU
  * analogue of the cpu.cpp pair program's score (cpu.cpp:43-74).         */
-int sw_score_pair(sw_handle* h, const uint8_t* query, int32_t qlen,
+SW_API int sw_score_pair(sw_handle* h, const uint8_t* query, int32_t qlen,
                   const uint8_t* subject, int32_t slen, const sw_scoring* sc,
                   int32_t* score);
 

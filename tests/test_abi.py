@@ -14,7 +14,14 @@ from conftest import REPO
 def declared_functions():
     src = open(os.path.join(REPO, "include", "sw_amd.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|int32_t|void\s*\*|const char\s*\*)\s*(sw_\w+)\s*\(", src, re.M)))
+    pat = r"^\s*(?:SW_API\s+)?(?:int|int32_t|void\s*\*|const char\s*\*)\s*(sw_\w+)\s*\("
+    return sorted(set(re.findall(pat, src, re.M)))
+
+
+def test_only_the_c_abi_is_exported(sw):
+    out = subprocess.run(["nm", "-D", "--defined-only", sw.capi.LIB_PATH], capture_output=True, text=True).stdout
+    text = [ln.split()[-1] for ln in out.splitlines() if " T " in ln]
+    assert sorted(text) == declared_functions()
 
 
 def test_header_symbols_exported(sw):

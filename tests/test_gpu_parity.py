@@ -147,3 +147,34 @@ def test_int16_saturation_rescue(sw, oracle, handle, reps):
     want = oracle.scan(q, res, offs)
     assert got[37] == 15 * reps
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("n,k", [(10, 4), (5000, 100), (100000, 100), (300000, 1000), (7, 20)])
+def test_device_topk(sw, handle, n, k):
+    """sw_topk_device and the multi-rank merge (sw_topk_keys_device):
+    score descending, id ascending, against numpy."""
+    import torch
+    rng = np.random.default_rng(n + k)
+    s = rng.integers(0, 60, size=n).astype(np.int32)   # many ties
+    order = np.lexsort((np.arange(n), -s))[:k]
+    m = min(n, k)
+    d = torch.from_numpy(s).cuda()
+    out = torch.empty(k, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    handle.topk_device(d.data_ptr(), n, k, out.data_ptr(), id_base=1000)
+    torch.cuda.synchronize()
+    ids, sc = sw.capi.decode_keys(out.cpu().numpy())
+    assert ids[:m].tolist() == (order[:m] + 1000).tolist()
+    assert sc[:m].tolist() == s[order[:m]].tolist()
+    assert (ids[m:] == -1).all()
+    # two "ranks": top-k of each half, all-gathered, merged == top-k of all
+    h = n // 2
+    parts = torch.empty(2 * k, dtype=torch.int64, device="cuda")
+    handle.topk_device(d.data_ptr(), h, k, parts.data_ptr(), id_base=0)
+    handle.topk_device(d[h:].data_ptr(), n - h, k, parts[k:].data_ptr(), id_base=h)
+    merged = torch.empty(k, dtype=torch.int64, device="cuda")
+    handle.topk_keys_device(parts.data_ptr(), 2 * k, k, merged.data_ptr())
+    torch.cuda.synchronize()
+    ids2, sc2 = sw.capi.decode_keys(merged.cpu().numpy())
+    assert ids2[:m].tolist() == order[:m].tolist()
+    assert sc2[:m].tolist() == s[order[:m]].tolist()
