@@ -5,7 +5,11 @@ Workload (BASELINE.json configs[1]): the 375-residue
 query P07327 (data/queries/P07327.fasta of the reference, shipped as a fixture)
 against a Swiss-Prot-sized synthetic database (570,000 subjects, log-normal
 lengths median 290 / mean ~360, Swiss-Prot residue frequencies; Swiss-Prot
-itself is not available here), BLOSUM50 of SWSolver.cu:54-81, linear gap 2.
+itself is not available here), scored as configs[1] states: BLOSUM62 with
+affine gaps, BLAST's default 11/1 (a gap of k residues costs 11 + k, i.e.
+gap_open 12 and gap_extend 1 in this library's convention).  The reference's
+own scoring (BLOSUM50 of SWSolver.cu:54-81, linear gap 2) is timed the same
+way right after and reported under "reference_scoring".
 
 One step = one pass of the hot path over the rank's resident shard: build the
 query profile, run the intra-sequence kernel (subjects longer than the long
@@ -32,8 +36,22 @@ sys.path.insert(0, REPO)
 
 METRIC = "GCUPS (DP cell updates/s) query-vs-SwissProt, 1/2/4/8 MI355X; bit-exact scores"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T lane-ops/s
-INTER_OPS_PER_CELL = 3.5        # v_add_sdwa + v_max3 + v_sub clamp + 1/2 v_max3 (running max)
+SIMDS, CLOCK_HZ = 1024, 2.4e9   # 256 CUs x 4 SIMDs
+# VALU issue model of each per-wave inter kernel: SIMD cycles per DP cell,
+# from the compiled inner loop's instruction counts (hipcc -S) priced at the
+# measured gfx950 issue costs (profiles/r01_valu_rate_*.txt: v_sub_u32 clamp
+# 2.45, v_max_i32 4.37, v_max3_i32 4.4, v_add_u32_sdwa 4.2, v_pk_* 4.25,
+# v_or_b32 2.7 cycles per wave64 instruction).
+VALU_MODEL = {
+    # per 2 x 64 cells: 4.83 v_pk_max_i16, 2.83 v_pk_sub_u16, 1 v_pk_add_u16, 1 v_or_b32
+    "sw_inter_x2<32,8,affine>": ((4.83 + 2.83 + 1) * 4.25 + 2.7) / 128,
+    "sw_inter_x2<16,16,affine>": ((4.87 + 2.87 + 1) * 4.25 + 2.7) / 128,
+    # per 64 cells: 1.5 v_max3, 1 v_add_sdwa, 1 v_sub clamp
+    "sw_inter<64,8,linear>": (1.5 * 4.4 + 4.2 + 2.45) / 64,
+    # per 64 cells: 2.82 v_sub clamp, 1.83 v_max, 1.5 v_max3, 1 v_add_sdwa
+    "sw_inter<32,8,affine>": (2.82 * 2.45 + 1.83 * 4.37 + 1.5 * 4.4 + 4.2) / 64,
+}
+MATRICES = {"blosum50": 0, "blosum62": 1}
 
 
 def log(*a):
@@ -45,9 +63,29 @@ def read_query(name):
         return "".join(f.read().split("\n")[1:])
 
 
-def cpu_baseline(sw, q, res, offs, gpu_scores, seconds, threads):
-    """The oracle (C restatement of cpu.cpp's recurrence, kind "port") on a
-    bounded random sample of the same shard, on this host's cores."""
+def workload_key(args, qlen):
+    return "%s/%d/%d/%s-%d-%d" % (args.query, args.db_seqs, qlen, args.matrix, args.gap_open, args.gap_extend)
+
+
+def valu_roofline(kernel, cells_rank, scan_ms, kernel_gcups):
+    """The binding roofline: VALU instruction issue.  peak = the modeled
+    issue-bound rate of the per-wave inter kernel (VALU_MODEL), achieved =
+    the whole scan's rate (all kernels of the scan, concurrent)."""
+    cpc = VALU_MODEL.get(kernel)
+    if cpc is None or scan_ms <= 0:
+        return None
+    peak = SIMDS * CLOCK_HZ / cpc / 1e9
+    achieved = cells_rank / (scan_ms * 1e-3) / 1e9
+    return {"bound": "valu-issue", "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "GCUPS",
+            "frac": round(achieved / peak, 4), "kernel": kernel, "simd_cycles_per_cell": round(cpc, 5),
+            "kernel_alone_gcups_while_concurrent": round(kernel_gcups, 1)}
+
+
+def cpu_baseline(sw, q, res, offs, gpu_scores, seconds, threads, scoring):
+    """The oracle (C restatement of cpu.cpp's recurrence, Gotoh for affine;
+    kind "port") on a bounded random sample of the same shard, on this host's
+    cores, with the same scoring as the GPU run."""
+    mat, go, ge = scoring
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import sw_oracle
     n = len(offs) - 1
@@ -65,12 +103,12 @@ def cpu_baseline(sw, q, res, offs, gpu_scores, seconds, threads):
     # calibrate on a small sample, then size the real one to ~`seconds`
     idx, sr, so = sample(min(n, 2000))
     t = time.perf_counter()
-    sw_oracle.scan(q, sr, so, nthreads=threads)
+    sw_oracle.scan(q, sr, so, mat=mat, gap_open=go, gap_extend=ge, nthreads=threads)
     dt = max(time.perf_counter() - t, 1e-3)
     m = int(min(n, max(2000, 2000 * seconds / dt)))
     idx, sr, so = sample(m)
     t = time.perf_counter()
-    cpu = sw_oracle.scan(q, sr, so, nthreads=threads)
+    cpu = sw_oracle.scan(q, sr, so, mat=mat, gap_open=go, gap_extend=ge, nthreads=threads)
     dt = time.perf_counter() - t
     cells = len(q) * int(so[-1])
     parity = bool(np.array_equal(cpu, gpu_scores[idx]))
@@ -88,6 +126,11 @@ def main():
     ap.add_argument("--db-seqs", type=int, default=570000, help="subjects per rank")
     ap.add_argument("--query", default="P07327")
     ap.add_argument("--topk", type=int, default=100)
+    ap.add_argument("--matrix", default="blosum62", choices=sorted(MATRICES))
+    ap.add_argument("--gap-open", type=int, default=12, help="cost of a 1-residue gap (BLAST 11/1 -> 12)")
+    ap.add_argument("--gap-extend", type=int, default=1)
+    ap.add_argument("--no-reference-scoring", action="store_true",
+                    help="skip the second timed loop with the reference's BLOSUM50 / linear 2")
     ap.add_argument("--long-threshold", type=int, default=0, help="0 = library default")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -143,8 +186,11 @@ def main():
     gathered = torch.empty(world * K, dtype=torch.int64, device=dev)
     final = torch.empty(K, dtype=torch.int64, device=dev)
 
+    mat = sw.capi.builtin_matrix(MATRICES[args.matrix])
+    scoring = (mat, args.gap_open, args.gap_extend)
+
     def step():
-        db.scan_device(q, scores.data_ptr())
+        db.scan_device(q, scores.data_ptr(), *scoring)
         # device top-K: int64 keys (score << 32 | 2^31-1-global id), best first
         handle.topk_device(scores.data_ptr(), n, K, top.data_ptr(), id_base=rank * n)
         if world == 1:
@@ -158,35 +204,55 @@ def main():
         handle.topk_keys_device(gathered.data_ptr(), world * K, K, final.data_ptr())
         return final
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    handle.timing_reset()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        final = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    kt = handle.timing_total()
-
     cells_rank = float(len(q)) * residues
-    if world > 1:
-        t = torch.tensor([elapsed, cells_rank], dtype=torch.float64,
-                         device=dev if args.backend == "nccl" else "cpu")
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        elapsed_max, cells_all = float(tmax[0]), float(t[1])
-    else:
-        elapsed_max, cells_all = elapsed, cells_rank
 
-    top_ids, top_scores = sw.capi.decode_keys(final.cpu().numpy())
+    def timed_loop():
+        """W untimed steps, then K timed steps between barrier + sync pairs;
+        returns (max-over-ranks seconds, all ranks' cells per step, kernel
+        timing, name of the per-wave inter kernel)."""
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        handle.timing_reset()
+        t_start = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t_start
+        kt = handle.timing_total()
+        if world > 1:
+            t = torch.tensor([elapsed, cells_rank], dtype=torch.float64,
+                             device=dev if args.backend == "nccl" else "cpu")
+            tmax = t.clone()
+            dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            return float(tmax[0]), float(t[1]), kt, handle.last_kernel()
+        return elapsed, cells_rank, kt, handle.last_kernel()
+
+    elapsed_max, cells_all, kt, kernel = timed_loop()
+    st = db.stats()  # the coop split of the timed scans
+    final_keys = (final if world > 1 else top).cpu().numpy()
+    top_ids, top_scores = sw.capi.decode_keys(final_keys)
+    gs = scores.cpu().numpy() if (not args.no_cpu_baseline and world == 1 and rank == 0) else None
+
+    ref = None
+    if not args.no_reference_scoring:
+        scoring = (sw.capi.builtin_matrix(0), 2, 2)  # SWSolver.cu:54-81, GAP_PENALTY 2 (:7)
+        r_elapsed, r_cells, r_kt, r_kernel = timed_loop()
+        r_n = max(r_kt["scans"], 1)
+        ref = {"scoring": "BLOSUM50 (SWSolver.cu:54-81), linear gap 2 (the reference's own)",
+               "value": round(r_cells * args.steps / r_elapsed / 1e9, 2), "unit": "GCUPS",
+               "ms_per_step": round(r_elapsed * 1e3 / args.steps, 3), "kernel": r_kernel,
+               "kernel_ms": {"sw_inter": round(r_kt["wave_ms"] / r_n, 4),
+                             "sw_inter_coop": round(r_kt["coop_ms"] / r_n, 4),
+                             "sw_intra": round(r_kt["intra_ms"] / r_n, 4),
+                             "scan_total": round(r_kt["total_ms"] / r_n, 4)}}
 
     if rank == 0:
         value = cells_all * args.steps / elapsed_max / 1e9
@@ -194,21 +260,27 @@ def main():
         nsc = max(kt["scans"], 1)
         inter_ms = kt["inter_ms"] / nsc
         intra_ms = kt["intra_ms"] / nsc
-        # dominant kernel: inter-sequence.  Algorithmic bytes per launch
-        # (SURVEY.md §8d): 1 B per residue it scans + 12 B per subject
-        # (offset, length, int32 score).
+        wave_ms = kt["wave_ms"] / nsc
+        coop_ms = kt["coop_ms"] / nsc
+        # Dominant kernel: the per-wave inter-sequence kernel (most of the
+        # cells; the cooperative kernel takes the widest blocks beside it on
+        # another stream, the intra kernel the long subjects).
+        # Its duration is HIP events around its launch on its own stream.
+        # Algorithmic bytes per launch: 1 B per residue it
+        # scans + 12 B per subject (offset, length, int32 score).
+        lens_desc = np.sort(offs[1:] - offs[:-1])[::-1]
         n_inter = n - st["n_long"]
-        inter_res = residues - int(sum(
-            np.sort(offs[1:] - offs[:-1])[::-1][:st["n_long"]])) if st["n_long"] else residues
-        alg_bytes = inter_res + 12 * n_inter
-        achieved = alg_bytes / (inter_ms * 1e-3) / 1e9 if inter_ms > 0 else 0.0
-        inter_cells = float(len(q)) * inter_res
-        inter_gcups = inter_cells / (inter_ms * 1e-3) / 1e9 if inter_ms > 0 else 0.0
+        inter_res = residues - int(lens_desc[:st["n_long"]].sum())
+        n_coop = min(st["coop_blocks"] * 64, n_inter)
+        wave_res = inter_res - st["coop_residues"]
+        alg_bytes = wave_res + 12 * (n_inter - n_coop)
+        achieved = alg_bytes / (wave_ms * 1e-3) / 1e9 if wave_ms > 0 else 0.0
+        wave_gcups = float(len(q)) * wave_res / (wave_ms * 1e-3) / 1e9 if wave_ms > 0 else 0.0
         traffic = None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("workload_key") == "%s/%d/%d" % (args.query, args.db_seqs, len(q)):
+            if tj.get("workload_key") == workload_key(args, len(q)) and tj.get("kernel") == kernel:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -227,30 +299,35 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": "C2: query %s (%d aa) vs synthetic Swiss-Prot-sized db, %d subjects/rank "
-                            "(%d residues/rank), BLOSUM50 (SWSolver.cu:54-81), linear gap 2, top-%d "
-                            "all-gathered" % (args.query, len(q), n, residues, K),
+                            "(%d residues/rank), %s, gap open %d / extend %d (BLAST 11/1), top-%d "
+                            "all-gathered" % (args.query, len(q), n, residues, args.matrix.upper(),
+                                              args.gap_open, args.gap_extend, K),
+                "scoring": {"matrix": args.matrix, "gap_open": args.gap_open, "gap_extend": args.gap_extend},
                 "query": args.query, "query_len": int(len(q)), "subjects_per_rank": n,
                 "residues_per_rank": residues, "parallelism": "db-shard x%d + RCCL allgather top-K" % world,
                 "long_threshold": st["long_threshold"], "long_subjects": st["n_long"],
                 "cells_per_step": cells_all,
             },
-            "kernel_ms": {"inter": round(inter_ms, 4), "intra": round(intra_ms, 4),
+            "kernel_ms": {"inter_phase": round(inter_ms, 4), "sw_inter": round(wave_ms, 4),
+                          "sw_inter_coop": round(coop_ms, 4), "sw_intra": round(intra_ms, 4),
                           "scan_total": round(kt["total_ms"] / nsc, 4)},
+            "cells_split": {"sw_inter": float(len(q)) * wave_res,
+                            "sw_inter_coop": float(len(q)) * st["coop_residues"],
+                            "sw_intra": float(len(q)) * (residues - inter_res)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": traffic,
-                         "kernel": "sw_inter (inter-sequence, linear gap)",
-                         "alg_bytes_per_launch": alg_bytes},
-            "valu_roofline": {"bound": "valu-int32", "achieved": round(inter_gcups * INTER_OPS_PER_CELL / 1e3, 3),
-                              "peak": round(VALU_PEAK_TOPS, 2), "unit": "T lane-ops/s",
-                              "frac": round(inter_gcups * INTER_OPS_PER_CELL / 1e3 / VALU_PEAK_TOPS, 4),
-                              "inter_gcups": round(inter_gcups, 1), "ops_per_cell": INTER_OPS_PER_CELL},
+                         "kernel": kernel,
+                         "alg_bytes_per_launch": int(alg_bytes), "kernel_ms": round(wave_ms, 4)},
+            "valu_roofline": valu_roofline(kernel, cells_all / world, kt["total_ms"] / nsc, wave_gcups),
             "top_hit": {"id": int(top_ids[0]), "score": int(top_scores[0])},
         }
-        if not args.no_cpu_baseline and world == 1:
-            gs = scores.cpu().numpy()
+        if ref is not None:
+            out["reference_scoring"] = ref
+        if gs is not None:
             threads = min(args.cpu_threads, os.cpu_count() or 1)
-            cb, parity = cpu_baseline(sw, q, res, offs, gs, args.cpu_seconds, threads)
+            cb, parity = cpu_baseline(sw, q, res, offs, gs, args.cpu_seconds, threads, scoring=(mat, args.gap_open,
+                                                                                              args.gap_extend))
             out["cpu_baseline"] = cb
             out["parity_sample_ok"] = parity
         print(json.dumps(out), flush=True)

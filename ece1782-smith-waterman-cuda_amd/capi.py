@@ -25,7 +25,7 @@ EXPORTED = (
     "sw_create", "sw_destroy", "sw_stream", "sw_set_stream",
     "sw_db_create", "sw_db_free", "sw_db_get_stats", "sw_db_set_long_threshold",
     "sw_scan", "sw_scan_device", "sw_scan_batch", "sw_get_timing",
-    "sw_timing_reset", "sw_timing_total",
+    "sw_timing_reset", "sw_timing_total", "sw_last_kernel",
     "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_score_pair",
 )
 
@@ -44,13 +44,15 @@ class DbStats(ctypes.Structure):
     _fields_ = [("n_subjects", ctypes.c_int64), ("residues", ctypes.c_int64),
                 ("packed_cells", ctypes.c_int64), ("n_blocks", ctypes.c_int64),
                 ("n_long", ctypes.c_int64), ("device_bytes", ctypes.c_int64),
-                ("max_length", ctypes.c_int32), ("long_threshold", ctypes.c_int32)]
+                ("max_length", ctypes.c_int32), ("long_threshold", ctypes.c_int32),
+                ("coop_blocks", ctypes.c_int32), ("coop_residues", ctypes.c_int64)]
 
 
 class Timing(ctypes.Structure):
     _fields_ = [("inter_ms", ctypes.c_float), ("intra_ms", ctypes.c_float),
                 ("total_ms", ctypes.c_float), ("rescued", ctypes.c_int32),
-                ("launches", ctypes.c_int32)]
+                ("launches", ctypes.c_int32), ("coop_ms", ctypes.c_float),
+                ("wave_ms", ctypes.c_float)]
 
 
 _LIB = None
@@ -98,6 +100,7 @@ def lib():
         "sw_get_timing": (ctypes.c_int, [vp, ctypes.POINTER(Timing)]),
         "sw_timing_reset": (ctypes.c_int, [vp]),
         "sw_timing_total": (ctypes.c_int, [vp, ctypes.POINTER(Timing), i32p]),
+        "sw_last_kernel": (ctypes.c_char_p, [vp]),
         "sw_topk": (ctypes.c_int, [i32p, i64, i32, i32p, i32p]),
         "sw_topk_device": (ctypes.c_int, [vp, vp, i64, i64, i32, vp]),
         "sw_topk_keys_device": (ctypes.c_int, [vp, vp, i64, i32, vp]),
@@ -187,19 +190,23 @@ class Handle:
     def timing(self):
         t = Timing()
         _check(lib().sw_get_timing(self._h, ctypes.byref(t)))
-        return {"inter_ms": t.inter_ms, "intra_ms": t.intra_ms, "total_ms": t.total_ms,
-                "rescued": t.rescued, "launches": t.launches}
+        return {k: getattr(t, k) for k, _ in Timing._fields_}
 
     def timing_reset(self):
         _check(lib().sw_timing_reset(self._h))
+
+    def last_kernel(self):
+        """Per-wave inter kernel of the last scan, e.g. 'sw_inter_x2<16,16,affine>'."""
+        return lib().sw_last_kernel(self._h).decode()
 
     def timing_total(self):
         """Kernel ms summed over all scans since timing_reset(); waits."""
         t = Timing()
         n = ctypes.c_int32()
         _check(lib().sw_timing_total(self._h, ctypes.byref(t), ctypes.byref(n)))
-        return {"inter_ms": t.inter_ms, "intra_ms": t.intra_ms, "total_ms": t.total_ms,
-                "launches": t.launches, "scans": n.value}
+        out = {k: getattr(t, k) for k, _ in Timing._fields_ if k != "rescued"}
+        out["scans"] = n.value
+        return out
 
     def topk_device(self, scores_dev_ptr, n, k, keys_out_dev_ptr, id_base=0):
         """Asynchronous device top-k into an int64 key buffer (best first)."""

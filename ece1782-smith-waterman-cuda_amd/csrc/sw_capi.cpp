@@ -147,7 +147,10 @@ void parallel_for(int64_t n, F&& f) {
 
 // ---------------------------------------------------------------------------
 struct ScanEvents {
-    hipEvent_t ev[4] = {};  // start, after intra, after inter, end
+    // 0 fork, 1 intra done (side), 2 inter done (main), 3 end, and around
+    // each inter kernel on its own stream: 4/5 the cooperative kernel
+    // (side2), 6/7 the per-wave kernel (main)
+    hipEvent_t ev[8] = {};
     int launches = 0;
 };
 
@@ -177,6 +180,7 @@ struct sw_handle {
     int32_t* d_scores = nullptr;  // for the synchronous sw_scan
     size_t scores_cap = 0;
     int64_t* d_topk_work = nullptr;  // device top-K workspace
+    std::string last_kernel = "none";  // per-wave inter kernel of the last scan
     size_t topk_cap = 0;
     bool timed = false;
     bool had_intra = false;
@@ -202,6 +206,8 @@ struct sw_db {
     int32_t* d_bnd_f = nullptr;
     int32_t* d_rescue = nullptr;  // [count, block ids...] for the 16-bit kernel
     std::vector<uint32_t> h_blk_groups;  // block widths (16-column groups), widest first
+    std::vector<int64_t> h_blk_res;      // unpadded residues per block
+    int32_t last_ncoop = 0;              // blocks the last scan gave the coop kernel
     // intra part (long subjects)
     int64_t nlong = 0;
     int32_t long_max = 0;
@@ -294,6 +300,7 @@ int build_db(sw_db* db) {
     std::vector<uint64_t> blk_off(nblocks);
     std::vector<uint32_t> blk_groups(nblocks);
     std::vector<int32_t> lane_ids(nblocks * swk::kLanes, -1);
+    std::vector<int64_t> blk_res(nblocks, 0);  // unpadded residues per block
     uint64_t total = 0;
     for (int64_t b = 0; b < nblocks; ++b) {
         const int64_t first = nlong + b * swk::kLanes;  // longest subject of the block
@@ -311,6 +318,7 @@ int build_db(sw_db* db) {
             lane_ids[b * swk::kLanes + l] = db->h_ids[src];
             const uint8_t* p = db->h_residues.data() + db->h_offsets[src];
             const int64_t L = len(src);
+            blk_res[b] += L;
             for (int64_t j = 0; j < L; ++j)
                 res[blk_off[b] + (j / swk::kGroupCols) * swk::kGroupBytes + l * swk::kGroupCols +
                     (j % swk::kGroupCols)] = p[j];
@@ -329,6 +337,7 @@ int build_db(sw_db* db) {
     if ((rc = upload(&db->d_lid, lid, s, &acc))) return rc;
     HIPCHECK(hipStreamSynchronize(s));  // host vectors go out of scope
     db->h_blk_groups = blk_groups;
+    db->h_blk_res = blk_res;
     db->res_bytes = total;
     db->lres_bytes = ltotal;
     db->nblocks = nblocks;
@@ -469,8 +478,11 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
 // C2 (2.05e8 residues, profiles/r01_tune_coop.jsonl): width 384 with long
 // threshold 2048 is best, i.e. W ~ sum(residues) / 530000.  SW_COOP_WIDTH
 // overrides (tuning); 0 disables.
-int32_t coop_blocks(const sw_db* db) {
-    int64_t wmin = std::max<int64_t>(128, db->residues / 530000);
+int32_t coop_blocks(const sw_db* db, bool x2) {
+    // the packed kernel covers two blocks per wave, so its per-wave tail is
+    // shorter relative to the coop kernel's int32 cells: a wider cut-off
+    // (measured on C2: 1024 beats 386 and 640, profiles/r01_tune_x2.jsonl)
+    int64_t wmin = std::max<int64_t>(128, db->residues / (x2 ? 200000 : 530000));
     if (const char* e = std::getenv("SW_COOP_WIDTH")) wmin = std::atoll(e);
     if (wmin <= 0) return 0;
     int32_t n = 0;
@@ -512,34 +524,44 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     h->had_intra = false;
     if ((rc = next_events(h))) return rc;
 
-    const int R = swk::inter_rows(affine);
+    // The packed int16 kernel is exact when no H, E, F or H_diag + S can
+    // leave int16: H <= qlen * max S, plus one profile entry (+ gap bias).
+    int max_s = 0;
+    for (int k = 0; k < 625; ++k) max_s = std::max<int>(max_s, mat[k]);
+    const bool x2_ok = (static_cast<int64_t>(qlen) + 2) * (max_s + go) < 32767;
+    const int R = swk::inter_rows(affine, x2_ok);
     const int32_t qpad_inter = static_cast<int32_t>(round_up(qlen, R));
     const int ri = db->nlong ? swk::intra_rows_for(qlen, db->long_max) : 0;
     const int32_t qpad_intra = ri ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri)) : 0;
     // Empty query: every score is 0 (the reference's kernel leaves maxScore 0).
     if (qlen == 0) {
+        db->last_ncoop = 0;
+        h->last_kernel = "none";
         HIPCHECK(hipEventRecord(h->ev[0], h->stream));
         if (db->max_id >= 0)
             HIPCHECK(hipMemsetAsync(scores_dev, 0, static_cast<size_t>(db->max_id + 1) * 4, h->stream));
-        HIPCHECK(hipEventRecord(h->ev[1], h->stream));
-        HIPCHECK(hipEventRecord(h->ev[2], h->stream));
-        HIPCHECK(hipEventRecord(h->ev[3], h->stream));
+        for (int k = 1; k < 8; ++k) HIPCHECK(hipEventRecord(h->ev[k], h->stream));
         h->timed = true;
         return SW_OK;
     }
     Profiles P;
-    const bool p32 = swk::inter_profile32(affine);
-    const bool i16 = swk::inter_uses_16bit(affine);
+    const bool p32 = swk::inter_profile32(affine, x2_ok);
+    const bool i16 = swk::inter_uses_16bit(affine, x2_ok);
+    const bool x2 = swk::inter_uses_x2(affine, x2_ok);
     // the int32 rescue pass after a 16-bit kernel walks 64-row strips
     const int32_t qpad_rescue = i16 ? static_cast<int32_t>(round_up(qlen, 64)) : 0;
-    if ((rc = build_profiles(h, query, qlen, mat, go, affine, std::max(qpad_inter, qpad_rescue), i16, p32, ri,
-                             qpad_intra, &P)))
+    // widest blocks first, one cooperative workgroup each (int32, int8-profile paths)
+    const int32_t ncoop = (!i16 && !p32 && db->nblocks) ? coop_blocks(db, x2) : 0;
+    db->last_ncoop = ncoop;
+    const int32_t qpad_coop = ncoop ? static_cast<int32_t>(round_up(qlen, swk::inter_coop_rows())) : 0;
+    if ((rc = build_profiles(h, query, qlen, mat, go, affine, std::max({qpad_inter, qpad_rescue, qpad_coop}), i16 || x2,
+                             p32, ri, qpad_intra, &P)))
         return rc;
     if (i16 && db->nblocks && !db->d_rescue) {
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rescue), (db->nblocks + 1) * sizeof(int32_t)));
         db->device_bytes += (db->nblocks + 1) * sizeof(int32_t);
     }
-    const bool multi_inter = qpad_inter > R || qpad_rescue > 64;
+    const bool multi_inter = qpad_inter > R || qpad_rescue > 64 || qpad_coop > swk::inter_coop_rows();
     const bool multi_intra = ri && qpad_intra > swk::kLanes * ri;
     if ((multi_inter || multi_intra) && (rc = ensure_bnd(db, affine))) return rc;
 
@@ -572,7 +594,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         a.blk_groups = db->d_blk_groups;
         a.lane_ids = db->d_lane_ids;
         a.nblocks = static_cast<int32_t>(db->nblocks);
-        a.prof = h->d_prof + (i16 ? P.off16 : p32 ? P.off32 : P.off8);
+        a.prof = h->d_prof + ((i16 || x2) ? P.off16 : p32 ? P.off32 : P.off8);
         a.prof_stride = P.stride;
         a.qpad = qpad_inter;
         a.gap_open = go;
@@ -585,19 +607,26 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             a.rescue_list = db->d_rescue + 1;
             HIPCHECK(hipMemsetAsync(a.rescue_count, 0, sizeof(int32_t), h->stream));
         }
-        // widest blocks first, one cooperative workgroup each (linear int32 path)
-        const int32_t ncoop = (!affine && !i16 && !p32) ? coop_blocks(db) : 0;
         if (ncoop) {
             // on its own stream, so the per-wave kernel fills the GPU beside it
             swk::InterArgs c = a;
-            c.qpad = static_cast<int32_t>(round_up(qlen, swk::inter_coop_rows()));
+            c.qpad = qpad_coop;
+            c.prof = h->d_prof + P.off8;  // the coop kernel reads the int8 profile
             HIPCHECK(hipStreamWaitEvent(h->side2, h->ev[0], 0));
-            HIPCHECK(swk::launch_inter_coop(c, ncoop, h->side2));
+            HIPCHECK(hipEventRecord(h->ev[4], h->side2));
+            HIPCHECK(swk::launch_inter_coop(c, ncoop, affine, h->side2));
+            HIPCHECK(hipEventRecord(h->ev[5], h->side2));
             HIPCHECK(hipEventRecord(h->coop_done, h->side2));
             ++h->launches;
             a.blk_first = ncoop;
+        } else {
+            HIPCHECK(hipEventRecord(h->ev[4], h->stream));
+            HIPCHECK(hipEventRecord(h->ev[5], h->stream));
         }
-        HIPCHECK(swk::launch_inter(a, affine, h->stream));
+        HIPCHECK(hipEventRecord(h->ev[6], h->stream));
+        HIPCHECK(swk::launch_inter(a, affine, x2_ok, h->stream));
+        h->last_kernel = swk::inter_kernel_name(affine, x2_ok);
+        HIPCHECK(hipEventRecord(h->ev[7], h->stream));
         ++h->launches;
         if (ncoop) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
         if (i16) {
@@ -614,6 +643,8 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             ++h->launches;
         }
     }
+    if (!db->nblocks)
+        for (int k = 4; k < 8; ++k) HIPCHECK(hipEventRecord(h->ev[k], h->stream));
     HIPCHECK(hipEventRecord(h->ev[2], h->stream));
     // join
     if (db->nlong) HIPCHECK(hipStreamWaitEvent(h->stream, h->ev[1], 0));
@@ -808,6 +839,9 @@ int sw_db_get_stats(const sw_db* db, sw_db_stats* out) {
     out->device_bytes = static_cast<int64_t>(db->device_bytes);
     out->max_length = db->max_len;
     out->long_threshold = db->long_threshold;
+    out->coop_blocks = db->built ? db->last_ncoop : 0;
+    out->coop_residues = 0;
+    for (int32_t b = 0; b < out->coop_blocks; ++b) out->coop_residues += db->h_blk_res[b];
     return SW_OK;
 }
 
@@ -867,9 +901,14 @@ int read_events(const ScanEvents& se, sw_timing* t) {
     HIPCHECK(hipEventElapsedTime(&t01, se.ev[0], se.ev[1]));
     HIPCHECK(hipEventElapsedTime(&t02, se.ev[0], se.ev[2]));
     HIPCHECK(hipEventElapsedTime(&t03, se.ev[0], se.ev[3]));
+    float t45 = 0, t67 = 0;
+    HIPCHECK(hipEventElapsedTime(&t45, se.ev[4], se.ev[5]));
+    HIPCHECK(hipEventElapsedTime(&t67, se.ev[6], se.ev[7]));
     t->intra_ms += t01;
     t->inter_ms += t02;
     t->total_ms += t03;
+    t->coop_ms += t45;
+    t->wave_ms += t67;
     t->launches += se.launches;
     return SW_OK;
 }
@@ -881,6 +920,8 @@ int sw_get_timing(sw_handle* h, sw_timing* out) {
     if (!h->timed || h->nscans == 0) return SW_OK;
     return read_events(h->evpool[h->nscans - 1], out);
 }
+
+const char* sw_last_kernel(sw_handle* h) { return h ? h->last_kernel.c_str() : "none"; }
 
 int sw_timing_reset(sw_handle* h) {
     if (!h) return fail(SW_E_INVALID, "null argument");

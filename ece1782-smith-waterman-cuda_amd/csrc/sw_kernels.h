@@ -86,26 +86,36 @@ struct IntraArgs {
 
 // Strip heights (query rows held in registers per lane) the kernels are
 // instantiated for.
-int inter_rows(bool affine);
+// Shape of the inter kernel for this gap model.  x2_ok: the scan is provably
+// int16-safe, so the packed two-subjects-per-lane kernel may be chosen;
+// otherwise the int32 default is used.
+int inter_rows(bool affine, bool x2_ok);
 // true: the inter kernel takes an int32 profile [kProfileRows][prof_stride] int32
-bool inter_profile32(bool affine);
+bool inter_profile32(bool affine, bool x2_ok);
+// true if the packed two-subjects-per-lane kernel is used (int16 profile).
+bool inter_uses_x2(bool affine, bool x2_ok);
+// Name of the per-wave inter kernel launch_inter() runs, e.g. "sw_inter_x2<16,16,affine>".
+const char* inter_kernel_name(bool affine, bool x2_ok);
 // Query rows per lane the intra kernel uses for this query (2..16, even).
 int intra_rows_for(int qlen, int longest);
 // Bytes of one intra profile chunk (64*ri query rows, 32 codes).
 int intra_chunk_bytes(int ri);
 __host__ __device__ constexpr int intra_rip(int RI) { return (RI + 3) / 4 * 4; }
 
-hipError_t launch_inter(const InterArgs& a, bool affine, hipStream_t s);
+hipError_t launch_inter(const InterArgs& a, bool affine, bool x2_ok, hipStream_t s);
 // Wide blocks [0, ncoop): one 4-wave workgroup per block, the waves pipelined
 // over query strips (linear gap).  Returns the strip height it uses.
-hipError_t launch_inter_coop(const InterArgs& a, int ncoop, hipStream_t s);
+hipError_t launch_inter_coop(const InterArgs& a, int ncoop, bool affine, hipStream_t s);
 int inter_coop_rows();
 // Linear gap: true if the 16-bit inter kernel is used (profile int16 [32][stride]).
-bool inter_uses_16bit(bool affine);
+bool inter_uses_16bit(bool affine, bool x2_ok);
 // The 16-bit inter kernel (sw_inter16.hip, its own translation unit).
 hipError_t launch_inter16(const InterArgs& a, int R, int SG, hipStream_t s);
 // The packed two-subjects-per-lane kernel (sw_inter_pk.hip).
 hipError_t launch_inter_pk(const InterArgs& a, int R, int SG, hipStream_t s);
+// Two subjects per lane, packed int16, dual profile images (sw_inter_x2.hip);
+// blocks [blk_first, nblocks) in pairs.
+hipError_t launch_inter_x2(const InterArgs& a, int R, int SG, bool affine, hipStream_t s);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.
 constexpr int kSat16 = 32767 - 1152;
 // int32 re-scoring of the blocks the 16-bit kernel listed (device-side count).

@@ -31,7 +31,11 @@
 // saturating subtract supplies the 0 floor; H_left, H_up >= 0).  For affine
 // the profile holds S, and E/F are kept clamped at 0 (exact: a negative E or F
 // can never win the max against the 0 floor, and clamping commutes with the
-// "- ge" step because ge > 0).
+// "- ge" step because ge > 0).  The inter kernels carry E and F one cell
+// AHEAD (Farrar's form): after H(i,j),  n = usat(H(i,j) - go),
+// E(i,j+1) = max(usat(E(i,j) - ge), n),  F(i+1,j) = max(usat(F(i,j) - ge), n),
+// so a cell is  h = max3(H_diag + S, E, F)  and n is shared by E and F; a
+// strip's F boundary row therefore holds F of the next strip's first row.
 #include "sw_kernels.h"
 
 #include <cstdio>
@@ -123,10 +127,127 @@ __device__ __forceinline__ void read_prof(int4 (&pv)[R / 16], const uint8_t* lp,
     for (int q = 0; q < R / 16; ++q) pv[q] = pp[q];
 }
 
-template <int R, int SG, bool AFFINE>
+// One DP cell at row r of a lane's column (see the recurrences at the top).
+// up: H of the cell above (in: row r-1, out: row r); diag: H(r-1, j-1) in,
+// H(r, j-1) out; Hr/Er: this row's H and E (in: column j-1, out: column j,
+// E already one column ahead); f: F one row ahead (affine).
+template <bool AFFINE>
+__device__ __forceinline__ void dp_cell(int& Hr, int& Er, int& up, int& f, int& diag, int sc, int& best,
+                                        uint32_t go, uint32_t ge) {
+    if constexpr (!AFFINE) {
+        const int h = usub(max(max(Hr, up), diag + sc), go);
+        diag = Hr;
+        Hr = h;
+        up = h;
+        best = max(best, h);
+    } else {
+        const int h = max(max(Er, f), diag + sc);
+        const int n = usub(h, go);
+        Er = max(usub(Er, ge), n);
+        f = max(usub(f, ge), n);
+        diag = Hr;
+        Hr = h;
+        up = h;
+        best = max(best, h);
+    }
+}
+
+template <int R>
+__device__ __forceinline__ int prof_at(const int4 (&p)[R / 16], int r) {
+    return sx8(pword(p, r >> 2), r & 3);
+}
+
+// Walk the SG columns of one sub-group over the strip's R rows.
+//   bh/bf  : in: H/F of the row above the strip (F one row ahead), per column;
+//            out: the strip's bottom row H/F, per column.
+//   dtop   : H(s0-1, first column - 1); out: H(s0-1, last column).
+//   pa, pb : in: profile rows of columns 0 (and 1 with SKEW); out, if `more`:
+//            those of rs_next's first columns (software pipeline; `dep`-tied
+//            reads so the compiler cannot hoist them all and spill).
+// SKEW: columns are taken in pairs, cell (r, j) beside cell (r-1, j+1): two
+// independent dependency chains per step, so the 3-deep affine chain (max3,
+// sub, max through F) and the 2-deep linear one hide their latency at the 2-3
+// waves per SIMD the register budget allows (profiles/r01_chain_rate.txt).
+template <int R, int SG, bool AFFINE, bool SKEW>
+__device__ __forceinline__ void sweep_group(int (&H)[R], int (&E)[AFFINE ? R : 1], int (&bh)[SG],
+                                            int (&bf)[AFFINE ? SG : 1], int& dtop, int& best, const uint8_t* lp,
+                                            const Residues<SG>& rs, const Residues<SG>& rs_next, bool more,
+                                            int4 (&pa)[R / 16], int4 (&pb)[R / 16], uint32_t go, uint32_t ge) {
+    if constexpr (!SKEW) {
+#pragma unroll
+        for (int jj = 0; jj < SG; ++jj) {
+            int4 pn[R / 16];
+            if (jj + 1 < SG) {
+                read_prof<R>(pn, lp, rs.code(jj + 1), H[R - 1]);
+            } else if (more) {
+                read_prof<R>(pn, lp, rs_next.code(0), H[R - 1]);
+            }
+            int up = bh[jj];
+            int diag = dtop;
+            dtop = up;
+            int f = AFFINE ? bf[AFFINE ? jj : 0] : 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                dp_cell<AFFINE>(H[r], E[AFFINE ? r : 0], up, f, diag, prof_at<R>(pa, r), best, go, ge);
+            bh[jj] = up;
+            if constexpr (AFFINE) bf[jj] = f;
+            if (jj + 1 < SG || more) {
+#pragma unroll
+                for (int q = 0; q < R / 16; ++q) pa[q] = pn[q];
+            }
+            // Stop LLVM from reassociating the running max across the
+            // unrolled columns (it would keep every column's H alive).
+            asm volatile("" : "+v"(best));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else {
+        static_assert(SG % 2 == 0, "column pairs");
+#pragma unroll
+        for (int jj = 0; jj < SG; jj += 2) {
+            int4 na[R / 16], nb[R / 16];
+            if (jj + 2 < SG) {
+                read_prof<R>(na, lp, rs.code(jj + 2), H[R - 1]);
+                read_prof<R>(nb, lp, rs.code(jj + 3), H[R - 1]);
+            } else if (more) {
+                read_prof<R>(na, lp, rs_next.code(0), H[R - 1]);
+                read_prof<R>(nb, lp, rs_next.code(1), H[R - 1]);
+            }
+            int upA = bh[jj], upB = bh[jj + 1];
+            int diagA = dtop, diagB = upA;
+            dtop = upB;
+            int fA = AFFINE ? bf[AFFINE ? jj : 0] : 0;
+            int fB = AFFINE ? bf[AFFINE ? jj + 1 : 0] : 0;
+            dp_cell<AFFINE>(H[0], E[0], upA, fA, diagA, prof_at<R>(pa, 0), best, go, ge);
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                dp_cell<AFFINE>(H[r], E[AFFINE ? r : 0], upA, fA, diagA, prof_at<R>(pa, r), best, go, ge);
+                dp_cell<AFFINE>(H[r - 1], E[AFFINE ? r - 1 : 0], upB, fB, diagB, prof_at<R>(pb, r - 1), best, go,
+                                ge);
+            }
+            dp_cell<AFFINE>(H[R - 1], E[AFFINE ? R - 1 : 0], upB, fB, diagB, prof_at<R>(pb, R - 1), best, go, ge);
+            bh[jj] = upA;
+            bh[jj + 1] = upB;
+            if constexpr (AFFINE) {
+                bf[jj] = fA;
+                bf[jj + 1] = fB;
+            }
+            if (jj + 2 < SG || more) {
+#pragma unroll
+                for (int q = 0; q < R / 16; ++q) {
+                    pa[q] = na[q];
+                    pb[q] = nb[q];
+                }
+            }
+            asm volatile("" : "+v"(best));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
+template <int R, int SG, bool AFFINE, bool SKEW>
 __device__ __forceinline__ void inter_block(const InterArgs& a, int blk, uint8_t* lp, int lane);
 
-template <int R, int SG, bool AFFINE>
+template <int R, int SG, bool AFFINE, bool SKEW>
 __global__ __launch_bounds__(256) void sw_inter(InterArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerWG * kProfileRows * inter_stride(R)];
     // threadIdx.x >> 6 is wave-uniform, but the compiler cannot prove it:
@@ -137,17 +258,16 @@ __global__ __launch_bounds__(256) void sw_inter(InterArgs a) {
     if (a.blk_list) {  // rescue mode: the listed blocks only (count on the device)
         const int n = __builtin_amdgcn_readfirstlane(*a.blk_count);
         for (int i = blockIdx.x * kWavesPerWG + wave; i < n; i += gridDim.x * kWavesPerWG)
-            inter_block<R, SG, AFFINE>(a, __builtin_amdgcn_readfirstlane(a.blk_list[i]), lp, lane);
+            inter_block<R, SG, AFFINE, SKEW>(a, __builtin_amdgcn_readfirstlane(a.blk_list[i]), lp, lane);
         return;
     }
     const int blk = a.blk_first + blockIdx.x * kWavesPerWG + wave;
     if (blk >= a.nblocks) return;  // wave-uniform
-    inter_block<R, SG, AFFINE>(a, blk, lp, lane);
+    inter_block<R, SG, AFFINE, SKEW>(a, blk, lp, lane);
 }
 
-template <int R, int SG, bool AFFINE>
+template <int R, int SG, bool AFFINE, bool SKEW>
 __device__ __forceinline__ void inter_block(const InterArgs& a, int blk, uint8_t* lp, int lane) {
-
     const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
     const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
     const uint32_t go = static_cast<uint32_t>(a.gap_open);
@@ -184,8 +304,9 @@ __device__ __forceinline__ void inter_block(const InterArgs& a, int blk, uint8_t
 #pragma unroll
             for (int q = 0; q < (AFFINE ? SG : 1); ++q) bf[q] = 0;
         }
-        int4 pcur[R / 16], pnext[R / 16];
-        read_prof<R>(pcur, lp, rs.code(0), 0);
+        int4 pa[R / 16], pb[R / 16];
+        read_prof<R>(pa, lp, rs.code(0), 0);
+        if constexpr (SKEW) read_prof<R>(pb, lp, rs.code(1), 0);
 
         for (uint32_t col0 = 0; col0 < ncols; col0 += SG) {
             const uint64_t idx = base + (col0 >> 4) * kGroupBytes + (col0 & 15);
@@ -198,51 +319,7 @@ __device__ __forceinline__ void inter_block(const InterArgs& a, int blk, uint8_t
                     if constexpr (AFFINE) load_row<SG>(bf_next, a.bnd_f + nidx);
                 }
             }
-#pragma unroll
-            for (int jj = 0; jj < SG; ++jj) {
-                // prefetch the next column's profile rows
-                if (jj + 1 < SG) {
-                    read_prof<R>(pnext, lp, rs.code(jj + 1), H[R - 1]);
-                } else if (more) {
-                    read_prof<R>(pnext, lp, rs_next.code(0), H[R - 1]);
-                }
-                int up = bh[jj];
-                int diag = dtop;
-                dtop = up;
-                if constexpr (!AFFINE) {
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        const int sc = sx8(pword(pcur, r >> 2), r & 3);
-                        const int h = usub(max(max(H[r], up), diag + sc), go);
-                        diag = H[r];
-                        H[r] = h;
-                        up = h;
-                        best = max(best, h);
-                    }
-                } else {
-                    int f = bf[jj];
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        const int sc = sx8(pword(pcur, r >> 2), r & 3);
-                        const int e = max(usub(E[r], ge), usub(H[r], go));
-                        f = max(usub(f, ge), usub(up, go));
-                        const int h = max(max(e, f), diag + sc);
-                        diag = H[r];
-                        H[r] = h;
-                        E[r] = e;
-                        up = h;
-                        best = max(best, h);
-                    }
-                    bf[jj] = f;
-                }
-                bh[jj] = up;
-#pragma unroll
-                for (int q = 0; q < R / 16; ++q) pcur[q] = pnext[q];
-                // Stop LLVM from reassociating the running max across the
-                // unrolled columns (it would keep every column's H alive).
-                asm volatile("" : "+v"(best));
-                __builtin_amdgcn_sched_barrier(0);
-            }
+            sweep_group<R, SG, AFFINE, SKEW>(H, E, bh, bf, dtop, best, lp, rs, rs_next, more, pa, pb, go, ge);
             if (!last) {
                 store_row<SG>(a.bnd_h + idx, bh);
                 if constexpr (AFFINE) store_row<SG>(a.bnd_f + idx, bf);
@@ -273,22 +350,23 @@ done:
 }
 
 // ---------------------------------------------------------------------------
-// inter-sequence, linear gap, cooperative: one workgroup per WIDE block
+// inter-sequence, cooperative: one workgroup per WIDE block
 // ---------------------------------------------------------------------------
 // With one block per wave, the widest blocks (subjects near the long
 // threshold) are the kernel's critical path: a 1536-column block is ~7 ms of
 // one wave's work at 2 waves/SIMD.  Here the 4 waves of a workgroup share one
 // block: in pass p wave w computes query strip 4p+w, one 8-column chunk behind
-// wave w-1, and receives that wave's strip-bottom row for the chunk through an
-// LDS double buffer (one workgroup barrier per chunk step).  Only the last
-// strip of a pass hands its bottom row to the next pass through HBM.  The
-// block's latency drops ~4x.
-template <int R>
+// wave w-1, and receives that wave's strip-bottom row (H, and F for affine)
+// for the chunk through an LDS double buffer (one workgroup barrier per chunk
+// step).  Only the last strip of a pass hands its bottom row to the next pass
+// through HBM.  The block's latency drops ~4x.
+template <int R, bool AFFINE, bool SKEW>
 __global__ __launch_bounds__(256) void sw_inter_coop(InterArgs a) {
     constexpr int SG = 8;
     constexpr int S = inter_stride(R);
+    constexpr int NF = AFFINE ? 2 : 1;  // rows handed down: H (+ F)
     __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerWG * kProfileRows * S];
-    __shared__ __attribute__((aligned(16))) int4 ring[kWavesPerWG - 1][2][kLanes][SG / 4];
+    __shared__ __attribute__((aligned(16))) int4 ring[NF][kWavesPerWG - 1][2][kLanes][SG / 4];
     __shared__ int red[kWavesPerWG][kLanes];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -297,6 +375,7 @@ __global__ __launch_bounds__(256) void sw_inter_coop(InterArgs a) {
     const int nchunks = static_cast<int>(a.blk_groups[blk] * (kGroupCols / SG));
     const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
     const uint32_t go = static_cast<uint32_t>(a.gap_open);
+    const uint32_t ge = static_cast<uint32_t>(a.gap_extend);
     const int nstrips = a.qpad / R;
     const int passes = (nstrips + kWavesPerWG - 1) / kWavesPerWG;
     int best = 0;
@@ -309,8 +388,11 @@ __global__ __launch_bounds__(256) void sw_inter_coop(InterArgs a) {
         const int s0 = strip * R;
         if (valid) stage_profile<R>(lp, a.prof, a.prof_stride, s0, lane);
         int H[R];
+        int E[AFFINE ? R : 1];
 #pragma unroll
         for (int r = 0; r < R; ++r) H[r] = 0;
+#pragma unroll
+        for (int r = 0; r < (AFFINE ? R : 1); ++r) E[r] = 0;
         int dtop = 0;
         __syncthreads();  // profile staged; the previous pass's HBM boundary rows are visible
 
@@ -322,50 +404,44 @@ __global__ __launch_bounds__(256) void sw_inter_coop(InterArgs a) {
                 Residues<SG> rs;
                 rs.load(a.residues + idx);
                 int bv[SG];
+                int bf[AFFINE ? SG : 1];
                 if (first) {
 #pragma unroll
                     for (int q = 0; q < SG; ++q) bv[q] = 0;
+#pragma unroll
+                    for (int q = 0; q < (AFFINE ? SG : 1); ++q) bf[q] = 0;
                 } else if (wave == 0) {
                     load_row<SG>(bv, a.bnd_h + idx);
+                    if constexpr (AFFINE) load_row<SG>(bf, a.bnd_f + idx);
                 } else {
-                    const int4* rp = ring[wave - 1][(t - 1) & 1][lane];
 #pragma unroll
-                    for (int q = 0; q < SG / 4; ++q) {
-                        const int4 v = rp[q];
-                        bv[4 * q] = v.x; bv[4 * q + 1] = v.y; bv[4 * q + 2] = v.z; bv[4 * q + 3] = v.w;
+                    for (int k = 0; k < NF; ++k) {
+                        const int4* rp = ring[k][wave - 1][(t - 1) & 1][lane];
+                        int* d = k == 0 ? bv : bf;
+#pragma unroll
+                        for (int q = 0; q < SG / 4; ++q) {
+                            const int4 v = rp[q];
+                            d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+                        }
                     }
                 }
-                int4 pcur[R / 16], pnext[R / 16];
-                read_prof<R>(pcur, lp, rs.code(0), 0);
-#pragma unroll
-                for (int jj = 0; jj < SG; ++jj) {
-                    if (jj + 1 < SG) read_prof<R>(pnext, lp, rs.code(jj + 1), H[R - 1]);
-                    int up = bv[jj];
-                    int diag = dtop;
-                    dtop = up;
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        const int sc = sx8(pword(pcur, r >> 2), r & 3);
-                        const int h = usub(max(max(H[r], up), diag + sc), go);
-                        diag = H[r];
-                        H[r] = h;
-                        up = h;
-                        best = max(best, h);
-                    }
-                    bv[jj] = up;
-#pragma unroll
-                    for (int q = 0; q < R / 16; ++q) pcur[q] = pnext[q];
-                    asm volatile("" : "+v"(best));
-                    __builtin_amdgcn_sched_barrier(0);
-                }
+                int4 pa[R / 16], pb[R / 16];
+                read_prof<R>(pa, lp, rs.code(0), 0);
+                if constexpr (SKEW) read_prof<R>(pb, lp, rs.code(1), 0);
+                sweep_group<R, SG, AFFINE, SKEW>(H, E, bv, bf, dtop, best, lp, rs, rs, false, pa, pb, go, ge);
                 if (!last) {
                     if (wave == kWavesPerWG - 1) {
                         store_row<SG>(a.bnd_h + idx, bv);
+                        if constexpr (AFFINE) store_row<SG>(a.bnd_f + idx, bf);
                     } else {
-                        int4* wp = ring[wave][t & 1][lane];
 #pragma unroll
-                        for (int q = 0; q < SG / 4; ++q)
-                            wp[q] = make_int4(bv[4 * q], bv[4 * q + 1], bv[4 * q + 2], bv[4 * q + 3]);
+                        for (int k = 0; k < NF; ++k) {
+                            int4* wp = ring[k][wave][t & 1][lane];
+                            const int* d = k == 0 ? bv : bf;
+#pragma unroll
+                            for (int q = 0; q < SG / 4; ++q)
+                                wp[q] = make_int4(d[4 * q], d[4 * q + 1], d[4 * q + 2], d[4 * q + 3]);
+                        }
                     }
                 }
             }
@@ -384,9 +460,19 @@ __global__ __launch_bounds__(256) void sw_inter_coop(InterArgs a) {
 constexpr int kCoopRows = 32;
 int inter_coop_rows() { return kCoopRows; }
 
-hipError_t launch_inter_coop(const InterArgs& a, int ncoop, hipStream_t s) {
+static bool coop_skew() {
+    const char* e = std::getenv("SW_COOP_SKEW");
+    return !(e && e[0] == '0');
+}
+
+hipError_t launch_inter_coop(const InterArgs& a, int ncoop, bool affine, hipStream_t s) {
     if (ncoop <= 0 || a.qpad <= 0) return hipSuccess;
-    hipLaunchKernelGGL((sw_inter_coop<kCoopRows>), dim3(ncoop), dim3(kWavesPerWG * kLanes), 0, s, a);
+    const dim3 grid(ncoop), block(kWavesPerWG * kLanes);
+    const bool sk = coop_skew();
+    if (affine && sk) hipLaunchKernelGGL((sw_inter_coop<kCoopRows, true, true>), grid, block, 0, s, a);
+    else if (affine) hipLaunchKernelGGL((sw_inter_coop<kCoopRows, true, false>), grid, block, 0, s, a);
+    else if (sk) hipLaunchKernelGGL((sw_inter_coop<kCoopRows, false, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((sw_inter_coop<kCoopRows, false, false>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 
@@ -676,14 +762,21 @@ __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
 // ---------------------------------------------------------------------------
 // Inter-kernel shape: R query rows per strip x SG columns per software-
 // pipelined sub-group.  SW_INTER_VARIANT="RxSG" overrides (tuning only).
-struct InterShape { int R, SG; bool p32; bool i16; bool pk; };
-static InterShape inter_shape(bool affine) {
+struct InterShape { int R, SG; bool p32; bool i16; bool pk; bool skew = false; bool x2 = false; };
+static InterShape inter_shape(bool affine, bool x2_ok) {
     // measured on MI355X (scripts/tune_inter.py, profiles/r01_tune_inter.jsonl):
     // 64x8 is fastest for the linear kernel (170 VGPRs, 2 waves/SIMD, half
     // the boundary traffic of 32-row strips); affine keeps 32x8.
     // measured on MI355X: 64x8 int32 beats the 16-bit-value (h*) and int32-
     // profile (p*) variants on C2 (profiles/r01_tune_inter*.jsonl)
-    InterShape v = affine ? InterShape{32, 8, false, false, false} : InterShape{64, 8, false, false, false};
+    // Affine, int16-safe scans: the packed two-subjects-per-lane kernel x32x8
+    // (profiles/r01_tune_x2*.jsonl: +28% over int32 32x8 on C2 BLOSUM62 12/1;
+    // 32-row strips halve the boundary-row traffic of x16x16).
+    // Linear: int32 64x8 (packed gains nothing there: 5 packed ops per cell
+    // pair vs 3.5 int32 ops per cell).
+    InterShape v = affine ? (x2_ok ? InterShape{32, 8, false, false, false, false, true}
+                                   : InterShape{32, 8, false, false, false})
+                          : InterShape{64, 8, false, false, false};
     if (const char* e = std::getenv("SW_INTER_VARIANT")) {
         int r = 0, g = 0;
         if (std::sscanf(e, "k%dx%d", &r, &g) == 2 && !affine &&
@@ -695,6 +788,12 @@ static InterShape inter_shape(bool affine) {
         else if (std::sscanf(e, "p%dx%d", &r, &g) == 2 && !affine &&
             ((r == 64 && (g == 8 || g == 4)) || (r == 32 && g == 8) || (r == 48 && g == 8)))
             v = InterShape{r, g, true, false, false};
+        else if (std::sscanf(e, "x%dx%d", &r, &g) == 2 && x2_ok &&
+            ((r == 16 && (g == 8 || g == 16)) || (r == 32 && g == 8) || (r == 48 && g == 8)))
+            v = InterShape{r, g, false, false, false, false, true};
+        else if (std::sscanf(e, "s%dx%d", &r, &g) == 2 &&
+            ((r == 32 && (g == 8 || g == 16)) || (r == 48 && g == 8) || (r == 64 && g == 8) || (r == 16 && g == 16)))
+            v = InterShape{r, g, false, false, false, true};
         else if (std::sscanf(e, "%dx%d", &r, &g) == 2 &&
             ((r == 32 && (g == 8 || g == 16)) || (r == 48 && g == 8) || (r == 64 && g == 8) || (r == 16 && g == 16)))
             v = InterShape{r, g, false, false, false};
@@ -702,15 +801,26 @@ static InterShape inter_shape(bool affine) {
     return v;
 }
 
-int inter_rows(bool affine) { return inter_shape(affine).R; }
-bool inter_profile32(bool affine) { return inter_shape(affine).p32; }
-bool inter_uses_16bit(bool affine) { return inter_shape(affine).i16; }
+int inter_rows(bool affine, bool x2_ok) { return inter_shape(affine, x2_ok).R; }
+bool inter_profile32(bool affine, bool x2_ok) { return inter_shape(affine, x2_ok).p32; }
+bool inter_uses_16bit(bool affine, bool x2_ok) { return inter_shape(affine, x2_ok).i16; }
+bool inter_uses_x2(bool affine, bool x2_ok) { return inter_shape(affine, x2_ok).x2; }
+
+const char* inter_kernel_name(bool affine, bool x2_ok) {
+    const InterShape v = inter_shape(affine, x2_ok);
+    const char* kind = v.x2 ? "sw_inter_x2" : v.pk ? "sw_inter_pk" : v.i16 ? "sw_inter16" : v.p32 ? "sw_inter_p32"
+                                                                                               : "sw_inter";
+    static thread_local char buf[96];
+    std::snprintf(buf, sizeof buf, "%s<%d,%d,%s%s>", kind, v.R, v.SG, affine ? "affine" : "linear",
+                  v.skew ? ",skew" : "");
+    return buf;
+}
 
 // int32 re-scoring of the blocks the 16-bit kernel put on the rescue list.
 hipError_t launch_inter_rescue(const InterArgs& a, hipStream_t s) {
     // A few hundred waves walk the device-side list; an empty list costs one
     // tiny launch and no host synchronisation.
-    hipLaunchKernelGGL((sw_inter<64, 8, false>), dim3(64), dim3(kWavesPerWG * kLanes), 0, s, a);
+    hipLaunchKernelGGL((sw_inter<64, 8, false, false>), dim3(64), dim3(kWavesPerWG * kLanes), 0, s, a);
     return hipGetLastError();
 }
 
@@ -732,11 +842,12 @@ int intra_rows_for(int qlen, int longest) {
 
 int intra_chunk_bytes(int ri) { return kProfileRows * kLanes * intra_rip(ri); }
 
-hipError_t launch_inter(const InterArgs& a, bool affine, hipStream_t s) {
+hipError_t launch_inter(const InterArgs& a, bool affine, bool x2_ok, hipStream_t s) {
     if (a.nblocks - a.blk_first <= 0 || a.qpad <= 0) return hipSuccess;
     const dim3 grid((a.nblocks - a.blk_first + kWavesPerWG - 1) / kWavesPerWG);
     const dim3 block(kWavesPerWG * kLanes);
-    const InterShape v = inter_shape(affine);
+    const InterShape v = inter_shape(affine, x2_ok);
+    if (v.x2) return launch_inter_x2(a, v.R, v.SG, affine, s);
     if (v.pk) return launch_inter_pk(a, v.R, v.SG, s);
     if (v.i16) return launch_inter16(a, v.R, v.SG, s);
     if (v.p32) {
@@ -752,11 +863,13 @@ hipError_t launch_inter(const InterArgs& a, bool affine, hipStream_t s) {
 #undef SW_LAUNCH_P32
         return hipErrorInvalidValue;
     }
-#define SW_LAUNCH_INTER(R_, SG_)                                                             \
-    if (v.R == R_ && v.SG == SG_) {                                                          \
-        if (affine) hipLaunchKernelGGL((sw_inter<R_, SG_, true>), grid, block, 0, s, a);     \
-        else hipLaunchKernelGGL((sw_inter<R_, SG_, false>), grid, block, 0, s, a);           \
-        return hipGetLastError();                                                            \
+#define SW_LAUNCH_INTER(R_, SG_)                                                                         \
+    if (v.R == R_ && v.SG == SG_) {                                                                      \
+        if (affine && v.skew) hipLaunchKernelGGL((sw_inter<R_, SG_, true, true>), grid, block, 0, s, a); \
+        else if (affine) hipLaunchKernelGGL((sw_inter<R_, SG_, true, false>), grid, block, 0, s, a);     \
+        else if (v.skew) hipLaunchKernelGGL((sw_inter<R_, SG_, false, true>), grid, block, 0, s, a);     \
+        else hipLaunchKernelGGL((sw_inter<R_, SG_, false, false>), grid, block, 0, s, a);                \
+        return hipGetLastError();                                                                        \
     }
     SW_LAUNCH_INTER(32, 8)
     SW_LAUNCH_INTER(32, 16)

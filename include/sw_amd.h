@@ -78,6 +78,10 @@ typedef struct sw_db_stats {
     int64_t device_bytes;    /* HBM held by the packed database */
     int32_t max_length;      /* longest subject */
     int32_t long_threshold;  /* subjects longer than this use the intra kernel */
+    int32_t coop_blocks;     /* widest blocks the cooperative kernel took in the
+                                most recent scan of this database (the split
+                                depends on the scoring) */
+    int64_t coop_residues;   /* unpadded residues in those blocks */
 } sw_db_stats;
 
 typedef struct sw_timing {
@@ -86,6 +90,8 @@ typedef struct sw_timing {
     float total_ms;     /* first launch to last completion of the last scan */
     int32_t rescued;    /* subjects re-scored at int32 after an int16 saturation */
     int32_t launches;   /* kernel launches in the last scan */
+    float coop_ms;      /* cooperative wide-block kernel alone (events on its stream) */
+    float wave_ms;      /* per-wave inter kernel alone (events on the handle's stream) */
 } sw_timing;
 
 typedef struct sw_handle sw_handle;
@@ -153,6 +159,11 @@ SW_API int sw_get_timing(sw_handle* h, sw_timing* out);
  * between them (bench.py).                                               */
 SW_API int sw_timing_reset(sw_handle* h);
 SW_API int sw_timing_total(sw_handle* h, sw_timing* out, int32_t* nscans);
+/* Name of the per-wave inter-sequence kernel the handle's last scan ran,
+ * e.g. "sw_inter_x2<16,16,affine>" (packed int16, two subjects per lane) or
+ * "sw_inter<32,8,affine>" (int32); "none" before any scan.  Valid until the
+ * next scan on the handle.                                                  */
+SW_API const char* sw_last_kernel(sw_handle* h);
 
 /* ---- ranking ---------------------------------------------------------------
  * Top-k of a score vector (score descending, id ascending on ties).

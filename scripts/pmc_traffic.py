@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Per-launch HBM bytes of the bench's dominant kernel from two rocprofv3
+--pmc passes (FETCH_SIZE and WRITE_SIZE cannot share one pass on gfx950).
+
+FETCH_SIZE / WRITE_SIZE are reported in KiB.  Per MI355X_MICROARCH.md (HBM
+section), on gfx950 FETCH_SIZE counts half the bytes of a wide (16 B/lane)
+streaming read, which is how sw_inter loads its packed residue groups, so it
+is doubled; WRITE_SIZE is taken as reported.
+
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR WORKLOAD_KEY OUT_JSON ROCPROF_NAME_SUBSTR LABEL
+(LABEL = the library's kernel name, sw_last_kernel(), which bench.py matches)
+"""
+import csv
+import json
+import sys
+
+
+def per_dispatch(d, counter, kernel):
+    vals = []
+    with open(d + "/run_counter_collection.csv") as f:
+        for row in csv.DictReader(f):
+            if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                vals.append(float(row["Counter_Value"]))
+    if not vals:
+        raise SystemExit("no %s rows for %s in %s" % (counter, kernel, d))
+    return vals
+
+
+def main():
+    fdir, wdir, key, out, kernel, label = sys.argv[1:7]
+    f = per_dispatch(fdir, "FETCH_SIZE", kernel)
+    w = per_dispatch(wdir, "WRITE_SIZE", kernel)
+    fetch = sum(f) / len(f) * 1024 * 2
+    write = sum(w) / len(w) * 1024
+    res = {"workload_key": key, "kernel": label, "rocprof_kernel": kernel,
+           "fetch_bytes_per_launch": round(fetch), "write_bytes_per_launch": round(write),
+           "hbm_bytes_per_launch": round(fetch + write),
+           "dispatches": {"fetch_pass": len(f), "write_pass": len(w)},
+           "raw_kib_mean": {"FETCH_SIZE": sum(f) / len(f), "WRITE_SIZE": sum(w) / len(w)},
+           "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane streaming reads); WRITE_SIZE as reported"}
+    with open(out, "w") as fo:
+        json.dump(res, fo, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -18,6 +18,10 @@ thresholds = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "3072,2048,
 qname = sys.argv[3] if len(sys.argv) > 3 else "P07327"
 nseq = int(sys.argv[4]) if len(sys.argv) > 4 else 570000
 reps = 5
+# scoring: SW_TUNE_SCORING="<matrix id>:<gap open>:<gap extend>" (default the
+# reference's BLOSUM50, linear gap 2)
+mid, go, ge = (int(x) for x in os.environ.get("SW_TUNE_SCORING", "0:2:2").split(":"))
+mat = sw.capi.builtin_matrix(mid)
 res, offs = sw.synth.database(nseq, shard=0)
 with open(os.path.join(REPO, "tests/golden/queries/%s.fasta" % qname)) as f:
     q = sw.encode("".join(f.read().split("\n")[1:]))
@@ -30,18 +34,18 @@ for thr in thresholds:
     st = db.stats()
     for v in variants:
         os.environ["SW_INTER_VARIANT"] = v
-        out = db.scan(q)  # warm
+        out = db.scan(q, mat, go, ge)  # warm
         if ref is None:
             ref = out
         ok = bool(np.array_equal(out, ref))
         h.timing_reset()
         t = time.perf_counter()
         for _ in range(reps):
-            db.scan(q)
+            db.scan(q, mat, go, ge)
         wall = (time.perf_counter() - t) / reps
         kt = h.timing_total()
         n = kt["scans"]
-        rec = {"variant": v, "long_threshold": thr, "n_long": st["n_long"], "ok": ok,
+        rec = {"scoring": [mid, go, ge], "variant": v, "long_threshold": thr, "n_long": st["n_long"], "ok": ok,
                "inter_ms": round(kt["inter_ms"] / n, 3), "intra_ms": round(kt["intra_ms"] / n, 3),
                "scan_ms": round(kt["total_ms"] / n, 3), "wall_ms": round(wall * 1e3, 3),
                "gcups_scan": round(cells / (kt["total_ms"] / n * 1e-3) / 1e9, 1)}

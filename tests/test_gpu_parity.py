@@ -178,3 +178,58 @@ def test_device_topk(sw, handle, n, k):
     ids2, sc2 = sw.capi.decode_keys(merged.cpu().numpy())
     assert ids2[:m].tolist() == order[:m].tolist()
     assert sc2[:m].tolist() == s[order[:m]].tolist()
+
+
+INTER_VARIANTS = ["32x8", "s32x8", "32x16", "s32x16", "48x8", "s48x8", "64x8", "s64x8", "16x16", "s16x16",
+                  "x16x8", "x16x16", "x32x8", "x48x8"]
+
+
+@pytest.mark.parametrize("variant", INTER_VARIANTS)
+@pytest.mark.parametrize("coop", ["0", "128:0", "128:1"])
+def test_inter_variants_vs_oracle(sw, oracle, handle, monkeypatch, variant, coop):
+    """Every inter-kernel shape, plain and column-skewed, with the cooperative
+    wide-block kernel off / on (plain) / on (skewed), linear and affine."""
+    width, _, skew = coop.partition(":")
+    monkeypatch.setenv("SW_INTER_VARIANT", variant)
+    monkeypatch.setenv("SW_COOP_WIDTH", width)
+    monkeypatch.setenv("SW_COOP_SKEW", skew or "1")
+    r, o = sw.synth.database(900, shard=11)
+    db = sw.Database(handle, r, o, long_threshold=1500)
+    for qlen, mid, go, ge in [(375, 0, 2, 2), (150, 1, 12, 1), (97, 1, 11, 2)]:
+        q = sw.synth.query(qlen, shard=qlen + 1)
+        m = sw.capi.builtin_matrix(mid)
+        got = db.scan(q, m, go, ge)
+        want = oracle.scan(q, r, o, mat=m, gap_open=go, gap_extend=ge)
+        assert np.array_equal(got, want), (qlen, mid, go, ge, np.nonzero(got != want)[0][:10])
+
+
+@pytest.mark.parametrize("variant", ["x16x8", "x32x8"])
+def test_x2_falls_back_to_int32_when_int16_unsafe(sw, oracle, handle, monkeypatch, variant):
+    """A query long enough that (qlen + 2) * (max S + gap open) >= 32767 must
+    not run the packed int16 kernel: scores stay exact (int32 path)."""
+    monkeypatch.setenv("SW_INTER_VARIANT", variant)
+    r, o = sw.synth.database(300, shard=5)
+    q = sw.synth.query(2400, shard=9)
+    # plant a near-copy of the query so one score is large (> 32767 would
+    # wrap in int16): the subject is the query itself
+    r2 = np.concatenate([r, q])
+    o2 = np.concatenate([o, [o[-1] + len(q)]])
+    db = sw.Database(handle, r2, o2, long_threshold=3000)
+    for mid, go, ge in [(1, 12, 1), (0, 2, 2)]:
+        m = sw.capi.builtin_matrix(mid)
+        got = db.scan(q, m, go, ge)
+        want = oracle.scan(q, r2, o2, mat=m, gap_open=go, gap_extend=ge)
+        assert np.array_equal(got, want), (mid, np.nonzero(got != want)[0][:10])
+        assert got[-1] > 9000
+        assert not handle.last_kernel().startswith("sw_inter_x2"), handle.last_kernel()
+
+
+def test_default_kernel_selection(sw, handle):
+    """Affine int16-safe scans run the packed kernel; linear runs int32 64x8."""
+    r, o = sw.synth.database(200, shard=3)
+    db = sw.Database(handle, r, o)
+    q = sw.synth.query(375, shard=4)
+    db.scan(q, sw.capi.builtin_matrix(1), 12, 1)
+    assert handle.last_kernel() == "sw_inter_x2<32,8,affine>"
+    db.scan(q)
+    assert handle.last_kernel() == "sw_inter<64,8,linear>"
