@@ -44,6 +44,9 @@ SIMDS, CLOCK_HZ = 1024, 2.4e9   # 256 CUs x 4 SIMDs
 # v_or_b32 2.7 cycles per wave64 instruction).
 VALU_MODEL = {
     # per 2 x 64 cells: 4.83 v_pk_max_i16, 2.83 v_pk_sub_u16, 1 v_pk_add_u16, 1 v_or_b32
+    "sw_inter_x2s<32,8,affine>": ((4.83 + 2.83 + 1) * 4.25 + 2.7) / 128,
+    # per 2 x 64 cells: 3 v_pk_max_i16, 1 v_pk_sub_u16, 1 v_pk_add_u16, 1 v_or_b32
+    "sw_inter_x2s<48,4,linear>": ((3 + 1 + 1) * 4.25 + 2.7) / 128,
     "sw_inter_x2<32,8,affine>": ((4.83 + 2.83 + 1) * 4.25 + 2.7) / 128,
     "sw_inter_x2<16,16,affine>": ((4.87 + 2.87 + 1) * 4.25 + 2.7) / 128,
     # per 64 cells: 1.5 v_max3, 1 v_add_sdwa, 1 v_sub clamp

@@ -478,11 +478,12 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
 // C2 (2.05e8 residues, profiles/r01_tune_coop.jsonl): width 384 with long
 // threshold 2048 is best, i.e. W ~ sum(residues) / 530000.  SW_COOP_WIDTH
 // overrides (tuning); 0 disables.
-int32_t coop_blocks(const sw_db* db, bool x2) {
-    // the packed kernel covers two blocks per wave, so its per-wave tail is
-    // shorter relative to the coop kernel's int32 cells: a wider cut-off
-    // (measured on C2: 1024 beats 386 and 640, profiles/r01_tune_x2.jsonl)
-    int64_t wmin = std::max<int64_t>(128, db->residues / (x2 ? 200000 : 530000));
+int32_t coop_blocks(const sw_db* db, int divisor) {
+    // divisor from the inter kernel's shape (swk::inter_coop_divisor): the
+    // two-subjects-per-lane kernel wants a wider cut-off than int32 (measured
+    // on C2: 1024 beats 386 and 640, profiles/r01_x2/); 0 = no coop kernel
+    if (divisor <= 0 && !std::getenv("SW_COOP_WIDTH")) return 0;
+    int64_t wmin = divisor > 0 ? std::max<int64_t>(128, db->residues / divisor) : 0;
     if (const char* e = std::getenv("SW_COOP_WIDTH")) wmin = std::atoll(e);
     if (wmin <= 0) return 0;
     int32_t n = 0;
@@ -551,7 +552,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // the int32 rescue pass after a 16-bit kernel walks 64-row strips
     const int32_t qpad_rescue = i16 ? static_cast<int32_t>(round_up(qlen, 64)) : 0;
     // widest blocks first, one cooperative workgroup each (int32, int8-profile paths)
-    const int32_t ncoop = (!i16 && !p32 && db->nblocks) ? coop_blocks(db, x2) : 0;
+    const int32_t ncoop = (!i16 && !p32 && db->nblocks) ? coop_blocks(db, swk::inter_coop_divisor(affine, x2_ok)) : 0;
     db->last_ncoop = ncoop;
     const int32_t qpad_coop = ncoop ? static_cast<int32_t>(round_up(qlen, swk::inter_coop_rows())) : 0;
     if ((rc = build_profiles(h, query, qlen, mat, go, affine, std::max({qpad_inter, qpad_rescue, qpad_coop}), i16 || x2,

@@ -291,6 +291,206 @@ __global__ __launch_bounds__(256) void sw_inter_x2(InterArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// sw_inter_x2s: ONE subject per lane, TWO query strips per pass
+// ---------------------------------------------------------------------------
+// The low 16 bits of a lane's registers run rows [s0, s0+R) of its subject at
+// column t while the high 16 bits run rows [s0+R, s0+2R) of the same subject
+// at column t-SG.  The low strip's bottom row (H, F) reaches the high strip
+// SG steps later through an SG-entry register delay line (the values a
+// sub-group of SG columns produces are consumed by the next sub-group at the
+// same position), so only every second strip boundary goes through HBM, as
+// one dword (H | F << 16) per packed column per lane: 4x less boundary
+// traffic than sw_inter_x2 (2 dwords per 2 subjects per R rows), and 64
+// subjects per wave (finer work units, shorter tail).  Cost: the first
+// sub-group of a pass computes the high strip on SG virtual columns before
+// the subject (all-zero inputs, pad scores: they stay 0) and the last one the
+// low strip on SG pad columns after it.  Same packed cell as sw_inter_x2; the
+// score pair is lo[code(t)][i] | hi[code(t-SG)][i] with the two images holding
+// the two strips' rows.
+template <int R>
+__device__ __forceinline__ void stage_x2s(X2Lds<R>& L, const int16_t* __restrict__ prof, int stride, int s0,
+                                          int lane) {
+    constexpr int RD = x2_row_dwords(R);
+    // lo image <- rows [s0, s0+R), hi image <- rows [s0+R, s0+2R)
+#pragma unroll
+    for (int t = lane; t < 2 * kProfileRows * (R / 8); t += kLanes) {
+        const int img = t / (kProfileRows * (R / 8));
+        const int u = t % (kProfileRows * (R / 8));
+        const int c = u / (R / 8);
+        const int k = u % (R / 8);
+        const int4 v = *reinterpret_cast<const int4*>(prof + static_cast<size_t>(c) * stride + s0 + img * R + 8 * k);
+        const uint32_t w[4] = {static_cast<uint32_t>(v.x), static_cast<uint32_t>(v.y), static_cast<uint32_t>(v.z),
+                               static_cast<uint32_t>(v.w)};
+        uint32_t o[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            o[2 * e] = img ? w[e] << 16 : w[e] & 0xffffu;
+            o[2 * e + 1] = img ? w[e] & 0xffff0000u : w[e] >> 16;
+        }
+        int4* d = reinterpret_cast<int4*>((img ? L.hi : L.lo) + c * RD + 8 * k);
+        d[0] = make_int4(o[0], o[1], o[2], o[3]);
+        d[1] = make_int4(o[4], o[5], o[6], o[7]);
+    }
+}
+
+__device__ __forceinline__ uint32_t lo_lo(uint32_t a, uint32_t b) { return (a & 0xffffu) | (b << 16); }
+__device__ __forceinline__ uint32_t hi_hi(uint32_t a, uint32_t b) { return (a >> 16) | (b & 0xffff0000u); }
+
+template <int R, int SG, bool AFFINE>
+__global__ __launch_bounds__(256) void sw_inter_x2s(InterArgs a) {
+    static_assert(R % 16 == 0 && SG % 4 == 0, "shape");
+    // SG: sub-group width = the lag (columns) between the two strips
+    constexpr int NCH = R / 16;
+    constexpr int STEPS = SG * NCH;
+    __shared__ __attribute__((aligned(16))) X2Lds<R> lds[kWavesPerWG];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    X2Lds<R>& L = lds[wave];
+    const int blk = a.blk_first + blockIdx.x * kWavesPerWG + wave;
+    if (blk >= a.nblocks) return;  // wave-uniform; waves never synchronise
+    const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
+    const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
+    const int16_t* prof16 = reinterpret_cast<const int16_t*>(a.prof);
+    const u2 go2 = {static_cast<unsigned short>(a.gap_open), static_cast<unsigned short>(a.gap_open)};
+    const u2 ge2 = {static_cast<unsigned short>(a.gap_extend), static_cast<unsigned short>(a.gap_extend)};
+    uint32_t* bnd = reinterpret_cast<uint32_t*>(a.bnd_h);
+    s2 best = {0, 0};
+
+    for (int s0 = 0; s0 < a.qpad && ncols > 0; s0 += 2 * R) {
+        const bool first = (s0 == 0);
+        const bool last = (s0 + 2 * R >= a.qpad);
+        stage_x2s<R>(L, prof16, a.prof_stride, s0, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+
+        s2 H[R];
+        s2 E[AFFINE ? R : 1];
+#pragma unroll
+        for (int r = 0; r < R; ++r) H[r] = s2{0, 0};
+#pragma unroll
+        for (int r = 0; r < (AFFINE ? R : 1); ++r) E[r] = s2{0, 0};
+        uint32_t dtop = 0;                 // packed H of row -1 at the previous step
+        uint32_t dl_h[SG], dl_f[SG];       // low strip's bottom row, SG steps back
+        uint32_t bin[SG], bin_n[SG];       // HBM boundary in (H | F << 16), this / next sub-group
+        uint32_t hb[SG];                   // HBM boundary out (high strip's bottom row)
+        uint32_t rc[SG / 4], rp[SG / 4], rn[SG / 4];  // codes: current (low), previous (high), next
+#pragma unroll
+        for (int q = 0; q < SG; ++q) {
+            dl_h[q] = 0;
+            dl_f[q] = 0;
+            bin[q] = 0;
+            bin_n[q] = 0;
+        }
+#pragma unroll
+        for (int q = 0; q < SG / 4; ++q) rp[q] = 0x19191919u;  // virtual columns before the subject
+        load_codes<SG>(rc, a.residues + base, true);
+        if (!first) load_pairs<SG>(bin, reinterpret_cast<const int32_t*>(bnd) + base);
+        int4 PL[2][4], PH[2][4];
+        read_x2<R>(PL[0], PH[0], L, code_of(rc, 0), code_of(rp, 0), 0, 0);
+
+        // sub-groups 0 .. ncols/SG: the last one runs the high strip only
+        for (uint32_t col0 = 0; col0 <= ncols; col0 += SG) {
+            const bool has_next = col0 + SG <= ncols;          // another sub-group follows
+            const bool next_lo = col0 + SG < ncols;            // ... with real low-strip columns
+            const uint32_t ncol = col0 + SG;
+            const uint64_t noff = (ncol >> 4) * kGroupBytes + (ncol & 15);
+            if (has_next) {
+                load_codes<SG>(rn, a.residues + base + noff, next_lo);
+                if (!first && next_lo) load_pairs<SG>(bin_n, reinterpret_cast<const int32_t*>(bnd) + base + noff);
+            }
+            s2 up = {0, 0}, diag = {0, 0}, f = {0, 0};
+#pragma unroll
+            for (int t = 0; t < STEPS; ++t) {
+                const int jj = t / NCH;
+                const int k = t % NCH;
+                const uint32_t dep = as_u32(k == 0 ? H[R - 1] : H[16 * k - 1]);
+                if (t + 1 < STEPS) {
+                    const int jn = (t + 1) / NCH, kn = (t + 1) % NCH;
+                    read_x2<R>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(rc, jn), code_of(rp, jn), kn, dep);
+                } else if (has_next) {
+                    read_x2<R>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(rn, 0), code_of(rc, 0), 0, dep);
+                }
+                if (k == 0) {
+                    // row -1 inputs: low strip from HBM (previous pass), high
+                    // strip from the low strip's bottom row 8 steps back
+                    const uint32_t u = lo_lo(bin[jj], dl_h[jj]);
+                    up = as_s2(u);
+                    diag = as_s2(dtop);
+                    dtop = u;
+                    if constexpr (AFFINE) f = as_s2(lo_lo(bin[jj] >> 16, dl_f[jj]));
+                }
+                const int4(&pl)[4] = PL[t & 1];
+                const int4(&ph)[4] = PH[t & 1];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int r = 16 * k + i;
+                    const s2 sc = as_s2(word(pl, i) | word(ph, i));
+                    if constexpr (!AFFINE) {
+                        const s2 h = usub2(max2(max2(H[r], up), diag + sc), go2);
+                        diag = H[r];
+                        H[r] = h;
+                        up = h;
+                        best = max2(best, h);
+                    } else {
+                        const s2 h = max2(max2(E[r], f), diag + sc);
+                        const s2 n = usub2(h, go2);
+                        E[r] = max2(usub2(E[r], ge2), n);
+                        f = max2(usub2(f, ge2), n);
+                        diag = H[r];
+                        H[r] = h;
+                        up = h;
+                        best = max2(best, h);
+                    }
+                }
+                if (k == NCH - 1) {
+                    const uint32_t oh = as_u32(up), of = AFFINE ? as_u32(f) : 0u;
+                    dl_h[jj] = oh;
+                    if constexpr (AFFINE) dl_f[jj] = of;
+                    hb[jj] = AFFINE ? hi_hi(oh, of) : (oh >> 16);
+                }
+                asm volatile("" : "+v"(best));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            // the high strip just finished columns [col0 - SG, col0)
+            if (!last && col0 >= SG) {
+                const uint32_t pc = col0 - SG;
+                const uint64_t poff = (pc >> 4) * kGroupBytes + (pc & 15);
+                store_pairs<SG>(reinterpret_cast<int32_t*>(bnd) + base + poff, hb);
+            }
+            if (has_next) {
+#pragma unroll
+                for (int q = 0; q < SG / 4; ++q) {
+                    rp[q] = rc[q];
+                    rc[q] = rn[q];
+                }
+#pragma unroll
+                for (int q = 0; q < SG; ++q) bin[q] = (first || !next_lo) ? 0u : bin_n[q];
+            }
+        }
+    }
+    const int id = a.lane_ids[static_cast<size_t>(blk) * kLanes + lane];
+    if (id >= 0) a.scores[id] = max(static_cast<int>(best.x), static_cast<int>(best.y));
+}
+
+template <int R, int SG>
+static hipError_t launch_x2s_shape(const InterArgs& a, bool affine, hipStream_t s) {
+    const dim3 grid((a.nblocks - a.blk_first + kWavesPerWG - 1) / kWavesPerWG), block(kWavesPerWG * kLanes);
+    if (affine) hipLaunchKernelGGL((sw_inter_x2s<R, SG, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((sw_inter_x2s<R, SG, false>), grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_inter_x2s(const InterArgs& a, int R, int SG, bool affine, hipStream_t s) {
+    if (a.nblocks - a.blk_first <= 0 || a.qpad <= 0) return hipSuccess;
+    if (R == 32 && SG == 8) return launch_x2s_shape<32, 8>(a, affine, s);
+    if (R == 32 && SG == 4) return launch_x2s_shape<32, 4>(a, affine, s);
+    if (R == 16 && SG == 8) return launch_x2s_shape<16, 8>(a, affine, s);
+    if (R == 48 && SG == 4) return launch_x2s_shape<48, 4>(a, affine, s);
+    return hipErrorInvalidValue;
+}
+
 template <int R, int SG>
 static hipError_t launch_x2_shape(const InterArgs& a, bool affine, hipStream_t s) {
     const int npairs = (a.nblocks - a.blk_first + 1) / 2;

@@ -94,6 +94,9 @@ int inter_rows(bool affine, bool x2_ok);
 bool inter_profile32(bool affine, bool x2_ok);
 // true if the packed two-subjects-per-lane kernel is used (int16 profile).
 bool inter_uses_x2(bool affine, bool x2_ok);
+// Wide-block cut-off for the cooperative kernel: residues / divisor columns
+// (0 = the chosen inter kernel does not use it).
+int inter_coop_divisor(bool affine, bool x2_ok);
 // Name of the per-wave inter kernel launch_inter() runs, e.g. "sw_inter_x2<16,16,affine>".
 const char* inter_kernel_name(bool affine, bool x2_ok);
 // Query rows per lane the intra kernel uses for this query (2..16, even).
@@ -116,6 +119,10 @@ hipError_t launch_inter_pk(const InterArgs& a, int R, int SG, hipStream_t s);
 // Two subjects per lane, packed int16, dual profile images (sw_inter_x2.hip);
 // blocks [blk_first, nblocks) in pairs.
 hipError_t launch_inter_x2(const InterArgs& a, int R, int SG, bool affine, hipStream_t s);
+// One subject per lane, two R-row query strips per pass in the two int16
+// halves (sw_inter_x2.hip); qpad is a multiple of 2R; boundary rows are
+// (H | F << 16) dwords in bnd_h.
+hipError_t launch_inter_x2s(const InterArgs& a, int R, int SG, bool affine, hipStream_t s);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.
 constexpr int kSat16 = 32767 - 1152;
 // int32 re-scoring of the blocks the 16-bit kernel listed (device-side count).

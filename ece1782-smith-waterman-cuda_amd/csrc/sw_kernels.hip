@@ -762,21 +762,23 @@ __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
 // ---------------------------------------------------------------------------
 // Inter-kernel shape: R query rows per strip x SG columns per software-
 // pipelined sub-group.  SW_INTER_VARIANT="RxSG" overrides (tuning only).
-struct InterShape { int R, SG; bool p32; bool i16; bool pk; bool skew = false; bool x2 = false; };
+struct InterShape { int R, SG; bool p32; bool i16; bool pk; bool skew = false; bool x2 = false; bool x2s = false; };
 static InterShape inter_shape(bool affine, bool x2_ok) {
     // measured on MI355X (scripts/tune_inter.py, profiles/r01_tune_inter.jsonl):
     // 64x8 is fastest for the linear kernel (170 VGPRs, 2 waves/SIMD, half
     // the boundary traffic of 32-row strips); affine keeps 32x8.
     // measured on MI355X: 64x8 int32 beats the 16-bit-value (h*) and int32-
     // profile (p*) variants on C2 (profiles/r01_tune_inter*.jsonl)
-    // Affine, int16-safe scans: the packed two-subjects-per-lane kernel x32x8
-    // (profiles/r01_tune_x2*.jsonl: +28% over int32 32x8 on C2 BLOSUM62 12/1;
-    // 32-row strips halve the boundary-row traffic of x16x16).
-    // Linear: int32 64x8 (packed gains nothing there: 5 packed ops per cell
-    // pair vs 3.5 int32 ops per cell).
-    InterShape v = affine ? (x2_ok ? InterShape{32, 8, false, false, false, false, true}
+    // int16-safe scans (the common case): the packed two-strips-per-lane
+    // kernel sw_inter_x2s, one subject per lane (profiles/r01_x2s/):
+    //   affine y32x8: 6.2 TCUPS on C2 BLOSUM62 11/1 (int32 32x8: 4.66;
+    //   two-subjects-per-lane x32x8 + coop: 5.92);
+    //   linear y48x4: 10.4 TCUPS on C2 BLOSUM50/2 (int32 64x8 + coop: 9.9).
+    // Otherwise int32: affine 32x8, linear 64x8 (+ the cooperative kernel).
+    InterShape v = affine ? (x2_ok ? InterShape{64, 8, false, false, false, false, false, true}
                                    : InterShape{32, 8, false, false, false})
-                          : InterShape{64, 8, false, false, false};
+                          : (x2_ok ? InterShape{96, 4, false, false, false, false, false, true}
+                                   : InterShape{64, 8, false, false, false});
     if (const char* e = std::getenv("SW_INTER_VARIANT")) {
         int r = 0, g = 0;
         if (std::sscanf(e, "k%dx%d", &r, &g) == 2 && !affine &&
@@ -788,6 +790,9 @@ static InterShape inter_shape(bool affine, bool x2_ok) {
         else if (std::sscanf(e, "p%dx%d", &r, &g) == 2 && !affine &&
             ((r == 64 && (g == 8 || g == 4)) || (r == 32 && g == 8) || (r == 48 && g == 8)))
             v = InterShape{r, g, true, false, false};
+        else if (std::sscanf(e, "y%dx%d", &r, &g) == 2 && x2_ok &&
+                 ((r == 32 && (g == 8 || g == 4)) || (r == 16 && g == 8) || (r == 48 && g == 4)))
+            v = InterShape{2 * r, g, false, false, false, false, false, true};  // R = rows per pass
         else if (std::sscanf(e, "x%dx%d", &r, &g) == 2 && x2_ok &&
             ((r == 16 && (g == 8 || g == 16)) || (r == 32 && g == 8) || (r == 48 && g == 8)))
             v = InterShape{r, g, false, false, false, false, true};
@@ -804,10 +809,27 @@ static InterShape inter_shape(bool affine, bool x2_ok) {
 int inter_rows(bool affine, bool x2_ok) { return inter_shape(affine, x2_ok).R; }
 bool inter_profile32(bool affine, bool x2_ok) { return inter_shape(affine, x2_ok).p32; }
 bool inter_uses_16bit(bool affine, bool x2_ok) { return inter_shape(affine, x2_ok).i16; }
-bool inter_uses_x2(bool affine, bool x2_ok) { return inter_shape(affine, x2_ok).x2; }
+bool inter_uses_x2(bool affine, bool x2_ok) {
+    const InterShape v = inter_shape(affine, x2_ok);
+    return v.x2 || v.x2s;
+}
+
+int inter_coop_divisor(bool affine, bool x2_ok) {
+    // blocks at least residues / divisor columns wide go to the cooperative
+    // kernel; 0 = none.  One subject per lane with two strips per pass has
+    // no long single-wave tail (measured: coop on/off within 1 %).
+    const InterShape v = inter_shape(affine, x2_ok);
+    if (v.x2s || v.pk || v.i16 || v.p32) return 0;
+    return v.x2 ? 200000 : 530000;
+}
 
 const char* inter_kernel_name(bool affine, bool x2_ok) {
     const InterShape v = inter_shape(affine, x2_ok);
+    if (v.x2s) {
+        static thread_local char b2[64];
+        std::snprintf(b2, sizeof b2, "sw_inter_x2s<%d,%d,%s>", v.R / 2, v.SG, affine ? "affine" : "linear");
+        return b2;
+    }
     const char* kind = v.x2 ? "sw_inter_x2" : v.pk ? "sw_inter_pk" : v.i16 ? "sw_inter16" : v.p32 ? "sw_inter_p32"
                                                                                                : "sw_inter";
     static thread_local char buf[96];
@@ -848,6 +870,7 @@ hipError_t launch_inter(const InterArgs& a, bool affine, bool x2_ok, hipStream_t
     const dim3 block(kWavesPerWG * kLanes);
     const InterShape v = inter_shape(affine, x2_ok);
     if (v.x2) return launch_inter_x2(a, v.R, v.SG, affine, s);
+    if (v.x2s) return launch_inter_x2s(a, v.R / 2, v.SG, affine, s);
     if (v.pk) return launch_inter_pk(a, v.R, v.SG, s);
     if (v.i16) return launch_inter16(a, v.R, v.SG, s);
     if (v.p32) {

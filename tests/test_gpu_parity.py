@@ -181,7 +181,8 @@ def test_device_topk(sw, handle, n, k):
 
 
 INTER_VARIANTS = ["32x8", "s32x8", "32x16", "s32x16", "48x8", "s48x8", "64x8", "s64x8", "16x16", "s16x16",
-                  "x16x8", "x16x16", "x32x8", "x48x8"]
+                  "x16x8", "x16x16", "x32x8", "x48x8", "y16x8", "y32x8", "y32x4",
+                  "y48x4"]
 
 
 @pytest.mark.parametrize("variant", INTER_VARIANTS)
@@ -203,7 +204,7 @@ def test_inter_variants_vs_oracle(sw, oracle, handle, monkeypatch, variant, coop
         assert np.array_equal(got, want), (qlen, mid, go, ge, np.nonzero(got != want)[0][:10])
 
 
-@pytest.mark.parametrize("variant", ["x16x8", "x32x8"])
+@pytest.mark.parametrize("variant", ["x16x8", "x32x8", "y32x8"])
 def test_x2_falls_back_to_int32_when_int16_unsafe(sw, oracle, handle, monkeypatch, variant):
     """A query long enough that (qlen + 2) * (max S + gap open) >= 32767 must
     not run the packed int16 kernel: scores stay exact (int32 path)."""
@@ -225,11 +226,17 @@ def test_x2_falls_back_to_int32_when_int16_unsafe(sw, oracle, handle, monkeypatc
 
 
 def test_default_kernel_selection(sw, handle):
-    """Affine int16-safe scans run the packed kernel; linear runs int32 64x8."""
+    """int16-safe scans run the packed two-strips-per-lane kernel; unsafe
+    ones the int32 kernels."""
     r, o = sw.synth.database(200, shard=3)
     db = sw.Database(handle, r, o)
     q = sw.synth.query(375, shard=4)
     db.scan(q, sw.capi.builtin_matrix(1), 12, 1)
-    assert handle.last_kernel() == "sw_inter_x2<32,8,affine>"
+    assert handle.last_kernel() == "sw_inter_x2s<32,8,affine>"
     db.scan(q)
+    assert handle.last_kernel() == "sw_inter_x2s<48,4,linear>"
+    # int16-unsafe ((qlen + 2) * (max S + gap open) >= 32767): int32 kernels
+    db.scan(q, sw.capi.builtin_matrix(0), 100, 1)
+    assert handle.last_kernel() == "sw_inter<32,8,affine>"
+    db.scan(q, sw.capi.builtin_matrix(0), 100, 100)
     assert handle.last_kernel() == "sw_inter<64,8,linear>"
