@@ -529,7 +529,13 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // leave int16: H <= qlen * max S, plus one profile entry (+ gap bias).
     int max_s = 0;
     for (int k = 0; k < 625; ++k) max_s = std::max<int>(max_s, mat[k]);
-    const bool x2_ok = (static_cast<int64_t>(qlen) + 2) * (max_s + go) < 32767;
+    // Beyond that bound the two-strips kernel runs guarded (saturating lanes
+    // flag their block for int32 re-scoring) as long as one cell's increment
+    // stays far inside the guard band (kSat16 leaves 1152).
+    //   m16 = 2: int16 exact; 1: guarded int16 allowed; 0: int32 only
+    const int x2_ok = (static_cast<int64_t>(qlen) + 2) * (max_s + go) < 32767 ? 2
+                      : (max_s + go < 1000 && ge < 1000)                     ? 1
+                                                                             : 0;
     const int R = swk::inter_rows(affine, x2_ok);
     const int32_t qpad_inter = static_cast<int32_t>(round_up(qlen, R));
     const int ri = db->nlong ? swk::intra_rows_for(qlen, db->long_max) : 0;
@@ -549,8 +555,9 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     const bool p32 = swk::inter_profile32(affine, x2_ok);
     const bool i16 = swk::inter_uses_16bit(affine, x2_ok);
     const bool x2 = swk::inter_uses_x2(affine, x2_ok);
-    // the int32 rescue pass after a 16-bit kernel walks 64-row strips
-    const int32_t qpad_rescue = i16 ? static_cast<int32_t>(round_up(qlen, 64)) : 0;
+    // int32 re-scoring of blocks a 16-bit kernel flags near saturation
+    const bool rescue = swk::inter_needs_rescue(affine, x2_ok);
+    const int32_t qpad_rescue = rescue ? static_cast<int32_t>(round_up(qlen, swk::rescue_rows(affine))) : 0;
     // widest blocks first, one cooperative workgroup each (int32, int8-profile paths)
     const int32_t ncoop = (!i16 && !p32 && db->nblocks) ? coop_blocks(db, swk::inter_coop_divisor(affine, x2_ok)) : 0;
     db->last_ncoop = ncoop;
@@ -558,11 +565,12 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     if ((rc = build_profiles(h, query, qlen, mat, go, affine, std::max({qpad_inter, qpad_rescue, qpad_coop}), i16 || x2,
                              p32, ri, qpad_intra, &P)))
         return rc;
-    if (i16 && db->nblocks && !db->d_rescue) {
+    if (rescue && db->nblocks && !db->d_rescue) {
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rescue), (db->nblocks + 1) * sizeof(int32_t)));
         db->device_bytes += (db->nblocks + 1) * sizeof(int32_t);
     }
-    const bool multi_inter = qpad_inter > R || qpad_rescue > 64 || qpad_coop > swk::inter_coop_rows();
+    const bool multi_inter = qpad_inter > R || qpad_rescue > swk::rescue_rows(affine) ||
+                             qpad_coop > swk::inter_coop_rows();
     const bool multi_intra = ri && qpad_intra > swk::kLanes * ri;
     if ((multi_inter || multi_intra) && (rc = ensure_bnd(db, affine))) return rc;
 
@@ -603,7 +611,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         a.bnd_h = db->d_bnd_h;
         a.bnd_f = db->d_bnd_f;
         a.scores = scores_dev;
-        if (i16) {
+        if (rescue) {
             a.rescue_count = db->d_rescue;
             a.rescue_list = db->d_rescue + 1;
             HIPCHECK(hipMemsetAsync(a.rescue_count, 0, sizeof(int32_t), h->stream));
@@ -630,7 +638,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         HIPCHECK(hipEventRecord(h->ev[7], h->stream));
         ++h->launches;
         if (ncoop) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
-        if (i16) {
+        if (rescue) {
             // int32 re-scoring of any block the 16-bit kernel flagged (rare:
             // scores near 32767); the list and its count stay on the device
             swk::InterArgs r = a;
@@ -640,7 +648,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             r.blk_count = db->d_rescue;
             r.rescue_list = nullptr;
             r.rescue_count = nullptr;
-            HIPCHECK(swk::launch_inter_rescue(r, h->stream));
+            HIPCHECK(swk::launch_inter_rescue(r, affine, h->stream));
             ++h->launches;
         }
     }

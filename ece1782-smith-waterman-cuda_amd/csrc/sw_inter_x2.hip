@@ -23,9 +23,11 @@
 // block's width read as the pad code (score 0).  Strip boundary rows are
 // packed (H, and F for affine) pairs in the wider block's slots of bnd_h/f.
 //
-// Exactness: the host routes a scan here only when (qlen + 2) * (max S + gap
-// open) < 32767, so no H, E, F or H_diag + S can leave int16 and the packed
-// recurrences equal the int32 ones (sw_kernels.hip) bit for bit.
+// Exactness: sw_inter_x2 runs only when (qlen + 2) * (max S + gap open) <
+// 32767, so no H, E, F or H_diag + S can leave int16 and the packed
+// recurrences equal the int32 ones (sw_kernels.hip) bit for bit.  sw_inter_x2s
+// also runs beyond that bound in guarded mode: lanes that reach kSat16 flag
+// their block for the int32 kernel (see the end of the kernel).
 #include "sw_kernels.h"
 
 namespace swk {
@@ -470,8 +472,17 @@ __global__ __launch_bounds__(256) void sw_inter_x2s(InterArgs a) {
             }
         }
     }
+    const int b = max(static_cast<int>(best.x), static_cast<int>(best.y));
     const int id = a.lane_ids[static_cast<size_t>(blk) * kLanes + lane];
-    if (id >= 0) a.scores[id] = max(static_cast<int>(best.x), static_cast<int>(best.y));
+    if (id >= 0) a.scores[id] = b;
+    // Guarded mode (queries too long for the static int16 bound): H grows by
+    // at most max S per cell, so a lane whose values could have wrapped has
+    // its running maximum in [kSat16, 32767] first (or, after a wrap, stays
+    // flagged); its block is re-scored by the int32 kernel from the list.
+    if (a.rescue_list) {
+        const uint64_t m = __builtin_amdgcn_ballot_w64(b >= kSat16 || b < 0);
+        if (m && lane == 0) a.rescue_list[atomicAdd(a.rescue_count, 1)] = blk;
+    }
 }
 
 template <int R, int SG>

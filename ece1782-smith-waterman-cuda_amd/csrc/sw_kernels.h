@@ -86,32 +86,32 @@ struct IntraArgs {
 
 // Strip heights (query rows held in registers per lane) the kernels are
 // instantiated for.
-// Shape of the inter kernel for this gap model.  x2_ok: the scan is provably
-// int16-safe, so the packed two-subjects-per-lane kernel may be chosen;
-// otherwise the int32 default is used.
-int inter_rows(bool affine, bool x2_ok);
+// Shape of the inter kernel for this gap model.  x2_ok: 2 = the scan is
+// provably int16-safe (any packed kernel may run); 1 = a guarded packed
+// kernel may run (saturating blocks are re-scored at int32); 0 = int32 only.
+int inter_rows(bool affine, int x2_ok);
 // true: the inter kernel takes an int32 profile [kProfileRows][prof_stride] int32
-bool inter_profile32(bool affine, bool x2_ok);
+bool inter_profile32(bool affine, int x2_ok);
 // true if the packed two-subjects-per-lane kernel is used (int16 profile).
-bool inter_uses_x2(bool affine, bool x2_ok);
+bool inter_uses_x2(bool affine, int x2_ok);
 // Wide-block cut-off for the cooperative kernel: residues / divisor columns
 // (0 = the chosen inter kernel does not use it).
-int inter_coop_divisor(bool affine, bool x2_ok);
+int inter_coop_divisor(bool affine, int x2_ok);
 // Name of the per-wave inter kernel launch_inter() runs, e.g. "sw_inter_x2<16,16,affine>".
-const char* inter_kernel_name(bool affine, bool x2_ok);
+const char* inter_kernel_name(bool affine, int x2_ok);
 // Query rows per lane the intra kernel uses for this query (2..16, even).
 int intra_rows_for(int qlen, int longest);
 // Bytes of one intra profile chunk (64*ri query rows, 32 codes).
 int intra_chunk_bytes(int ri);
 __host__ __device__ constexpr int intra_rip(int RI) { return (RI + 3) / 4 * 4; }
 
-hipError_t launch_inter(const InterArgs& a, bool affine, bool x2_ok, hipStream_t s);
+hipError_t launch_inter(const InterArgs& a, bool affine, int x2_ok, hipStream_t s);
 // Wide blocks [0, ncoop): one 4-wave workgroup per block, the waves pipelined
 // over query strips (linear gap).  Returns the strip height it uses.
 hipError_t launch_inter_coop(const InterArgs& a, int ncoop, bool affine, hipStream_t s);
 int inter_coop_rows();
 // Linear gap: true if the 16-bit inter kernel is used (profile int16 [32][stride]).
-bool inter_uses_16bit(bool affine, bool x2_ok);
+bool inter_uses_16bit(bool affine, int x2_ok);
 // The 16-bit inter kernel (sw_inter16.hip, its own translation unit).
 hipError_t launch_inter16(const InterArgs& a, int R, int SG, hipStream_t s);
 // The packed two-subjects-per-lane kernel (sw_inter_pk.hip).
@@ -125,8 +125,13 @@ hipError_t launch_inter_x2(const InterArgs& a, int R, int SG, bool affine, hipSt
 hipError_t launch_inter_x2s(const InterArgs& a, int R, int SG, bool affine, hipStream_t s);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.
 constexpr int kSat16 = 32767 - 1152;
-// int32 re-scoring of the blocks the 16-bit kernel listed (device-side count).
-hipError_t launch_inter_rescue(const InterArgs& a, hipStream_t s);
+// true if the chosen inter kernel may flag blocks for int32 re-scoring
+// (16-bit kernels beyond the static int16 bound).
+bool inter_needs_rescue(bool affine, int x2_ok);
+// int32 re-scoring of the blocks a 16-bit kernel listed (device-side count);
+// strips of rescue_rows(affine) query rows.
+int rescue_rows(bool affine);
+hipError_t launch_inter_rescue(const InterArgs& a, bool affine, hipStream_t s);
 hipError_t launch_intra(const IntraArgs& a, int ri, bool affine, hipStream_t s);
 
 // Device top-K (sw_topk.hip): keys = score << 32 | (2^31 - 1 - id), best first.

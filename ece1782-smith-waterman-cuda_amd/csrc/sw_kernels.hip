@@ -763,7 +763,7 @@ __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
 // Inter-kernel shape: R query rows per strip x SG columns per software-
 // pipelined sub-group.  SW_INTER_VARIANT="RxSG" overrides (tuning only).
 struct InterShape { int R, SG; bool p32; bool i16; bool pk; bool skew = false; bool x2 = false; bool x2s = false; };
-static InterShape inter_shape(bool affine, bool x2_ok) {
+static InterShape inter_shape(bool affine, int x2_ok) {
     // measured on MI355X (scripts/tune_inter.py, profiles/r01_tune_inter.jsonl):
     // 64x8 is fastest for the linear kernel (170 VGPRs, 2 waves/SIMD, half
     // the boundary traffic of 32-row strips); affine keeps 32x8.
@@ -775,10 +775,15 @@ static InterShape inter_shape(bool affine, bool x2_ok) {
     //   two-subjects-per-lane x32x8 + coop: 5.92);
     //   linear y48x4: 10.4 TCUPS on C2 BLOSUM50/2 (int32 64x8 + coop: 9.9).
     // Otherwise int32: affine 32x8, linear 64x8 (+ the cooperative kernel).
-    InterShape v = affine ? (x2_ok ? InterShape{64, 8, false, false, false, false, false, true}
-                                   : InterShape{32, 8, false, false, false})
-                          : (x2_ok ? InterShape{96, 4, false, false, false, false, false, true}
-                                   : InterShape{64, 8, false, false, false});
+    // Beyond the static int16 bound the packed kernel runs guarded (blocks
+    // reaching kSat16 are re-scored at int32); SW_INT16_GUARD=0 disables that.
+    // x2_ok: 2 = int16 provably exact, 1 = guarded int16 allowed, 0 = int32 only
+    const char* ge = std::getenv("SW_INT16_GUARD");
+    const bool y_ok = x2_ok == 2 || (x2_ok == 1 && !(ge && ge[0] == '0'));
+    InterShape v = affine ? (y_ok ? InterShape{64, 8, false, false, false, false, false, true}
+                                  : InterShape{32, 8, false, false, false})
+                          : (y_ok ? InterShape{96, 4, false, false, false, false, false, true}
+                                  : InterShape{64, 8, false, false, false});
     if (const char* e = std::getenv("SW_INTER_VARIANT")) {
         int r = 0, g = 0;
         if (std::sscanf(e, "k%dx%d", &r, &g) == 2 && !affine &&
@@ -790,10 +795,10 @@ static InterShape inter_shape(bool affine, bool x2_ok) {
         else if (std::sscanf(e, "p%dx%d", &r, &g) == 2 && !affine &&
             ((r == 64 && (g == 8 || g == 4)) || (r == 32 && g == 8) || (r == 48 && g == 8)))
             v = InterShape{r, g, true, false, false};
-        else if (std::sscanf(e, "y%dx%d", &r, &g) == 2 && x2_ok &&
+        else if (std::sscanf(e, "y%dx%d", &r, &g) == 2 && y_ok &&
                  ((r == 32 && (g == 8 || g == 4)) || (r == 16 && g == 8) || (r == 48 && g == 4)))
             v = InterShape{2 * r, g, false, false, false, false, false, true};  // R = rows per pass
-        else if (std::sscanf(e, "x%dx%d", &r, &g) == 2 && x2_ok &&
+        else if (std::sscanf(e, "x%dx%d", &r, &g) == 2 && x2_ok == 2 &&
             ((r == 16 && (g == 8 || g == 16)) || (r == 32 && g == 8) || (r == 48 && g == 8)))
             v = InterShape{r, g, false, false, false, false, true};
         else if (std::sscanf(e, "s%dx%d", &r, &g) == 2 &&
@@ -806,15 +811,20 @@ static InterShape inter_shape(bool affine, bool x2_ok) {
     return v;
 }
 
-int inter_rows(bool affine, bool x2_ok) { return inter_shape(affine, x2_ok).R; }
-bool inter_profile32(bool affine, bool x2_ok) { return inter_shape(affine, x2_ok).p32; }
-bool inter_uses_16bit(bool affine, bool x2_ok) { return inter_shape(affine, x2_ok).i16; }
-bool inter_uses_x2(bool affine, bool x2_ok) {
+int inter_rows(bool affine, int x2_ok) { return inter_shape(affine, x2_ok).R; }
+bool inter_profile32(bool affine, int x2_ok) { return inter_shape(affine, x2_ok).p32; }
+bool inter_uses_16bit(bool affine, int x2_ok) { return inter_shape(affine, x2_ok).i16; }
+bool inter_uses_x2(bool affine, int x2_ok) {
     const InterShape v = inter_shape(affine, x2_ok);
     return v.x2 || v.x2s;
 }
 
-int inter_coop_divisor(bool affine, bool x2_ok) {
+bool inter_needs_rescue(bool affine, int x2_ok) {
+    const InterShape v = inter_shape(affine, x2_ok);
+    return v.i16 || (v.x2s && x2_ok != 2);
+}
+
+int inter_coop_divisor(bool affine, int x2_ok) {
     // blocks at least residues / divisor columns wide go to the cooperative
     // kernel; 0 = none.  One subject per lane with two strips per pass has
     // no long single-wave tail (measured: coop on/off within 1 %).
@@ -823,7 +833,7 @@ int inter_coop_divisor(bool affine, bool x2_ok) {
     return v.x2 ? 200000 : 530000;
 }
 
-const char* inter_kernel_name(bool affine, bool x2_ok) {
+const char* inter_kernel_name(bool affine, int x2_ok) {
     const InterShape v = inter_shape(affine, x2_ok);
     if (v.x2s) {
         static thread_local char b2[64];
@@ -838,11 +848,15 @@ const char* inter_kernel_name(bool affine, bool x2_ok) {
     return buf;
 }
 
-// int32 re-scoring of the blocks the 16-bit kernel put on the rescue list.
-hipError_t launch_inter_rescue(const InterArgs& a, hipStream_t s) {
+// int32 re-scoring of the blocks a 16-bit kernel put on the rescue list.
+int rescue_rows(bool affine) { return affine ? 32 : 64; }
+hipError_t launch_inter_rescue(const InterArgs& a, bool affine, hipStream_t s) {
     // A few hundred waves walk the device-side list; an empty list costs one
     // tiny launch and no host synchronisation.
-    hipLaunchKernelGGL((sw_inter<64, 8, false, false>), dim3(64), dim3(kWavesPerWG * kLanes), 0, s, a);
+    if (affine)
+        hipLaunchKernelGGL((sw_inter<32, 8, true, false>), dim3(64), dim3(kWavesPerWG * kLanes), 0, s, a);
+    else
+        hipLaunchKernelGGL((sw_inter<64, 8, false, false>), dim3(64), dim3(kWavesPerWG * kLanes), 0, s, a);
     return hipGetLastError();
 }
 
@@ -864,7 +878,7 @@ int intra_rows_for(int qlen, int longest) {
 
 int intra_chunk_bytes(int ri) { return kProfileRows * kLanes * intra_rip(ri); }
 
-hipError_t launch_inter(const InterArgs& a, bool affine, bool x2_ok, hipStream_t s) {
+hipError_t launch_inter(const InterArgs& a, bool affine, int x2_ok, hipStream_t s) {
     if (a.nblocks - a.blk_first <= 0 || a.qpad <= 0) return hipSuccess;
     const dim3 grid((a.nblocks - a.blk_first + kWavesPerWG - 1) / kWavesPerWG);
     const dim3 block(kWavesPerWG * kLanes);

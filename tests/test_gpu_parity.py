@@ -130,23 +130,27 @@ def test_long_query_self_hit_int32(sw, oracle, handle):
     assert got == want and got > 32767
 
 
-@pytest.mark.parametrize("reps", [2100, 2190, 2300])
-def test_int16_saturation_rescue(sw, oracle, handle, reps):
-    """Scores at/above the 16-bit kernel's saturation guard are re-scored at
-    int32 (block-level rescue), next to ordinary subjects in the same block."""
+@pytest.mark.parametrize("mid,go,ge,ww,reps", [(0, 2, 2, 15, 2100), (0, 2, 2, 15, 2190), (0, 2, 2, 15, 2300),
+                                              (1, 12, 1, 11, 2870), (1, 12, 1, 11, 2990), (1, 12, 1, 11, 3100)])
+def test_int16_saturation_rescue(sw, oracle, handle, mid, go, ge, ww, reps):
+    """Scores at/above the 16-bit kernels' saturation guard are re-scored at
+    int32 (block-level rescue), next to ordinary subjects in the same block;
+    linear (BLOSUM50, W-W = 15) and affine (BLOSUM62, W-W = 11) scoring."""
     rng = np.random.default_rng(reps)
     q = sw.encode("W" * reps)
     seqs = [rng.integers(0, 20, size=rng.integers(50, 400)).astype(np.uint8) for _ in range(150)]
-    seqs[37] = sw.encode("W" * reps)            # 15 * reps: 31500 .. 34500
+    seqs[37] = sw.encode("W" * reps)            # ww * reps: 31500 .. 34500
     seqs[90] = sw.encode("W" * (reps // 2) + "A" * 30 + "W" * (reps // 2))
     res = np.concatenate(seqs)
     offs = np.zeros(len(seqs) + 1, dtype=np.int64)
     offs[1:] = np.cumsum([len(x) for x in seqs])
     db = sw.Database(handle, res, offs, long_threshold=4096)
-    got = db.scan(q)
-    want = oracle.scan(q, res, offs)
-    assert got[37] == 15 * reps
+    m = sw.capi.builtin_matrix(mid)
+    got = db.scan(q, m, go, ge)
+    want = oracle.scan(q, res, offs, mat=m, gap_open=go, gap_extend=ge)
+    assert got[37] == ww * reps
     assert np.array_equal(got, want)
+    assert handle.last_kernel().startswith("sw_inter_x2s")
 
 
 @pytest.mark.parametrize("n,k", [(10, 4), (5000, 100), (100000, 100), (300000, 1000), (7, 20)])
@@ -204,15 +208,19 @@ def test_inter_variants_vs_oracle(sw, oracle, handle, monkeypatch, variant, coop
         assert np.array_equal(got, want), (qlen, mid, go, ge, np.nonzero(got != want)[0][:10])
 
 
-@pytest.mark.parametrize("variant", ["x16x8", "x32x8", "y32x8"])
-def test_x2_falls_back_to_int32_when_int16_unsafe(sw, oracle, handle, monkeypatch, variant):
-    """A query long enough that (qlen + 2) * (max S + gap open) >= 32767 must
-    not run the packed int16 kernel: scores stay exact (int32 path)."""
-    monkeypatch.setenv("SW_INTER_VARIANT", variant)
+@pytest.mark.parametrize("guard", ["1", "0"])
+@pytest.mark.parametrize("variant", ["", "x32x8", "y32x8"])
+def test_long_query_int16_guard(sw, oracle, handle, monkeypatch, variant, guard):
+    """A query long enough that (qlen + 2) * (max S + gap open) >= 32767: the
+    two-strips kernel runs guarded (SW_INT16_GUARD unset / 1) — the two-
+    subjects x2 kernel, which has no guard, is never chosen — or the int32
+    kernel runs (SW_INT16_GUARD=0).  Scores stay exact either way."""
+    monkeypatch.setenv("SW_INT16_GUARD", guard)
+    if variant:
+        monkeypatch.setenv("SW_INTER_VARIANT", variant)
     r, o = sw.synth.database(300, shard=5)
     q = sw.synth.query(2400, shard=9)
-    # plant a near-copy of the query so one score is large (> 32767 would
-    # wrap in int16): the subject is the query itself
+    # plant the query itself as a subject so one score is large
     r2 = np.concatenate([r, q])
     o2 = np.concatenate([o, [o[-1] + len(q)]])
     db = sw.Database(handle, r2, o2, long_threshold=3000)
@@ -222,12 +230,17 @@ def test_x2_falls_back_to_int32_when_int16_unsafe(sw, oracle, handle, monkeypatc
         want = oracle.scan(q, r2, o2, mat=m, gap_open=go, gap_extend=ge)
         assert np.array_equal(got, want), (mid, np.nonzero(got != want)[0][:10])
         assert got[-1] > 9000
-        assert not handle.last_kernel().startswith("sw_inter_x2"), handle.last_kernel()
+        k = handle.last_kernel()
+        if guard == "0":
+            assert not k.startswith("sw_inter_x2"), k
+        else:
+            assert k.startswith("sw_inter_x2s"), k
 
 
-def test_default_kernel_selection(sw, handle):
-    """int16-safe scans run the packed two-strips-per-lane kernel; unsafe
-    ones the int32 kernels."""
+def test_default_kernel_selection(sw, handle, monkeypatch):
+    """int16-safe scans run the packed two-strips-per-lane kernel; longer
+    queries run it guarded; gaps too large for the guard band, or the guard
+    switched off, run the int32 kernels."""
     r, o = sw.synth.database(200, shard=3)
     db = sw.Database(handle, r, o)
     q = sw.synth.query(375, shard=4)
@@ -235,8 +248,12 @@ def test_default_kernel_selection(sw, handle):
     assert handle.last_kernel() == "sw_inter_x2s<32,8,affine>"
     db.scan(q)
     assert handle.last_kernel() == "sw_inter_x2s<48,4,linear>"
-    # int16-unsafe ((qlen + 2) * (max S + gap open) >= 32767): int32 kernels
+    # beyond the static int16 bound but inside the guard band: guarded packed
     db.scan(q, sw.capi.builtin_matrix(0), 100, 1)
+    assert handle.last_kernel() == "sw_inter_x2s<32,8,affine>"
+    # max S + gap open >= 1000: int32
+    db.scan(q, sw.capi.builtin_matrix(0), 1000, 1)
     assert handle.last_kernel() == "sw_inter<32,8,affine>"
+    monkeypatch.setenv("SW_INT16_GUARD", "0")
     db.scan(q, sw.capi.builtin_matrix(0), 100, 100)
     assert handle.last_kernel() == "sw_inter<64,8,linear>"
