@@ -1,20 +1,28 @@
 #!/usr/bin/env python3
 """bench.py — headline measurement of the Smith-Waterman database scan.
 
-Workload (BASELINE.json configs[1]): the 375-residue
-query P07327 (data/queries/P07327.fasta of the reference, shipped as a fixture)
-against a Swiss-Prot-sized synthetic database (570,000 subjects, log-normal
-lengths median 290 / mean ~360, Swiss-Prot residue frequencies; Swiss-Prot
-itself is not available here), scored as configs[1] states: BLOSUM62 with
-affine gaps, BLAST's default 11/1 (a gap of k residues costs 11 + k, i.e.
-gap_open 12 and gap_extend 1 in this library's convention).  The reference's
-own scoring (BLOSUM50 of SWSolver.cu:54-81, linear gap 2) is timed the same
-way right after and reported under "reference_scoring".
+Default workload (BASELINE.json configs[1]): the
+375-residue query P07327 (data/queries/P07327.fasta of the reference, shipped
+as a fixture) against a Swiss-Prot-sized synthetic database (570,000
+subjects, log-normal lengths median 290 / mean ~360, Swiss-Prot residue
+frequencies; Swiss-Prot itself is not available here), scored as configs[1]
+states: BLOSUM62 with affine gaps, BLAST's default 11/1 (a gap of k residues
+costs 11 + k, i.e. gap_open 12 and gap_extend 1 in this library's
+convention).  The reference's own scoring (BLOSUM50 of SWSolver.cu:54-81,
+linear gap 2) is timed the same way right after and reported under
+"reference_scoring".
+
+--config c3: the 20 shipped queries (144..5478 aa, sum 41,752) as one batch
+against the same database (configs[2]); --config c5: a 5,000-residue
+synthetic query against 10,000 subjects of N(2000, 200) residues
+(configs[4]).  These are the other BASELINE configurations, measured with
+the same code; the driver's headline is the default (c2).
 
 One step = one pass of the hot path over the rank's resident shard: build the
-query profile, run the intra-sequence kernel (subjects longer than the long
-threshold) and the inter-sequence kernel, then the top-K exchange (local
-top-K, RCCL all-gather of K (score, id) keys per rank, global merge).
+query profile(s), run the scan kernels (intra-sequence for subjects longer
+than the long threshold, inter-sequence for the rest), then the top-K
+exchange (device top-K per query, RCCL all-gather of K (score, id) keys per
+rank, device merge).
 
 Multi-GPU (torchrun, one process per GPU): every rank holds its OWN shard of
 the same size (weak scaling; shard = the rank's seed), so the global database
@@ -55,6 +63,9 @@ VALU_MODEL = {
     "sw_inter<32,8,affine>": (2.82 * 2.45 + 1.83 * 4.37 + 1.5 * 4.4 + 4.2) / 64,
 }
 MATRICES = {"blosum50": 0, "blosum62": 1}
+C3_QUERIES = ["P02232", "P05013", "P14942", "P07327", "P01008", "P03435", "P42357", "P21177",
+              "Q38941", "P27895", "P07756", "P04775", "P19096", "P28167", "P0C6B8", "P20930",
+              "P08519", "Q7TMA5", "P33450", "Q9UKN1"]
 
 
 def log(*a):
@@ -84,10 +95,11 @@ def valu_roofline(kernel, cells_rank, scan_ms, kernel_gcups):
             "kernel_alone_gcups_while_concurrent": round(kernel_gcups, 1)}
 
 
-def cpu_baseline(sw, q, res, offs, gpu_scores, seconds, threads, scoring):
+def cpu_baseline(sw, queries, res, offs, gpu_scores, seconds, threads, scoring):
     """The oracle (C restatement of cpu.cpp's recurrence, Gotoh for affine;
-    kind "port") on a bounded random sample of the same shard, on this host's
-    cores, with the same scoring as the GPU run."""
+    kind "port") on a bounded random sample of the same shard, every query of
+    the workload, on this host's cores, with the same scoring as the GPU run.
+    gpu_scores: [nq][n] scores of the measured run (parity check)."""
     mat, go, ge = scoring
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import sw_oracle
@@ -103,30 +115,56 @@ def cpu_baseline(sw, q, res, offs, gpu_scores, seconds, threads, scoring):
         sr = np.concatenate([res[offs[i]:offs[i + 1]] for i in idx]) if m else np.zeros(0, np.uint8)
         return idx, sr, so
 
+    def run(sr, so):
+        return [sw_oracle.scan(q, sr, so, mat=mat, gap_open=go, gap_extend=ge, nthreads=threads) for q in queries]
+
     # calibrate on a small sample, then size the real one to ~`seconds`
-    idx, sr, so = sample(min(n, 2000))
+    m0 = min(n, 200)
+    idx, sr, so = sample(m0)
     t = time.perf_counter()
-    sw_oracle.scan(q, sr, so, mat=mat, gap_open=go, gap_extend=ge, nthreads=threads)
+    run(sr, so)
     dt = max(time.perf_counter() - t, 1e-3)
-    m = int(min(n, max(2000, 2000 * seconds / dt)))
+    m = int(min(n, max(m0, m0 * seconds / dt)))
     idx, sr, so = sample(m)
     t = time.perf_counter()
-    cpu = sw_oracle.scan(q, sr, so, mat=mat, gap_open=go, gap_extend=ge, nthreads=threads)
+    cpu = run(sr, so)
     dt = time.perf_counter() - t
-    cells = len(q) * int(so[-1])
-    parity = bool(np.array_equal(cpu, gpu_scores[idx]))
+    qtot = sum(len(q) for q in queries)
+    cells = qtot * int(so[-1])
+    parity = all(bool(np.array_equal(c, gpu_scores[k][idx])) for k, c in enumerate(cpu))
     return {"value": round(cells / dt / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": "port",
-            "sample": "%d of %d subjects (%d residues, %.3g cells) of rank 0's shard, same query, "
+            "sample": "%d of %d subjects (%d residues) of rank 0's shard x %d quer%s (%d residues), %.3g cells, "
                       "%.1f s on %d threads; scores equal to the GPU's: %s"
-                      % (m, n, int(so[-1]), cells, dt, threads, parity)}, parity
+                      % (m, n, int(so[-1]), len(queries), "y" if len(queries) == 1 else "ies", qtot, cells, dt,
+                         threads, parity)}, parity
+
+
+def make_workload(sw, args, rank):
+    """(queries [code arrays], query names, residues, offsets, description)."""
+    if args.config == "c2":
+        res, offs = sw.synth.database(args.db_seqs, shard=rank)
+        return [sw.encode(read_query(args.query))], [args.query], res, offs, \
+            "C2: query %s (%d aa) vs synthetic Swiss-Prot-sized db" % (args.query, len(read_query(args.query)))
+    if args.config == "c3":
+        res, offs = sw.synth.database(args.db_seqs, shard=rank)
+        qs = [sw.encode(read_query(n)) for n in C3_QUERIES]
+        return qs, C3_QUERIES, res, offs, \
+            "C3: batch of the %d shipped queries (%d..%d aa, sum %d) vs synthetic Swiss-Prot-sized db" % (
+                len(qs), min(map(len, qs)), max(map(len, qs)), sum(map(len, qs)))
+    # c5: one 5,000-residue query vs 10,000 subjects of N(2000, 200)
+    res, offs = sw.synth.fixed_length_database(args.db_seqs, 2000, 200, shard=rank)
+    return [sw.synth.query(5000)], ["synthetic-5000"], res, offs, \
+        "C5: synthetic 5000-aa query vs N(2000, 200)-residue subjects"
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--db-seqs", type=int, default=570000, help="subjects per rank")
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5"],
+                    help="c2 = the headline (BASELINE configs[1]); c3 / c5 = configs[2] / [4]")
+    ap.add_argument("--steps", type=int, default=None, help="default 10 (c2, c5) / 3 (c3)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 2 (c2, c5) / 1 (c3)")
+    ap.add_argument("--db-seqs", type=int, default=None, help="subjects per rank (default 570000; c5: 10000)")
     ap.add_argument("--query", default="P07327")
     ap.add_argument("--topk", type=int, default=100)
     ap.add_argument("--matrix", default="blosum62", choices=sorted(MATRICES))
@@ -143,6 +181,12 @@ def main():
                     help="gloo = rehearse the multi-rank path on one GPU (CPU collectives)")
     ap.add_argument("--device", type=int, default=None, help="override the GPU index (rehearsal)")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 3 if args.config == "c3" else 10
+    if args.warmup is None:
+        args.warmup = 1 if args.config == "c3" else 2
+    if args.db_seqs is None:
+        args.db_seqs = 10000 if args.config == "c5" else 570000
 
     import torch
     import torch.distributed as dist
@@ -165,10 +209,11 @@ def main():
     sw = _swpkg.load()
 
     t0 = time.perf_counter()
-    res, offs = sw.synth.database(args.db_seqs, shard=rank)
+    queries, qnames, res, offs, desc = make_workload(sw, args, rank)
     n = len(offs) - 1
     residues = int(offs[-1])
-    q = sw.encode(read_query(args.query))
+    nq = len(queries)
+    qtot = sum(len(q) for q in queries)
     log("rank %d: shard %d subjects, %d residues, generated in %.1fs" % (rank, n, residues, time.perf_counter() - t0))
 
     handle = sw.Handle(gpu)
@@ -183,31 +228,36 @@ def main():
     st = db.stats()
     log("rank %d: packed + uploaded in %.1fs: %s" % (rank, time.perf_counter() - t0, st))
 
-    scores = torch.zeros(n, dtype=torch.int32, device=dev)
+    scores = torch.zeros((nq, n), dtype=torch.int32, device=dev)
     K = min(args.topk, n)
-    top = torch.empty(K, dtype=torch.int64, device=dev)
-    gathered = torch.empty(world * K, dtype=torch.int64, device=dev)
-    final = torch.empty(K, dtype=torch.int64, device=dev)
+    top = torch.empty((nq, K), dtype=torch.int64, device=dev)
+    gathered = torch.empty((world, nq, K), dtype=torch.int64, device=dev)
+    final = torch.empty((nq, K), dtype=torch.int64, device=dev)
 
     mat = sw.capi.builtin_matrix(MATRICES[args.matrix])
     scoring = (mat, args.gap_open, args.gap_extend)
 
     def step():
-        db.scan_device(q, scores.data_ptr(), *scoring)
-        # device top-K: int64 keys (score << 32 | 2^31-1-global id), best first
-        handle.topk_device(scores.data_ptr(), n, K, top.data_ptr(), id_base=rank * n)
-        if world == 1:
-            return top
-        if args.backend == "nccl":
-            dist.all_gather_into_tensor(gathered, top)  # RCCL over xGMI: K x 8 B per rank
+        if nq == 1:
+            db.scan_device(queries[0], scores.data_ptr(), *scoring)
         else:
-            parts = [torch.empty(K, dtype=torch.int64) for _ in range(world)]
+            db.scan_batch_device(queries, scores.data_ptr(), *scoring)
+        # device top-K per query: int64 keys (score << 32 | 2^31-1-global id), best first
+        for k in range(nq):
+            handle.topk_device(scores[k].data_ptr(), n, K, top[k].data_ptr(), id_base=rank * n)
+        if world == 1:
+            return
+        if args.backend == "nccl":
+            dist.all_gather_into_tensor(gathered, top)  # RCCL over xGMI: nq x K x 8 B per rank
+        else:
+            parts = [torch.empty((nq, K), dtype=torch.int64) for _ in range(world)]
             dist.all_gather(parts, top.cpu())
-            gathered.copy_(torch.cat(parts))
-        handle.topk_keys_device(gathered.data_ptr(), world * K, K, final.data_ptr())
-        return final
+            gathered.copy_(torch.stack(parts))
+        for k in range(nq):
+            merged = gathered[:, k, :].contiguous()
+            handle.topk_keys_device(merged.data_ptr(), world * K, K, final[k].data_ptr())
 
-    cells_rank = float(len(q)) * residues
+    cells_rank = float(qtot) * residues
 
     def timed_loop():
         """W untimed steps, then K timed steps between barrier + sync pairs;
@@ -241,7 +291,7 @@ def main():
     elapsed_max, cells_all, kt, kernel = timed_loop()
     st = db.stats()  # the coop split of the timed scans
     final_keys = (final if world > 1 else top).cpu().numpy()
-    top_ids, top_scores = sw.capi.decode_keys(final_keys)
+    top_ids, top_scores = sw.capi.decode_keys(final_keys[0])
     gs = scores.cpu().numpy() if (not args.no_cpu_baseline and world == 1 and rank == 0) else None
 
     ref = None
@@ -252,10 +302,10 @@ def main():
         ref = {"scoring": "BLOSUM50 (SWSolver.cu:54-81), linear gap 2 (the reference's own)",
                "value": round(r_cells * args.steps / r_elapsed / 1e9, 2), "unit": "GCUPS",
                "ms_per_step": round(r_elapsed * 1e3 / args.steps, 3), "kernel": r_kernel,
-               "kernel_ms": {"sw_inter": round(r_kt["wave_ms"] / r_n, 4),
-                             "sw_inter_coop": round(r_kt["coop_ms"] / r_n, 4),
-                             "sw_intra": round(r_kt["intra_ms"] / r_n, 4),
-                             "scan_total": round(r_kt["total_ms"] / r_n, 4)}}
+               "kernel_ms_per_scan": {"sw_inter": round(r_kt["wave_ms"] / r_n, 4),
+                                      "sw_inter_coop": round(r_kt["coop_ms"] / r_n, 4),
+                                      "sw_intra": round(r_kt["intra_ms"] / r_n, 4),
+                                      "scan_total": round(r_kt["total_ms"] / r_n, 4)}}
 
     if rank == 0:
         value = cells_all * args.steps / elapsed_max / 1e9
@@ -266,11 +316,12 @@ def main():
         wave_ms = kt["wave_ms"] / nsc
         coop_ms = kt["coop_ms"] / nsc
         # Dominant kernel: the per-wave inter-sequence kernel (most of the
-        # cells; the cooperative kernel takes the widest blocks beside it on
-        # another stream, the intra kernel the long subjects).
-        # Its duration is HIP events around its launch on its own stream.
-        # Algorithmic bytes per launch: 1 B per residue it
-        # scans + 12 B per subject (offset, length, int32 score).
+        # cells; the intra kernel takes the long subjects beside it on a side
+        # stream; int32 paths also run a cooperative kernel on the widest
+        # blocks).  Its duration is HIP events around its launch on its own
+        # stream, per scan (per query for c3).  Algorithmic bytes per launch
+        # (SURVEY.md §8d): 1 B per residue it scans + 12 B per subject
+        # (offset, length, int32 score).
         lens_desc = np.sort(offs[1:] - offs[:-1])[::-1]
         n_inter = n - st["n_long"]
         inter_res = residues - int(lens_desc[:st["n_long"]].sum())
@@ -278,12 +329,13 @@ def main():
         wave_res = inter_res - st["coop_residues"]
         alg_bytes = wave_res + 12 * (n_inter - n_coop)
         achieved = alg_bytes / (wave_ms * 1e-3) / 1e9 if wave_ms > 0 else 0.0
-        wave_gcups = float(len(q)) * wave_res / (wave_ms * 1e-3) / 1e9 if wave_ms > 0 else 0.0
+        wave_gcups = float(qtot) / nq * wave_res / (wave_ms * 1e-3) / 1e9 if wave_ms > 0 else 0.0
         traffic = None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("workload_key") == workload_key(args, len(q)) and tj.get("kernel") == kernel:
+            if (args.config == "c2" and tj.get("workload_key") == workload_key(args, qtot)
+                    and tj.get("kernel") == kernel):
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -301,36 +353,39 @@ def main():
             "dtype": "int32",
             "data": "synthetic",
             "config": {
-                "workload": "C2: query %s (%d aa) vs synthetic Swiss-Prot-sized db, %d subjects/rank "
-                            "(%d residues/rank), %s, gap open %d / extend %d (BLAST 11/1), top-%d "
-                            "all-gathered" % (args.query, len(q), n, residues, args.matrix.upper(),
-                                              args.gap_open, args.gap_extend, K),
+                "workload": "%s, %d subjects/rank (%d residues/rank), %s, gap open %d / extend %d%s, top-%d "
+                            "all-gathered" % (desc, n, residues, args.matrix.upper(), args.gap_open,
+                                              args.gap_extend,
+                                              " (BLAST 11/1)" if (args.gap_open, args.gap_extend) == (12, 1) else "",
+                                              K),
+                "config": args.config,
                 "scoring": {"matrix": args.matrix, "gap_open": args.gap_open, "gap_extend": args.gap_extend},
-                "query": args.query, "query_len": int(len(q)), "subjects_per_rank": n,
-                "residues_per_rank": residues, "parallelism": "db-shard x%d + RCCL allgather top-K" % world,
+                "queries": qnames if nq > 1 else qnames[0], "query_residues": int(qtot),
+                "subjects_per_rank": n, "residues_per_rank": residues,
+                "parallelism": "db-shard x%d + RCCL allgather top-K" % world,
                 "long_threshold": st["long_threshold"], "long_subjects": st["n_long"],
                 "cells_per_step": cells_all,
             },
-            "kernel_ms": {"inter_phase": round(inter_ms, 4), "sw_inter": round(wave_ms, 4),
-                          "sw_inter_coop": round(coop_ms, 4), "sw_intra": round(intra_ms, 4),
-                          "scan_total": round(kt["total_ms"] / nsc, 4)},
-            "cells_split": {"sw_inter": float(len(q)) * wave_res,
-                            "sw_inter_coop": float(len(q)) * st["coop_residues"],
-                            "sw_intra": float(len(q)) * (residues - inter_res)},
+            "kernel_ms_per_scan": {"inter_phase": round(inter_ms, 4), "sw_inter": round(wave_ms, 4),
+                                   "sw_inter_coop": round(coop_ms, 4), "sw_intra": round(intra_ms, 4),
+                                   "scan_total": round(kt["total_ms"] / nsc, 4)},
+            "cells_split_per_step": {"sw_inter": float(qtot) * wave_res,
+                                     "sw_inter_coop": float(qtot) * st["coop_residues"],
+                                     "sw_intra": float(qtot) * (residues - inter_res)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": traffic,
                          "kernel": kernel,
                          "alg_bytes_per_launch": int(alg_bytes), "kernel_ms": round(wave_ms, 4)},
-            "valu_roofline": valu_roofline(kernel, cells_all / world, kt["total_ms"] / nsc, wave_gcups),
+            "valu_roofline": valu_roofline(kernel, cells_all / world, kt["total_ms"] / nsc * nq, wave_gcups),
             "top_hit": {"id": int(top_ids[0]), "score": int(top_scores[0])},
         }
         if ref is not None:
             out["reference_scoring"] = ref
         if gs is not None:
             threads = min(args.cpu_threads, os.cpu_count() or 1)
-            cb, parity = cpu_baseline(sw, q, res, offs, gs, args.cpu_seconds, threads, scoring=(mat, args.gap_open,
-                                                                                              args.gap_extend))
+            cb, parity = cpu_baseline(sw, queries, res, offs, gs, args.cpu_seconds, threads,
+                                      scoring=(mat, args.gap_open, args.gap_extend))
             out["cpu_baseline"] = cb
             out["parity_sample_ok"] = parity
         print(json.dumps(out), flush=True)

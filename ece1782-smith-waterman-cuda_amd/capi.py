@@ -24,7 +24,7 @@ EXPORTED = (
     "sw_version", "sw_last_error", "sw_encode", "sw_builtin_matrix",
     "sw_create", "sw_destroy", "sw_stream", "sw_set_stream",
     "sw_db_create", "sw_db_free", "sw_db_get_stats", "sw_db_set_long_threshold",
-    "sw_scan", "sw_scan_device", "sw_scan_batch", "sw_get_timing",
+    "sw_scan", "sw_scan_device", "sw_scan_batch", "sw_scan_batch_device", "sw_get_timing",
     "sw_timing_reset", "sw_timing_total", "sw_last_kernel",
     "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_score_pair",
 )
@@ -97,6 +97,7 @@ def lib():
         "sw_scan": (ctypes.c_int, [vp, vp, u8p, i32, ctypes.POINTER(Scoring), i32p]),
         "sw_scan_device": (ctypes.c_int, [vp, vp, u8p, i32, ctypes.POINTER(Scoring), vp]),
         "sw_scan_batch": (ctypes.c_int, [vp, vp, u8p, i64p, i32, ctypes.POINTER(Scoring), i32p]),
+        "sw_scan_batch_device": (ctypes.c_int, [vp, vp, u8p, i64p, i32, ctypes.POINTER(Scoring), vp]),
         "sw_get_timing": (ctypes.c_int, [vp, ctypes.POINTER(Timing)]),
         "sw_timing_reset": (ctypes.c_int, [vp]),
         "sw_timing_total": (ctypes.c_int, [vp, ctypes.POINTER(Timing), i32p]),
@@ -290,12 +291,26 @@ class Database:
         _check(lib().sw_scan_device(self.handle.ptr, self._d, qp, len(q), sc.ptr(),
                                     ctypes.c_void_p(scores_dev_ptr)))
 
-    def scan_batch(self, queries, matrix=None, gap_open=2, gap_extend=None):
-        """queries: list of code arrays; returns [nq, n_out] int32."""
-        cat = np.concatenate([np.asarray(q, dtype=np.uint8) for q in queries]) if queries else \
+    @staticmethod
+    def _cat(queries):
+        cat = np.concatenate([np.asarray(q, dtype=np.uint8) for q in queries]) if len(queries) else \
             np.zeros(0, dtype=np.uint8)
         offs = np.zeros(len(queries) + 1, dtype=np.int64)
         offs[1:] = np.cumsum([len(q) for q in queries])
+        return cat, offs
+
+    def scan_batch_device(self, queries, scores_dev_ptr, matrix=None, gap_open=2, gap_extend=None):
+        """Asynchronous batch scan into a device int32 buffer [nq, n_out]."""
+        cat, offs = self._cat(queries)
+        c, cp = _u8(cat)
+        sc = _ScoringArg(matrix, gap_open, gap_extend)
+        _check(lib().sw_scan_batch_device(self.handle.ptr, self._d, cp,
+                                          offs.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), len(queries),
+                                          sc.ptr(), ctypes.c_void_p(scores_dev_ptr)))
+
+    def scan_batch(self, queries, matrix=None, gap_open=2, gap_extend=None):
+        """queries: list of code arrays; returns [nq, n_out] int32."""
+        cat, offs = self._cat(queries)
         c, cp = _u8(cat)
         sc = _ScoringArg(matrix, gap_open, gap_extend)
         out = np.zeros((len(queries), self.n_out), dtype=np.int32)

@@ -171,12 +171,21 @@ struct sw_handle {
     hipEvent_t coop_done = nullptr;
     // per-query workspace: profiles (inter: [32][stride]; intra: lane-slotted
     // chunks) built in pinned host buffers, copied once per query
-    int8_t* d_prof = nullptr;
-    size_t prof_cap = 0;
-    int8_t* h_prof = nullptr;
-    size_t h_prof_cap = 0;
-    hipEvent_t prof_copied = nullptr;  // the staging buffer may be rewritten after this
-    bool prof_pending = false;
+    // A ring of profile slots (pinned staging + device copy): building the
+    // next query's profile waits only for the H2D copy made kProfSlots scans
+    // ago, not for the scans still running, so back-to-back scans
+    // (sw_scan_batch*) keep the GPU busy.
+    struct ProfSlot {
+        int8_t* d = nullptr;
+        size_t dcap = 0;
+        int8_t* h = nullptr;
+        size_t hcap = 0;
+        hipEvent_t copied = nullptr;  // the staging buffer may be rewritten after this
+        bool pending = false;
+    };
+    static constexpr int kProfSlots = 4;
+    ProfSlot prof[kProfSlots];
+    int prof_next = 0;
     int32_t* d_scores = nullptr;  // for the synchronous sw_scan
     size_t scores_cap = 0;
     int64_t* d_topk_work = nullptr;  // device top-K workspace
@@ -236,9 +245,19 @@ namespace {
 // blocks the best is ~2048 (profiles/r01_tune_coop.jsonl).  Default: 5.7 x
 // mean length, clamped.
 
+//
+// Small databases: the inter kernels put one 64-subject block on a wave and
+// need ~2 waves per SIMD (2048 blocks, ~131k subjects) to fill the chip.
+// Below ~1000 blocks the one-wave-per-subject wavefront kernel is the faster
+// path for subjects of a few hundred residues and up (config C5, 10,000
+// subjects of ~2000 aa vs a 5000-aa query: 2.7 TCUPS all-intra vs 0.62 TCUPS
+// inter, profiles/r01_c5/), so everything longer than 64 residues goes there.
+constexpr int64_t kSmallDbSubjects = 64 * 1000;
+
 int32_t default_long_threshold(const sw_db* db) {
     if (db->n == 0) return 1536;
     const double mean = static_cast<double>(db->residues) / static_cast<double>(db->n);
+    if (db->n < kSmallDbSubjects && mean >= 256) return 64;
     const double t = 5.7 * mean;
     return static_cast<int32_t>(std::min(8192.0, std::max(1024.0, t)));
 }
@@ -394,6 +413,7 @@ int check_scoring(const sw_scoring* sc, const int8_t** mat, int* go, int* ge) {
 // predecessors)).  Intra kernel: the same values laid out per chunk of
 // 64*ri query rows as [code][lane][RIP] so each lane's ri rows are contiguous.
 struct Profiles {
+    int8_t* dev = nullptr;  // device copy of this scan's profiles
     int32_t stride = 0;      // inter profiles: entries per code row
     size_t off8 = 0;         // int8 inter profile (biased for linear)
     size_t off16 = 0;        // int16 inter profile (16-bit kernel)
@@ -422,23 +442,25 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     const size_t intra_bytes = ri ? static_cast<size_t>(qpad_intra / (swk::kLanes * ri)) * swk::intra_chunk_bytes(ri) : 0;
     P->intra_off = take(intra_bytes);
     P->total = at;
-    if (P->total > h->h_prof_cap) {
-        if (h->prof_pending) HIPCHECK(hipEventSynchronize(h->prof_copied));
-        h->prof_pending = false;
-        if (h->h_prof) HIPCHECK(hipHostFree(h->h_prof));
-        h->h_prof_cap = std::max<size_t>(P->total, 1 << 16);
-        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h->h_prof), h->h_prof_cap, hipHostMallocDefault));
+    sw_handle::ProfSlot& S = h->prof[h->prof_next];
+    h->prof_next = (h->prof_next + 1) % sw_handle::kProfSlots;
+    if (S.pending) HIPCHECK(hipEventSynchronize(S.copied));  // its last copy has consumed the staging buffer
+    S.pending = false;
+    if (P->total > S.hcap) {
+        if (S.h) HIPCHECK(hipHostFree(S.h));
+        S.hcap = std::max<size_t>(P->total, 1 << 16);
+        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&S.h), S.hcap, hipHostMallocDefault));
     }
-    if (P->total > h->prof_cap) {
-        if (h->d_prof) {
-            HIPCHECK(hipStreamSynchronize(h->stream));
-            HIPCHECK(hipFree(h->d_prof));
+    if (P->total > S.dcap) {
+        if (S.d) {
+            HIPCHECK(hipStreamSynchronize(h->stream));  // scans in flight may still read it
+            HIPCHECK(hipFree(S.d));
         }
-        h->prof_cap = std::max<size_t>(P->total, 1 << 16);
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&h->d_prof), h->prof_cap));
+        S.dcap = std::max<size_t>(P->total, 1 << 16);
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&S.d), S.dcap));
     }
-    if (h->prof_pending) HIPCHECK(hipEventSynchronize(h->prof_copied));  // previous copy consumed the buffer
-    int8_t* hp = h->h_prof;
+    P->dev = S.d;
+    int8_t* hp = S.h;
     auto value = [&](int c, int64_t row) -> int {
         if (c >= SW_ALPHABET || row >= qlen) return bias;
         return mat[25 * q[row] + c] + bias;
@@ -465,9 +487,9 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
                     for (int r = 0; r < rip; ++r) d[r] = static_cast<int8_t>(r < ri ? value(c, ch * CH + t * ri + r) : 0);
                 }
     }
-    HIPCHECK(hipMemcpyAsync(h->d_prof, hp, P->total, hipMemcpyHostToDevice, h->stream));
-    HIPCHECK(hipEventRecord(h->prof_copied, h->stream));
-    h->prof_pending = true;
+    HIPCHECK(hipMemcpyAsync(S.d, hp, P->total, hipMemcpyHostToDevice, h->stream));
+    HIPCHECK(hipEventRecord(S.copied, h->stream));
+    S.pending = true;
     return SW_OK;
 }
 
@@ -584,7 +606,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         ia.subj_len = db->d_llen;
         ia.subj_id = db->d_lid;
         ia.nsubj = static_cast<int32_t>(db->nlong);
-        ia.prof = h->d_prof + P.intra_off;
+        ia.prof = P.dev + P.intra_off;
         ia.qpad = qpad_intra;
         ia.gap_open = go;
         ia.gap_extend = ge;
@@ -603,7 +625,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         a.blk_groups = db->d_blk_groups;
         a.lane_ids = db->d_lane_ids;
         a.nblocks = static_cast<int32_t>(db->nblocks);
-        a.prof = h->d_prof + ((i16 || x2) ? P.off16 : p32 ? P.off32 : P.off8);
+        a.prof = P.dev + ((i16 || x2) ? P.off16 : p32 ? P.off32 : P.off8);
         a.prof_stride = P.stride;
         a.qpad = qpad_inter;
         a.gap_open = go;
@@ -620,7 +642,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             // on its own stream, so the per-wave kernel fills the GPU beside it
             swk::InterArgs c = a;
             c.qpad = qpad_coop;
-            c.prof = h->d_prof + P.off8;  // the coop kernel reads the int8 profile
+            c.prof = P.dev + P.off8;  // the coop kernel reads the int8 profile
             HIPCHECK(hipStreamWaitEvent(h->side2, h->ev[0], 0));
             HIPCHECK(hipEventRecord(h->ev[4], h->side2));
             HIPCHECK(swk::launch_inter_coop(c, ncoop, affine, h->side2));
@@ -642,7 +664,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             // int32 re-scoring of any block the 16-bit kernel flagged (rare:
             // scores near 32767); the list and its count stay on the device
             swk::InterArgs r = a;
-            r.prof = h->d_prof + P.off8;
+            r.prof = P.dev + P.off8;
             r.qpad = qpad_rescue;
             r.blk_list = db->d_rescue + 1;
             r.blk_count = db->d_rescue;
@@ -739,7 +761,8 @@ int sw_create(int32_t device, sw_handle** out) {
     h->own_stream = true;
     e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side2, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->prof_copied, hipEventDisableTiming);
+    for (auto& S : h->prof)
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&S.copied, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->coop_done, hipEventDisableTiming);
     if (e != hipSuccess) { delete h; return fail(SW_E_HIP, hipGetErrorString(e)); }
     *out = h;
@@ -755,9 +778,11 @@ int sw_destroy(sw_handle* h) {
             if (ev) (void)hipEventDestroy(ev);
     if (h->side) (void)hipStreamSynchronize(h->side);
     if (h->side2) (void)hipStreamSynchronize(h->side2);
-    if (h->d_prof) (void)hipFree(h->d_prof);
-    if (h->h_prof) (void)hipHostFree(h->h_prof);
-    if (h->prof_copied) (void)hipEventDestroy(h->prof_copied);
+    for (auto& S : h->prof) {
+        if (S.d) (void)hipFree(S.d);
+        if (S.h) (void)hipHostFree(S.h);
+        if (S.copied) (void)hipEventDestroy(S.copied);
+    }
     if (h->d_scores) (void)hipFree(h->d_scores);
     if (h->d_topk_work) (void)hipFree(h->d_topk_work);
     if (h->side) (void)hipStreamDestroy(h->side);
@@ -888,15 +913,51 @@ int sw_scan(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen, c
     return SW_OK;
 }
 
-int sw_scan_batch(sw_handle* h, const sw_db* db, const uint8_t* queries, const int64_t* qoffsets, int32_t nq,
-                  const sw_scoring* sc, int32_t* scores_host) {
-    if (!h || !db || nq < 0 || (nq > 0 && (!qoffsets || !scores_host))) return fail(SW_E_INVALID, "null argument");
-    const size_t n = static_cast<size_t>(db->max_id + 1);
+namespace {
+int check_batch(const int64_t* qoffsets, int32_t nq) {
+    if (nq > 0 && qoffsets[0] < 0) return fail(SW_E_INVALID, "bad query offsets");
     for (int32_t k = 0; k < nq; ++k) {
         const int64_t ql = qoffsets[k + 1] - qoffsets[k];
         if (ql < 0 || ql > (int64_t(1) << 24)) return fail(SW_E_INVALID, "bad query offsets");
-        int rc = sw_scan(h, db, queries + qoffsets[k], static_cast<int32_t>(ql), sc, scores_host + k * n);
-        if (rc) return rc;
+    }
+    return SW_OK;
+}
+}  // namespace
+
+int sw_scan_batch_device(sw_handle* h, const sw_db* db, const uint8_t* queries, const int64_t* qoffsets, int32_t nq,
+                         const sw_scoring* sc, int32_t* scores_dev) {
+    if (!h || !db || nq < 0 || (nq > 0 && (!qoffsets || !queries || !scores_dev)))
+        return fail(SW_E_INVALID, "null argument");
+    int rc;
+    if ((rc = check_batch(qoffsets, nq))) return rc;
+    const size_t n = static_cast<size_t>(db->max_id + 1);
+    // back to back on the handle's stream: no host synchronisation between
+    // queries (profiles go through the slot ring), so the GPU never idles
+    for (int32_t k = 0; k < nq; ++k)
+        if ((rc = scan_impl(h, db, queries + qoffsets[k], static_cast<int32_t>(qoffsets[k + 1] - qoffsets[k]), sc,
+                            scores_dev + k * n)))
+            return rc;
+    return SW_OK;
+}
+
+int sw_scan_batch(sw_handle* h, const sw_db* db, const uint8_t* queries, const int64_t* qoffsets, int32_t nq,
+                  const sw_scoring* sc, int32_t* scores_host) {
+    if (!h || !db || nq < 0 || (nq > 0 && (!qoffsets || !queries || !scores_host)))
+        return fail(SW_E_INVALID, "null argument");
+    int rc;
+    if ((rc = check_batch(qoffsets, nq))) return rc;
+    const size_t n = static_cast<size_t>(db->max_id + 1);
+    if (n == 0 || nq == 0) return SW_OK;
+    HIPCHECK(hipSetDevice(h->device));
+    // chunks of queries whose score rows fit in ~1 GiB of device memory
+    const int32_t chunk = static_cast<int32_t>(std::max<size_t>(1, std::min<size_t>(nq, (size_t(1) << 30) / (n * 4))));
+    if ((rc = ensure_scores(h, chunk * n))) return rc;
+    for (int32_t k0 = 0; k0 < nq; k0 += chunk) {
+        const int32_t m = std::min(chunk, nq - k0);
+        HIPCHECK(hipMemsetAsync(h->d_scores, 0, m * n * 4, h->stream));  // unmapped slots read 0
+        if ((rc = sw_scan_batch_device(h, db, queries, qoffsets + k0, m, sc, h->d_scores))) return rc;
+        HIPCHECK(hipMemcpyAsync(scores_host + k0 * n, h->d_scores, m * n * 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHECK(hipStreamSynchronize(h->stream));
     }
     return SW_OK;
 }

@@ -124,9 +124,12 @@ SW_API int sw_db_create(sw_handle* h, const uint8_t* residues, const int64_t* of
                  int64_t n, const int32_t* ids, sw_db** out);
 SW_API int sw_db_free(sw_db* db);
 SW_API int sw_db_get_stats(const sw_db* db, sw_db_stats* out);
-/* Subjects longer than `threshold` go to the intra-sequence kernel
- * (default chosen at sw_db_create; 0 = library default).  Must be called
- * before the first scan. */
+/* Subjects longer than `threshold` go to the intra-sequence kernel (one
+ * wave per subject) instead of the inter-sequence kernels (one subject per
+ * lane).  0 = library default: 5.7 x the mean length clamped to
+ * [1024, 8192], or 64 for databases under 64,000 subjects with a mean
+ * length >= 256 (too few 64-subject blocks to fill the GPU).  May be changed
+ * between scans (re-packs the database). */
 SW_API int sw_db_set_long_threshold(sw_db* db, int32_t threshold);
 
 /* ---- scans ---------------------------------------------------------------
@@ -144,12 +147,19 @@ SW_API int sw_scan(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t 
 SW_API int sw_scan_device(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen,
                    const sw_scoring* sc, int32_t* scores_dev);
 
-/* Batch of nq queries (concatenated encoded residues, nq+1 offsets);
- * scores_host is [nq][max(id)+1].  Consecutive queries overlap on the
- * device (main.cpp handles one query per run).     */
+/* Batch of nq queries (concatenated encoded residues, nq+1 offsets, query
+ * k = queries[qoffsets[k] .. qoffsets[k+1])); scores_host is
+ * [nq][max(id)+1].  The scans run back to back on the device with no host
+ * synchronisation between queries (the reference's
+ * main.cpp handles one query per run).  Synchronous.                      */
 SW_API int sw_scan_batch(sw_handle* h, const sw_db* db, const uint8_t* queries,
                   const int64_t* qoffsets, int32_t nq, const sw_scoring* sc,
                   int32_t* scores_host);
+/* Same, asynchronous on the handle's stream, into DEVICE memory scores_dev
+ * [nq][max(id)+1] (only slots some subject maps to are written).          */
+SW_API int sw_scan_batch_device(sw_handle* h, const sw_db* db, const uint8_t* queries,
+                  const int64_t* qoffsets, int32_t nq, const sw_scoring* sc,
+                  int32_t* scores_dev);
 
 /* Timing of the most recent scan on this handle (waits for it). */
 SW_API int sw_get_timing(sw_handle* h, sw_timing* out);

@@ -257,3 +257,22 @@ def test_default_kernel_selection(sw, handle, monkeypatch):
     monkeypatch.setenv("SW_INT16_GUARD", "0")
     db.scan(q, sw.capi.builtin_matrix(0), 100, 100)
     assert handle.last_kernel() == "sw_inter<64,8,linear>"
+
+def test_batch_all_shipped_queries_c3(sw, oracle, handle):
+    """Config C3's shape at test size: the 20 shipped queries (144..5478 aa,
+    int16-exact, guarded and int32 paths mixed) in one batch, host and
+    device entry points, against the oracle query by query."""
+    import torch
+    r, o = sw.synth.database(700, shard=21)
+    db = sw.Database(handle, r, o)
+    qs = [sw.encode(read_query(n)) for n in QUERIES]
+    m = sw.capi.builtin_matrix(1)
+    out = db.scan_batch(qs, m, 12, 1)
+    dev = torch.zeros((len(qs), db.n_out), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()  # the fill ran on torch's stream, the scans run on the handle's
+    db.scan_batch_device(qs, dev.data_ptr(), m, 12, 1)
+    torch.cuda.synchronize()  # device-wide: waits for the handle's streams too
+    assert np.array_equal(dev.cpu().numpy(), out)
+    for k, q in enumerate(qs):
+        want = oracle.scan(q, r, o, mat=m, gap_open=12, gap_extend=1)
+        assert np.array_equal(out[k], want), (QUERIES[k], np.nonzero(out[k] != want)[0][:10])
