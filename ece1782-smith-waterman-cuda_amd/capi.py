@@ -26,7 +26,8 @@ EXPORTED = (
     "sw_db_create", "sw_db_free", "sw_db_get_stats", "sw_db_set_long_threshold",
     "sw_scan", "sw_scan_device", "sw_scan_batch", "sw_scan_batch_device", "sw_get_timing",
     "sw_timing_reset", "sw_timing_total", "sw_last_kernel",
-    "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_score_pair",
+    "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_score_pair", "sw_align",
+    "sw_db_save", "sw_db_load", "sw_db_subjects",
 )
 
 
@@ -45,7 +46,13 @@ class DbStats(ctypes.Structure):
                 ("packed_cells", ctypes.c_int64), ("n_blocks", ctypes.c_int64),
                 ("n_long", ctypes.c_int64), ("device_bytes", ctypes.c_int64),
                 ("max_length", ctypes.c_int32), ("long_threshold", ctypes.c_int32),
-                ("coop_blocks", ctypes.c_int32), ("coop_residues", ctypes.c_int64)]
+                ("coop_blocks", ctypes.c_int32), ("coop_residues", ctypes.c_int64),
+                ("max_id", ctypes.c_int32)]
+
+
+class Alignment(ctypes.Structure):
+    _fields_ = [("score", ctypes.c_int32), ("q_begin", ctypes.c_int32), ("q_end", ctypes.c_int32),
+                ("s_begin", ctypes.c_int32), ("s_end", ctypes.c_int32), ("ops_len", ctypes.c_int32)]
 
 
 class Timing(ctypes.Structure):
@@ -102,6 +109,10 @@ def lib():
         "sw_timing_reset": (ctypes.c_int, [vp]),
         "sw_timing_total": (ctypes.c_int, [vp, ctypes.POINTER(Timing), i32p]),
         "sw_last_kernel": (ctypes.c_char_p, [vp]),
+        "sw_db_save": (ctypes.c_int, [vp, ctypes.c_char_p]),
+        "sw_db_load": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.POINTER(vp)]),
+        "sw_align": (ctypes.c_int, [vp, vp, u8p, i32, ctypes.POINTER(Scoring), i32p, i32,
+                                    ctypes.POINTER(Alignment), ctypes.c_char_p, ctypes.c_int64]),
         "sw_topk": (ctypes.c_int, [i32p, i64, i32, i32p, i32p]),
         "sw_topk_device": (ctypes.c_int, [vp, vp, i64, i64, i32, vp]),
         "sw_topk_keys_device": (ctypes.c_int, [vp, vp, i64, i32, vp]),
@@ -251,6 +262,26 @@ class Database:
         if long_threshold is not None:
             self.set_long_threshold(long_threshold)
 
+    @classmethod
+    def load(cls, handle, path, long_threshold=None):
+        """A database from a sw_db_save file (one read, no FASTA parsing)."""
+        self = cls.__new__(cls)
+        self.handle = handle
+        d = ctypes.c_void_p()
+        _check(lib().sw_db_load(handle.ptr, os.fsencode(path), ctypes.byref(d)))
+        self._d = d
+        st = self.stats()
+        self.n = st["n_subjects"]
+        self.n_out = st["max_id"] + 1
+        handle._dbs.add(self)
+        if long_threshold is not None:
+            self.set_long_threshold(long_threshold)
+        return self
+
+    def save(self, path):
+        """Write the binary database file (sw_db_save)."""
+        _check(lib().sw_db_save(self._d, os.fsencode(path)))
+
     @property
     def ptr(self):
         return self._d
@@ -290,6 +321,26 @@ class Database:
         sc = _ScoringArg(matrix, gap_open, gap_extend)
         _check(lib().sw_scan_device(self.handle.ptr, self._d, qp, len(q), sc.ptr(),
                                     ctypes.c_void_p(scores_dev_ptr)))
+
+    def align(self, query_codes, ids, matrix=None, gap=2, gap_extend=None):
+        """Traceback of the query against the subjects with these result ids
+        (sw_align: cpu.cpp's tie rules, linear gap).  Returns a list of dicts
+        {score, q_begin, q_end, s_begin, s_end, ops} like the oracle's align."""
+        q, qp = _u8(query_codes)
+        idv = np.ascontiguousarray(ids, dtype=np.int32)
+        n = len(idv)
+        sc = _ScoringArg(matrix, gap, gap if gap_extend is None else gap_extend)
+        out = (Alignment * max(n, 1))()
+        stride = len(q) + int(self.stats()["max_length"]) + 1
+        buf = ctypes.create_string_buffer(max(n, 1) * stride)
+        _check(lib().sw_align(self.handle.ptr, self._d, qp, len(q), sc.ptr(),
+                              idv.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n, out, buf, stride))
+        res = []
+        for k in range(n):
+            a = out[k]
+            res.append({"score": a.score, "q_begin": a.q_begin, "q_end": a.q_end, "s_begin": a.s_begin,
+                        "s_end": a.s_end, "ops": buf.raw[k * stride: k * stride + a.ops_len].decode()})
+        return res
 
     @staticmethod
     def _cat(queries):

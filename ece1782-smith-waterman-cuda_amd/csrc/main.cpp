@@ -8,8 +8,13 @@
 //
 // Extra, optional: --metrics-json prints one JSON line after the METRICS
 // block with the kernel-only time and algorithmic GCUPS (unpadded cells).
+// Binary databases: --make-db OUT with --db FASTA
+// writes OUT (sw_db_save) and exits; --db X.swdb scans such a file with the
+// same output (same ids, same order) as the FASTA it came from, without
+// parsing FASTA.
 #include <sys/time.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <map>
@@ -18,6 +23,9 @@
 
 #include "FASTAParsers.h"
 #include "SWSolver.h"
+#include "sw_amd.h"
+
+void sw_save_fasta_db(FASTADatabase& fdb, const std::string& path);  // swsolver.cpp
 
 namespace {
 
@@ -31,7 +39,8 @@ void usage() {
     std::cout << "Smith-Waterman MI355X Usage:\n"
               << "  --help                Display this help message\n"
               << "  --query arg           Path to query file (required)\n"
-              << "  --db arg              Path to database file (required)\n";
+              << "  --db arg              Path to database file (required; FASTA, or a .swdb file)\n"
+              << "  --make-db arg         Write the FASTA --db as a binary .swdb database and exit\n";
 }
 
 }  // namespace
@@ -54,7 +63,7 @@ int main(int argc, char* argv[]) {
             if (i + 1 >= argc) { usage(); return 1; }
             val = argv[++i];
         }
-        if (key != "query" && key != "db" && key != "metrics-json") {
+        if (key != "query" && key != "db" && key != "metrics-json" && key != "make-db") {
             std::cerr << "unrecognised option '--" << key << "'\n";
             return 1;
         }
@@ -62,10 +71,24 @@ int main(int argc, char* argv[]) {
     }
     // reference: a missing required option prints the description and exits 1
     // (main.cpp:38-41), --help likewise (main.cpp:33-36)
+    if (opt.count("make-db") && opt.count("db") && !help) {
+        FASTADatabase fdb(opt["db"]);
+        try {
+            sw_save_fasta_db(fdb, opt["make-db"]);
+        } catch (const std::exception& e) {
+            std::cerr << e.what() << "\n";
+            return 1;
+        }
+        cout << "Wrote " << opt["make-db"] << ": " << fdb.numSubjects << " subjects, " << fdb.subjectLengthSum
+             << " padded residues." << endl;
+        return 0;
+    }
     if (!opt.count("query") || !opt.count("db") || help || argc <= 1) {
         usage();
         return 1;
     }
+    const std::string& dbpath = opt["db"];
+    const bool binary = dbpath.size() > 5 && dbpath.compare(dbpath.size() - 5, 5, ".swdb") == 0;
 
     FASTAQuery query(opt["query"], true);
     cout << "Input buffer:";
@@ -73,13 +96,51 @@ int main(int argc, char* argv[]) {
     cout << endl;
     string querySequence = query.get_buffer();
 
-    FASTADatabase db(opt["db"]);
-
     vector<seqid_score> result;
     result.reserve(600000);
-    const double t_solve = now_s();
-    smith_waterman_cuda(query, db, result);
-    const double solve_s = now_s() - t_solve;
+    int64_t num_subjects = 0, length_sum = 0;
+    double solve_s = 0;
+    if (!binary) {
+        FASTADatabase db(dbpath);
+        const double t_solve = now_s();
+        smith_waterman_cuda(query, db, result);
+        solve_s = now_s() - t_solve;
+        num_subjects = db.numSubjects;
+        length_sum = db.subjectLengthSum;
+    } else {
+        // the file holds the reference's order and record ids (sw_save_fasta_db)
+        auto die = [](const char* what) {
+            std::cerr << what << ": " << sw_last_error() << "\n";
+            return 1;
+        };
+        sw_handle* h = nullptr;
+        const char* dev = std::getenv("SW_DEVICE");
+        if (sw_create(dev ? std::atoi(dev) : 0, &h)) return die("sw_create");
+        sw_db* sdb = nullptr;
+        if (sw_db_load(h, dbpath.c_str(), &sdb)) return die("sw_db_load");
+        sw_db_stats st;
+        sw_db_get_stats(sdb, &st);
+        std::vector<int64_t> lens(static_cast<size_t>(st.n_subjects));
+        std::vector<int32_t> ids(static_cast<size_t>(st.n_subjects));
+        sw_db_subjects(sdb, lens.data(), ids.data());
+        std::string q = query.get_buffer();
+        while (q.size() % 8 != 0) q += "/";  // the reference pads the query (SWSolver.cu:267-269)
+        std::vector<uint8_t> qc(q.size());
+        sw_encode(q.data(), static_cast<int64_t>(q.size()), qc.data());
+        std::vector<int32_t> scores(static_cast<size_t>(st.max_id + 1), 0);
+        const sw_scoring sc = {nullptr, 2, 2};  // BLOSUM50 (SWSolver.cu:54-81), gap 2 (:7)
+        const double t_solve = now_s();
+        if (st.n_subjects && sw_scan(h, sdb, qc.data(), static_cast<int32_t>(qc.size()), &sc, scores.data()))
+            return die("sw_scan");
+        solve_s = now_s() - t_solve;
+        for (int64_t k = 0; k < st.n_subjects; ++k) {
+            result.push_back(std::make_pair(static_cast<int>(ids[k]), scores[ids[k]]));
+            length_sum += lens[k];
+        }
+        num_subjects = st.n_subjects;
+        sw_db_free(sdb);
+        sw_destroy(h);
+    }
 
     for (vector<seqid_score>::iterator it = result.begin(); it != result.end(); ++it)
         cout << (*it).first << ":" << (*it).second << "\n";
@@ -88,14 +149,14 @@ int main(int argc, char* argv[]) {
     cout << std::string(80, '=') << endl;
     cout << "METRICS:" << endl;
     cout << "Query length: " << querySequence.length() << " chars." << endl;
-    cout << "Num subjects: " << db.numSubjects << endl;
-    cout << "Sum of DB length: " << db.subjectLengthSum << " chars." << endl;
+    cout << "Num subjects: " << num_subjects << endl;
+    cout << "Sum of DB length: " << length_sum << " chars." << endl;
     cout << "Time elapsed: " << seconds_elapsed << " seconds." << endl;
-    cout << "Performance: " << 1E-9 * (querySequence.length() * static_cast<double>(db.subjectLengthSum)) / seconds_elapsed
+    cout << "Performance: " << 1E-9 * (querySequence.length() * static_cast<double>(length_sum)) / seconds_elapsed
          << " GCUPS." << endl;
     if (opt.count("metrics-json")) {
-        cout << "{\"query_len\": " << querySequence.length() << ", \"subjects\": " << db.numSubjects
-             << ", \"padded_residues\": " << db.subjectLengthSum << ", \"wall_s\": " << seconds_elapsed
+        cout << "{\"query_len\": " << querySequence.length() << ", \"subjects\": " << num_subjects
+             << ", \"padded_residues\": " << length_sum << ", \"wall_s\": " << seconds_elapsed
              << ", \"solve_s\": " << solve_s << "}" << endl;
     }
     return 0;

@@ -23,6 +23,7 @@
 #include <numeric>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/sw_amd.h"
@@ -231,6 +232,7 @@ struct sw_db {
     std::vector<uint8_t> h_residues;
     std::vector<int64_t> h_offsets;
     std::vector<int32_t> h_ids;
+    std::unordered_map<int32_t, int64_t> id_index;  // result id -> subject (built on first sw_align)
     bool built = false;
     size_t device_bytes = 0;
 };
@@ -853,6 +855,108 @@ int sw_db_create(sw_handle* h, const uint8_t* residues, const int64_t* offsets, 
     return SW_OK;
 }
 
+// ---- binary database file ---------------------------
+namespace {
+constexpr char kDbMagic[8] = {'S', 'W', 'A', 'M', 'D', 'D', 'B', '1'};
+struct DbFileHeader {
+    char magic[8];
+    int64_t n;         // subjects
+    int64_t residues;  // total residue codes
+    int32_t max_len;
+    int32_t version;   // 1
+    uint64_t fnv;      // FNV-1a 64 over offsets, ids and residues
+};
+
+uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+    const auto* b = static_cast<const uint8_t*>(p);
+    for (size_t k = 0; k < n; ++k) h = (h ^ b[k]) * 1099511628211ull;
+    return h;
+}
+}  // namespace
+
+int sw_db_save(const sw_db* db, const char* path) {
+    if (!db || !path) return fail(SW_E_INVALID, "null argument");
+    // length-sorted (descending, stable), ids kept: loading gives identical scores[id]
+    const int64_t n = db->n;
+    std::vector<int64_t> order(n);
+    std::iota(order.begin(), order.end(), 0);
+    auto len = [&](int64_t k) { return db->h_offsets[k + 1] - db->h_offsets[k]; };
+    std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return len(x) > len(y); });
+    std::vector<int64_t> offs(n + 1, 0);
+    std::vector<int32_t> ids(n);
+    std::vector<uint8_t> res(static_cast<size_t>(db->residues));
+    for (int64_t k = 0; k < n; ++k) {
+        const int64_t src = order[k];
+        std::memcpy(res.data() + offs[k], db->h_residues.data() + db->h_offsets[src], len(src));
+        offs[k + 1] = offs[k] + len(src);
+        ids[k] = db->h_ids[src];
+    }
+    DbFileHeader hd{};
+    std::memcpy(hd.magic, kDbMagic, 8);
+    hd.n = n;
+    hd.residues = db->residues;
+    hd.max_len = db->max_len;
+    hd.version = 1;
+    uint64_t f = 1469598103934665603ull;
+    f = fnv1a(f, offs.data(), offs.size() * sizeof(int64_t));
+    f = fnv1a(f, ids.data(), ids.size() * sizeof(int32_t));
+    hd.fnv = fnv1a(f, res.data(), res.size());
+    FILE* fp = std::fopen(path, "wb");
+    if (!fp) return fail(SW_E_IO, std::string("cannot open ") + path);
+    bool ok = std::fwrite(&hd, sizeof hd, 1, fp) == 1 &&
+              std::fwrite(offs.data(), sizeof(int64_t), offs.size(), fp) == offs.size() &&
+              (n == 0 || std::fwrite(ids.data(), sizeof(int32_t), ids.size(), fp) == ids.size()) &&
+              (res.empty() || std::fwrite(res.data(), 1, res.size(), fp) == res.size());
+    ok = (std::fclose(fp) == 0) && ok;
+    if (!ok) return fail(SW_E_IO, std::string("write failed: ") + path);
+    return SW_OK;
+}
+
+int sw_db_load(sw_handle* h, const char* path, sw_db** out) {
+    if (!h || !path || !out) return fail(SW_E_INVALID, "null argument");
+    *out = nullptr;
+    FILE* fp = std::fopen(path, "rb");
+    if (!fp) return fail(SW_E_IO, std::string("cannot open ") + path);
+    DbFileHeader hd{};
+    std::vector<int64_t> offs;
+    std::vector<int32_t> ids;
+    std::vector<uint8_t> res;
+    int rc = SW_OK;
+    if (std::fread(&hd, sizeof hd, 1, fp) != 1 || std::memcmp(hd.magic, kDbMagic, 8) != 0 || hd.version != 1 ||
+        hd.n < 0 || hd.residues < 0 || hd.n > (int64_t(1) << 40) || hd.residues > (int64_t(1) << 44)) {
+        rc = fail(SW_E_IO, std::string("not a database file (sw_db_save format 1): ") + path);
+    } else {
+        try {
+            offs.resize(hd.n + 1);
+            ids.resize(hd.n);
+            res.resize(static_cast<size_t>(hd.residues));
+        } catch (...) {
+            rc = fail(SW_E_NOMEM, "out of host memory");
+        }
+        if (!rc && (std::fread(offs.data(), sizeof(int64_t), offs.size(), fp) != offs.size() ||
+                    (hd.n && std::fread(ids.data(), sizeof(int32_t), ids.size(), fp) != ids.size()) ||
+                    (hd.residues && std::fread(res.data(), 1, res.size(), fp) != res.size())))
+            rc = fail(SW_E_IO, std::string("truncated database file: ") + path);
+    }
+    std::fclose(fp);
+    if (rc) return rc;
+    uint64_t f = 1469598103934665603ull;
+    f = fnv1a(f, offs.data(), offs.size() * sizeof(int64_t));
+    f = fnv1a(f, ids.data(), ids.size() * sizeof(int32_t));
+    if (fnv1a(f, res.data(), res.size()) != hd.fnv || offs.back() != hd.residues)
+        return fail(SW_E_IO, std::string("database file checksum mismatch: ") + path);
+    return sw_db_create(h, res.data(), offs.data(), hd.n, ids.data(), out);
+}
+
+int sw_db_subjects(const sw_db* db, int64_t* lengths, int32_t* ids) {
+    if (!db) return fail(SW_E_INVALID, "null argument");
+    for (int64_t k = 0; k < db->n; ++k) {
+        if (lengths) lengths[k] = db->h_offsets[k + 1] - db->h_offsets[k];
+        if (ids) ids[k] = db->h_ids[k];
+    }
+    return SW_OK;
+}
+
 int sw_db_free(sw_db* db) {
     if (!db) return SW_OK;
     (void)hipSetDevice(db->h->device);
@@ -876,6 +980,7 @@ int sw_db_get_stats(const sw_db* db, sw_db_stats* out) {
     out->coop_blocks = db->built ? db->last_ncoop : 0;
     out->coop_residues = 0;
     for (int32_t b = 0; b < out->coop_blocks; ++b) out->coop_residues += db->h_blk_res[b];
+    out->max_id = db->max_id;
     return SW_OK;
 }
 
@@ -1036,6 +1141,123 @@ int sw_topk_device(sw_handle* h, const int32_t* scores_dev, int64_t n, int64_t i
 
 int sw_topk_keys_device(sw_handle* h, const int64_t* keys_dev, int64_t n, int32_t k, int64_t* keys_out_dev) {
     return topk_impl(h, nullptr, keys_dev, n, 0, k, keys_out_dev);
+}
+
+int sw_align(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen, const sw_scoring* sc,
+             const int32_t* ids, int32_t n, sw_alignment* out, char* ops, int64_t ops_stride) {
+    sw_db* db = const_cast<sw_db*>(cdb);
+    if (!h || !db || n < 0 || qlen < 0 || (qlen > 0 && !query) || (n > 0 && (!ids || !out)) ||
+        (ops && ops_stride <= 0))
+        return fail(SW_E_INVALID, "null argument");
+    const int8_t* mat;
+    int go, ge, rc;
+    if ((rc = check_scoring(sc, &mat, &go, &ge))) return rc;
+    if (go != ge) return fail(SW_E_UNSUPPORTED, "sw_align: traceback is implemented for linear gaps only");
+    for (int32_t i = 0; i < qlen; ++i)
+        if (query[i] >= SW_ALPHABET) return fail(SW_E_INVALID, "query residue code out of range (use sw_encode)");
+    if (db->id_index.empty())
+        for (int64_t k = 0; k < db->n; ++k) db->id_index.emplace(db->h_ids[k], k);
+    std::vector<int64_t> sidx(n);
+    for (int32_t k = 0; k < n; ++k) {
+        auto it = db->id_index.find(ids[k]);
+        if (it == db->id_index.end()) return fail(SW_E_INVALID, "sw_align: id not in the database");
+        sidx[k] = it->second;
+    }
+    std::memset(out, 0, sizeof(sw_alignment) * static_cast<size_t>(n));
+    if (n == 0 || qlen == 0) return SW_OK;
+    HIPCHECK(hipSetDevice(h->device));
+    auto slen_of = [&](int64_t k) { return db->h_offsets[k + 1] - db->h_offsets[k]; };
+    // groups of hits whose direction arrays fit a 1 GiB budget
+    const int64_t W1 = static_cast<int64_t>(qlen) + 1;
+    int32_t k0 = 0;
+    while (k0 < n) {
+        int64_t bytes = 0, res = 0;
+        int32_t k1 = k0;
+        while (k1 < n) {
+            const int64_t b = (qlen + slen_of(sidx[k1]) + 1) * W1;
+            if (k1 > k0 && bytes + b > (int64_t(1) << 30)) break;
+            bytes += b;
+            res += slen_of(sidx[k1]);
+            ++k1;
+        }
+        const int32_t m = k1 - k0;
+        std::vector<uint8_t> hsub(static_cast<size_t>(std::max<int64_t>(res, 1)));
+        std::vector<int64_t> hoff(m + 1, 0), hdoff(m, 0);
+        int64_t dacc = 0;
+        for (int32_t k = 0; k < m; ++k) {
+            const int64_t src = sidx[k0 + k], L = slen_of(src);
+            std::memcpy(hsub.data() + hoff[k], db->h_residues.data() + db->h_offsets[src], L);
+            hoff[k + 1] = hoff[k] + L;
+            hdoff[k] = dacc;
+            dacc += (qlen + L + 1) * W1;
+        }
+        uint8_t *dq = nullptr, *dsub = nullptr, *ddir = nullptr;
+        int64_t *doff = nullptr, *ddoff = nullptr;
+        int8_t* dmat = nullptr;
+        int32_t *dh = nullptr, *dout = nullptr;
+        char* dops = nullptr;
+        auto cleanup = [&]() {
+            void* ptrs[] = {dq, dsub, ddir, doff, ddoff, dmat, dh, dout, dops};
+            for (void* p : ptrs)
+                if (p) (void)hipFree(p);
+        };
+        hipError_t e = hipSuccess;
+        auto alloc = [&](auto** p, size_t b) {
+            if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(b, 1));
+        };
+        alloc(&dq, qlen);
+        alloc(&dsub, hsub.size());
+        alloc(&doff, (m + 1) * sizeof(int64_t));
+        alloc(&ddoff, m * sizeof(int64_t));
+        alloc(&dmat, 625);
+        alloc(&ddir, static_cast<size_t>(dacc));
+        alloc(&dh, static_cast<size_t>(m) * 3 * W1 * sizeof(int32_t));
+        alloc(&dout, static_cast<size_t>(m) * 6 * sizeof(int32_t));
+        if (ops) alloc(&dops, static_cast<size_t>(m) * ops_stride);
+        if (e == hipSuccess) e = hipMemcpyAsync(dq, query, qlen, hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(dsub, hsub.data(), hsub.size(), hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(doff, hoff.data(), (m + 1) * sizeof(int64_t), hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(ddoff, hdoff.data(), m * sizeof(int64_t), hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(dmat, mat, 625, hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess) {
+            swk::AlignArgs a{};
+            a.query = dq;
+            a.qlen = qlen;
+            a.subj = dsub;
+            a.subj_off = doff;
+            a.n = m;
+            a.mat = dmat;
+            a.gap = go;
+            a.dirs = ddir;
+            a.dirs_off = ddoff;
+            a.hbuf = dh;
+            a.out = dout;
+            a.ops = dops;
+            a.ops_stride = ops ? ops_stride : 0;
+            e = swk::launch_align(a, h->stream);
+        }
+        std::vector<int32_t> hout(static_cast<size_t>(m) * 6);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(hout.data(), dout, hout.size() * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess && ops)
+            e = hipMemcpyAsync(ops + static_cast<int64_t>(k0) * ops_stride, dops, static_cast<size_t>(m) * ops_stride,
+                               hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        cleanup();
+        if (e != hipSuccess) return fail(SW_E_HIP, hipGetErrorString(e));
+        for (int32_t k = 0; k < m; ++k) {
+            sw_alignment& o = out[k0 + k];
+            if (slen_of(sidx[k0 + k]) == 0) continue;  // empty subject: all zero (as the oracle)
+            o.score = hout[6 * k];
+            o.q_begin = hout[6 * k + 1];
+            o.q_end = hout[6 * k + 2];
+            o.s_begin = hout[6 * k + 3];
+            o.s_end = hout[6 * k + 4];
+            o.ops_len = hout[6 * k + 5];
+        }
+        k0 = k1;
+    }
+    return SW_OK;
 }
 
 int sw_score_pair(sw_handle* h, const uint8_t* query, int32_t qlen, const uint8_t* subject, int32_t slen,

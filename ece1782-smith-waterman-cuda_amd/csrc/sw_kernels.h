@@ -134,6 +134,24 @@ int rescue_rows(bool affine);
 hipError_t launch_inter_rescue(const InterArgs& a, bool affine, hipStream_t s);
 hipError_t launch_intra(const IntraArgs& a, int ri, bool affine, hipStream_t s);
 
+// Traceback of chosen hits (sw_align.hip), linear gap, cpu.cpp's tie rules.
+struct AlignArgs {
+    const uint8_t* query;
+    int32_t qlen;
+    const uint8_t* subj;       // the hits' subject residues, concatenated
+    const int64_t* subj_off;   // n+1 offsets
+    int32_t n;
+    const int8_t* mat;         // 25 x 25
+    int32_t gap;
+    uint8_t* dirs;             // per hit: (qlen + slen + 1) x (qlen + 1) direction bytes
+    const int64_t* dirs_off;   // per hit offset into dirs
+    int32_t* hbuf;             // per hit: 3 x (qlen + 1) int32 diagonal scratch
+    int32_t* out;              // per hit: score, q_begin, q_end, s_begin, s_end, ops_len
+    char* ops;                 // per hit: ops_stride bytes (may be null)
+    int64_t ops_stride;
+};
+hipError_t launch_align(const AlignArgs& a, hipStream_t s);
+
 // Device top-K (sw_topk.hip): keys = score << 32 | (2^31 - 1 - id), best first.
 size_t topk_workspace_bytes(int64_t n, int k);
 hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, int k,

@@ -87,6 +87,22 @@ void smith_waterman_cuda(FASTAQuery& query, FASTADatabase& db, std::vector<seqid
     for (size_t k = 0; k < scores.size(); ++k) result.push_back(std::make_pair(f.record_ids[k], scores[k]));
 }
 
+// Not part of the reference interface: writes the flattened database (the
+// reference's reporting order, record ids as result ids) as a sw_db_save
+// file, for `main --make-db`.
+void sw_save_fasta_db(FASTADatabase& fdb, const std::string& path) {
+    std::lock_guard<std::mutex> lock(g_mu);
+    const Flat f = flatten(fdb);
+    const int64_t n = static_cast<int64_t>(f.record_ids.size());
+    std::vector<int32_t> ids(f.record_ids.begin(), f.record_ids.end());
+    sw_db* db = nullptr;
+    check(sw_db_create(handle(), f.residues.data(), f.offsets.data(), n, n ? ids.data() : nullptr, &db),
+          "sw_db_create");
+    const int rc = sw_db_save(db, path.c_str());
+    sw_db_free(db);
+    check(rc, "sw_db_save");
+}
+
 std::vector<seqid_score> smith_waterman_cuda_char(FASTAQuery& query, FASTADatabase& db) {
     std::lock_guard<std::mutex> lock(g_mu);
     const Flat f = flatten(db);

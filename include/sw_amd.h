@@ -50,6 +50,8 @@ extern "C" {
 #define SW_E_HIP -2       /* HIP runtime error (see sw_last_error) */
 #define SW_E_NOMEM -3     /* host allocation failed */
 #define SW_E_NODEVICE -4  /* no HIP device / kernel image for this GPU */
+#define SW_E_UNSUPPORTED -5 /* valid request this build does not implement */
+#define SW_E_IO -6          /* file could not be read / written / validated */
 
 #define SW_ALPHABET 25    /* residue codes 0..24 */
 #define SW_CODE_STAR 24
@@ -82,6 +84,7 @@ typedef struct sw_db_stats {
                                 most recent scan of this database (the split
                                 depends on the scoring) */
     int64_t coop_residues;   /* unpadded residues in those blocks */
+    int32_t max_id;          /* largest result id (-1 if empty): score arrays hold max_id+1 */
 } sw_db_stats;
 
 typedef struct sw_timing {
@@ -124,6 +127,16 @@ SW_API int sw_db_create(sw_handle* h, const uint8_t* residues, const int64_t* of
                  int64_t n, const int32_t* ids, sw_db** out);
 SW_API int sw_db_free(sw_db* db);
 SW_API int sw_db_get_stats(const sw_db* db, sw_db_stats* out);
+/* Binary database file (the intent of the reference's
+ * parse.py:40-46): subjects sorted by length (descending, stable) as encoded
+ * codes + int64 offsets + int32 result ids, with an FNV-1a checksum, so a
+ * database is parsed from FASTA once and then loaded in one read.  Loading
+ * gives a database whose scans produce identical scores[id].            */
+SW_API int sw_db_save(const sw_db* db, const char* path);
+SW_API int sw_db_load(sw_handle* h, const char* path, sw_db** out);
+/* Per-subject lengths and result ids in the database's order (the order of
+ * sw_db_create's input, or of the file for sw_db_load); either may be NULL. */
+SW_API int sw_db_subjects(const sw_db* db, int64_t* lengths, int32_t* ids);
 /* Subjects longer than `threshold` go to the intra-sequence kernel (one
  * wave per subject) instead of the inter-sequence kernels (one subject per
  * lane).  0 = library default: 5.7 x the mean length clamped to
@@ -190,6 +203,29 @@ SW_API int sw_topk_device(sw_handle* h, const int32_t* scores_dev, int64_t n, in
                    int32_t k, int64_t* keys_out_dev);
 SW_API int sw_topk_keys_device(sw_handle* h, const int64_t* keys_dev, int64_t n, int32_t k,
                         int64_t* keys_out_dev);
+
+/* ---- alignments of chosen hits (traceback) ------------------------------
+ * The GPU analogue of the cpu.cpp pair program's traceback (cpu.cpp:47-108;
+ * SURVEY.md §8 row f1): for each id in ids[0..n), the best local alignment of
+ * the query against that database subject under cpu.cpp's rules — a cell
+ * takes left, then up, then diagonal only on a strict improvement over 0,
+ * the first strict maximum in row-major order is the end cell, and the walk
+ * back stops at a zero cell.  Linear gap only (gap_open == gap_extend;
+ * otherwise SW_E_UNSUPPORTED).  Positions are 1-based and inclusive; ops
+ * (optional, n x ops_stride bytes, not NUL-terminated) spells the path from
+ * the begin cell: 'M' an aligned pair, 'I' a query residue against a gap,
+ * 'D' a subject residue against a gap; ops_len is the full path length even
+ * when it exceeds ops_stride.  Cost O(|q| x |subject|) per hit: meant for
+ * the top hits of a scan (e.g. the ids from sw_topk).                     */
+typedef struct sw_alignment {
+    int32_t score;
+    int32_t q_begin, q_end;
+    int32_t s_begin, s_end;
+    int32_t ops_len;
+} sw_alignment;
+SW_API int sw_align(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen,
+                    const sw_scoring* sc, const int32_t* ids, int32_t n, sw_alignment* out,
+                    char* ops, int64_t ops_stride);
 
 /* ---- single pair ---------------------------------------------------------
  * One query against one subject on the GPU (wavefront kernel); the GPU

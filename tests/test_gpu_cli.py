@@ -32,3 +32,39 @@ def test_swissprot_harness():
     assert out.returncode == 0, out.stdout + out.stderr
     assert "0 failure(s)" in out.stdout
     assert out.stdout.count("GCUPS") == 17
+
+
+def _pairs(stdout):
+    return [tuple(map(int, ln.split(":"))) for ln in stdout.split("\n") if ln and ln[0].isdigit() and ":" in ln]
+
+
+def test_binary_db_cli_same_output(tmp_path):
+    """--make-db writes the FASTA as a .swdb file; scanning it prints the
+    same id:score lines in the same order, and the same METRICS sizes."""
+    swdb = str(tmp_path / "subset111.swdb")
+    mk = subprocess.run([os.path.join(LIB, "main"), "--make-db", swdb, "--db", GOLDEN + "/subset111.fasta"],
+                        capture_output=True, text=True, timeout=300)
+    assert mk.returncode == 0, mk.stderr
+    runs = []
+    for db in (GOLDEN + "/subset111.fasta", swdb):
+        out = subprocess.run([os.path.join(LIB, "main"), "--query", GOLDEN + "/queries/P01008.fasta", "--db", db],
+                             capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stderr
+        runs.append(out.stdout)
+    assert _pairs(runs[0]) == _pairs(runs[1])
+    for key in ("Num subjects:", "Sum of DB length:", "Query length:"):
+        assert [ln for ln in runs[0].split("\n") if ln.startswith(key)] == \
+               [ln for ln in runs[1].split("\n") if ln.startswith(key)]
+
+
+def test_binary_db_rejects_corruption(tmp_path):
+    swdb = str(tmp_path / "x.swdb")
+    subprocess.run([os.path.join(LIB, "main"), "--make-db", swdb, "--db", GOLDEN + "/subset111.fasta"],
+                   capture_output=True, text=True, timeout=300, check=True)
+    data = bytearray(open(swdb, "rb").read())
+    data[-10] ^= 0x01  # flip one residue bit
+    bad = str(tmp_path / "bad.swdb")
+    open(bad, "wb").write(bytes(data))
+    out = subprocess.run([os.path.join(LIB, "main"), "--query", GOLDEN + "/queries/P01008.fasta", "--db", bad],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0 and "checksum" in out.stderr

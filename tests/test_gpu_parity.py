@@ -276,3 +276,23 @@ def test_batch_all_shipped_queries_c3(sw, oracle, handle):
     for k, q in enumerate(qs):
         want = oracle.scan(q, r, o, mat=m, gap_open=12, gap_extend=1)
         assert np.array_equal(out[k], want), (QUERIES[k], np.nonzero(out[k] != want)[0][:10])
+
+
+def test_db_save_load_roundtrip(sw, oracle, handle, tmp_path):
+    """sw_db_save / sw_db_load: identical scores[id], custom ids kept, bad
+    files rejected."""
+    r, o = sw.synth.database(500, shard=13)
+    ids = np.random.default_rng(2).permutation(700)[:500].astype(np.int32)
+    db = sw.Database(handle, r, o, ids=ids)
+    p = str(tmp_path / "db.swdb")
+    db.save(p)
+    db2 = sw.Database.load(handle, p)
+    assert db2.n == 500 and db2.n_out == int(ids.max()) + 1
+    q = sw.synth.query(300, shard=3)
+    for args in ((), (sw.capi.builtin_matrix(1), 12, 1)):
+        assert np.array_equal(db.scan(q, *args), db2.scan(q, *args))
+    with pytest.raises(sw.capi.SWError):
+        sw.Database.load(handle, str(tmp_path / "missing.swdb"))
+    open(str(tmp_path / "trunc.swdb"), "wb").write(open(p, "rb").read()[:100])
+    with pytest.raises(sw.capi.SWError):
+        sw.Database.load(handle, str(tmp_path / "trunc.swdb"))
