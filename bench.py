@@ -48,9 +48,14 @@ SIMDS, CLOCK_HZ = 1024, 2.4e9   # 256 CUs x 4 SIMDs
 # VALU issue model of each per-wave inter kernel: SIMD cycles per DP cell,
 # from the compiled inner loop's instruction counts (hipcc -S) priced at the
 # measured gfx950 issue costs (profiles/r01_valu_rate_*.txt: v_sub_u32 clamp
-# 2.45, v_max_i32 4.37, v_max3_i32 4.4, v_add_u32_sdwa 4.2, v_pk_* 4.25,
+# 2.45, v_max_i32 4.37, v_max3_i32 4.4, v_add_u32_sdwa 4.2, v_pk_* 4.25
+# (v_pk_maximum3_f16 and v_pk_add_f16 too, profiles/r01_f16_rate.txt),
 # v_or_b32 2.7 cycles per wave64 instruction).
 VALU_MODEL = {
+    # per 2 x 64 cells: 3.875 v_pk_add_f16, 3.375 v_pk_maximum3_f16, 1 v_or_b32
+    "sw_inter_x2s<32,8,affine,fp16>": ((3.875 + 3.375) * 4.25 + 2.7) / 128,
+    # per 2 x 64 cells: 3 v_pk_max_i16, 1 v_pk_sub_u16, 1 v_pk_add_u16, 1 v_or_b32
+    "sw_inter_x2s<32,8,linear>": ((3 + 1 + 1) * 4.25 + 2.7) / 128,
     # per 2 x 64 cells: 4.83 v_pk_max_i16, 2.83 v_pk_sub_u16, 1 v_pk_add_u16, 1 v_or_b32
     "sw_inter_x2s<32,8,affine>": ((4.83 + 2.83 + 1) * 4.25 + 2.7) / 128,
     # per 2 x 64 cells: 3 v_pk_max_i16, 1 v_pk_sub_u16, 1 v_pk_add_u16, 1 v_or_b32
@@ -118,12 +123,17 @@ def cpu_baseline(sw, queries, res, offs, gpu_scores, seconds, threads, scoring):
     def run(sr, so):
         return [sw_oracle.scan(q, sr, so, mat=mat, gap_open=go, gap_extend=ge, nthreads=threads) for q in queries]
 
-    # calibrate on a small sample, then size the real one to ~`seconds`
+    # calibrate on growing samples until one takes >= 0.5 s (thread start-up
+    # dominates tiny samples), then size the real one to ~`seconds`
     m0 = min(n, 200)
-    idx, sr, so = sample(m0)
-    t = time.perf_counter()
-    run(sr, so)
-    dt = max(time.perf_counter() - t, 1e-3)
+    while True:
+        idx, sr, so = sample(m0)
+        t = time.perf_counter()
+        run(sr, so)
+        dt = max(time.perf_counter() - t, 1e-3)
+        if dt >= 0.5 or m0 >= n:
+            break
+        m0 = min(n, m0 * 4)
     m = int(min(n, max(m0, m0 * seconds / dt)))
     idx, sr, so = sample(m)
     t = time.perf_counter()

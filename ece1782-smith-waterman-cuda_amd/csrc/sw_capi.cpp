@@ -214,7 +214,10 @@ struct sw_db {
     int32_t* d_lane_ids = nullptr;
     int32_t* d_bnd_h = nullptr;
     int32_t* d_bnd_f = nullptr;
-    int32_t* d_rescue = nullptr;  // [count, block ids...] for the 16-bit kernel
+    // two rescue lists [count, block ids...] of nblocks + 1 ints each: the
+    // 16-bit kernels' flagged blocks (list A), and the fp16 chain's second
+    // stage's (list B)
+    int32_t* d_rescue = nullptr;
     std::vector<uint32_t> h_blk_groups;  // block widths (16-column groups), widest first
     std::vector<int64_t> h_blk_res;      // unpadded residues per block
     int32_t last_ncoop = 0;              // blocks the last scan gave the coop kernel
@@ -581,6 +584,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     const bool x2 = swk::inter_uses_x2(affine, x2_ok);
     // int32 re-scoring of blocks a 16-bit kernel flags near saturation
     const bool rescue = swk::inter_needs_rescue(affine, x2_ok);
+    const bool f16 = swk::inter_uses_f16(affine, x2_ok);
     const int32_t qpad_rescue = rescue ? static_cast<int32_t>(round_up(qlen, swk::rescue_rows(affine))) : 0;
     // widest blocks first, one cooperative workgroup each (int32, int8-profile paths)
     const int32_t ncoop = (!i16 && !p32 && db->nblocks) ? coop_blocks(db, swk::inter_coop_divisor(affine, x2_ok)) : 0;
@@ -590,7 +594,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                              p32, ri, qpad_intra, &P)))
         return rc;
     if (rescue && db->nblocks && !db->d_rescue) {
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rescue), (db->nblocks + 1) * sizeof(int32_t)));
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rescue), 2 * (db->nblocks + 1) * sizeof(int32_t)));
         db->device_bytes += (db->nblocks + 1) * sizeof(int32_t);
     }
     const bool multi_inter = qpad_inter > R || qpad_rescue > swk::rescue_rows(affine) ||
@@ -635,10 +639,15 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         a.bnd_h = db->d_bnd_h;
         a.bnd_f = db->d_bnd_f;
         a.scores = scores_dev;
+        int32_t* listA = db->d_rescue;                    // [count, ids...]
+        int32_t* listB = db->d_rescue ? db->d_rescue + db->nblocks + 1 : nullptr;
         if (rescue) {
-            a.rescue_count = db->d_rescue;
-            a.rescue_list = db->d_rescue + 1;
-            HIPCHECK(hipMemsetAsync(a.rescue_count, 0, sizeof(int32_t), h->stream));
+            a.rescue_count = listA;
+            a.rescue_list = listA + 1;
+            HIPCHECK(hipMemsetAsync(listA, 0, sizeof(int32_t), h->stream));
+            if (f16) HIPCHECK(hipMemsetAsync(listB, 0, sizeof(int32_t), h->stream));
+            // fp16 exact range: every integer up to 2048; H grows by <= max S per cell
+            a.sat_limit = 2048 - 2 * std::max(max_s, 1);
         }
         if (ncoop) {
             // on its own stream, so the per-wave kernel fills the GPU beside it
@@ -662,14 +671,26 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         HIPCHECK(hipEventRecord(h->ev[7], h->stream));
         ++h->launches;
         if (ncoop) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
+        if (f16) {
+            // fp16 chain, stage 2: the int16 packed kernel re-scores the
+            // blocks the fp16 kernel flagged (scores near 2048) and flags
+            // its own near-32767 ones into list B for the int32 stage
+            swk::InterArgs r = a;
+            r.blk_list = listA + 1;
+            r.blk_count = listA;
+            r.rescue_list = listB + 1;
+            r.rescue_count = listB;
+            HIPCHECK(swk::launch_inter_x2s_list(r, affine, h->stream));
+            ++h->launches;
+        }
         if (rescue) {
             // int32 re-scoring of any block the 16-bit kernel flagged (rare:
             // scores near 32767); the list and its count stay on the device
             swk::InterArgs r = a;
             r.prof = P.dev + P.off8;
             r.qpad = qpad_rescue;
-            r.blk_list = db->d_rescue + 1;
-            r.blk_count = db->d_rescue;
+            r.blk_list = (f16 ? listB : listA) + 1;
+            r.blk_count = f16 ? listB : listA;
             r.rescue_list = nullptr;
             r.rescue_count = nullptr;
             HIPCHECK(swk::launch_inter_rescue(r, affine, h->stream));

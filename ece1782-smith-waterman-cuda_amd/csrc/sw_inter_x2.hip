@@ -310,7 +310,12 @@ __global__ __launch_bounds__(256) void sw_inter_x2(InterArgs a) {
 // low strip on SG pad columns after it.  Same packed cell as sw_inter_x2; the
 // score pair is lo[code(t)][i] | hi[code(t-SG)][i] with the two images holding
 // the two strips' rows.
-template <int R>
+// F16: the images hold the scores as fp16 bit patterns (exact integers).
+__device__ __forceinline__ uint32_t to_f16_bits(uint32_t v16) {
+    return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, static_cast<_Float16>(static_cast<int16_t>(v16))));
+}
+
+template <int R, bool F16 = false>
 __device__ __forceinline__ void stage_x2s(X2Lds<R>& L, const int16_t* __restrict__ prof, int stride, int s0,
                                           int lane) {
     constexpr int RD = x2_row_dwords(R);
@@ -327,8 +332,13 @@ __device__ __forceinline__ void stage_x2s(X2Lds<R>& L, const int16_t* __restrict
         uint32_t o[8];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            o[2 * e] = img ? w[e] << 16 : w[e] & 0xffffu;
-            o[2 * e + 1] = img ? w[e] & 0xffff0000u : w[e] >> 16;
+            uint32_t a0 = w[e] & 0xffffu, a1 = w[e] >> 16;
+            if constexpr (F16) {
+                a0 = to_f16_bits(a0);
+                a1 = to_f16_bits(a1);
+            }
+            o[2 * e] = img ? a0 << 16 : a0;
+            o[2 * e + 1] = img ? a1 << 16 : a1;
         }
         int4* d = reinterpret_cast<int4*>((img ? L.hi : L.lo) + c * RD + 8 * k);
         d[0] = make_int4(o[0], o[1], o[2], o[3]);
@@ -339,40 +349,95 @@ __device__ __forceinline__ void stage_x2s(X2Lds<R>& L, const int16_t* __restrict
 __device__ __forceinline__ uint32_t lo_lo(uint32_t a, uint32_t b) { return (a & 0xffffu) | (b << 16); }
 __device__ __forceinline__ uint32_t hi_hi(uint32_t a, uint32_t b) { return (a >> 16) | (b & 0xffff0000u); }
 
-template <int R, int SG, bool AFFINE>
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+// The packed cell in two number formats.  int16: wrapping add, saturating
+// subtract, v_pk_max_i16.  fp16 (affine only): v_pk_add_f16 and the gfx950
+// three-input v_pk_maximum3_f16, which folds the 0 floor into E and F
+// (E = max3(E - ge, n, 0)) and H's two maxima into one: 7.5 packed ops per
+// cell pair instead of 9.66 (profiles/r01_f16_rate.txt).  fp16 holds every
+// integer up to 2048 exactly.
+template <bool F16>
+struct PkCell;
+
+template <>
+struct PkCell<false> {
+    using V = s2;
+    static __device__ __forceinline__ V from(uint32_t x) { return as_s2(x); }
+    static __device__ __forceinline__ uint32_t bits(V x) { return as_u32(x); }
+};
+
+template <>
+struct PkCell<true> {
+    using V = h2;
+    static __device__ __forceinline__ V from(uint32_t x) { return __builtin_bit_cast(h2, x); }
+    static __device__ __forceinline__ uint32_t bits(V x) { return __builtin_bit_cast(uint32_t, x); }
+};
+
+__device__ __forceinline__ h2 max3h(h2 a, h2 b, h2 c) {
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
+
+template <int R, int SG, bool AFFINE, bool F16>
+__device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>& L, int lane);
+
+// LIST: a rescue stage walking the device-side block list (a separate
+// instantiation, so the list loop costs the scan kernels no registers).
+template <int R, int SG, bool AFFINE, bool F16, bool LIST>
 __global__ __launch_bounds__(256) void sw_inter_x2s(InterArgs a) {
     static_assert(R % 16 == 0 && SG % 4 == 0, "shape");
-    // SG: sub-group width = the lag (columns) between the two strips
-    constexpr int NCH = R / 16;
-    constexpr int STEPS = SG * NCH;
+    static_assert(AFFINE || !F16, "the fp16 cell is affine only");
     __shared__ __attribute__((aligned(16))) X2Lds<R> lds[kWavesPerWG];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     X2Lds<R>& L = lds[wave];
+    if constexpr (LIST) {
+        const int n = __builtin_amdgcn_readfirstlane(*a.blk_count);
+        for (int i = blockIdx.x * kWavesPerWG + wave; i < n; i += gridDim.x * kWavesPerWG)
+            x2s_block<R, SG, AFFINE, F16>(a, __builtin_amdgcn_readfirstlane(a.blk_list[i]), L, lane);
+        return;
+    }
     const int blk = a.blk_first + blockIdx.x * kWavesPerWG + wave;
     if (blk >= a.nblocks) return;  // wave-uniform; waves never synchronise
+    x2s_block<R, SG, AFFINE, F16>(a, blk, L, lane);
+}
+
+template <int R, int SG, bool AFFINE, bool F16>
+__device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>& L, int lane) {
+    // SG: sub-group width = the lag (columns) between the two strips
+    constexpr int NCH = R / 16;
+    constexpr int STEPS = SG * NCH;
+    using P = PkCell<F16>;
+    using V = typename P::V;
     const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
     const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
     const int16_t* prof16 = reinterpret_cast<const int16_t*>(a.prof);
     const u2 go2 = {static_cast<unsigned short>(a.gap_open), static_cast<unsigned short>(a.gap_open)};
     const u2 ge2 = {static_cast<unsigned short>(a.gap_extend), static_cast<unsigned short>(a.gap_extend)};
     uint32_t* bnd = reinterpret_cast<uint32_t*>(a.bnd_h);
-    s2 best = {0, 0};
+    // fp16 gap constants (exact integers; unused by the int16 cell)
+    h2 go_h = {}, ge_h = {}, zero_h = {};
+    if constexpr (F16) {
+        go_h = h2{static_cast<_Float16>(a.gap_open), static_cast<_Float16>(a.gap_open)};
+        ge_h = h2{static_cast<_Float16>(a.gap_extend), static_cast<_Float16>(a.gap_extend)};
+        zero_h = h2{static_cast<_Float16>(0), static_cast<_Float16>(0)};
+    }
+    V best = P::from(0u);
 
     for (int s0 = 0; s0 < a.qpad && ncols > 0; s0 += 2 * R) {
         const bool first = (s0 == 0);
         const bool last = (s0 + 2 * R >= a.qpad);
-        stage_x2s<R>(L, prof16, a.prof_stride, s0, lane);
+        stage_x2s<R, F16>(L, prof16, a.prof_stride, s0, lane);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 
-        s2 H[R];
-        s2 E[AFFINE ? R : 1];
+        V H[R];
+        V E[AFFINE ? R : 1];
 #pragma unroll
-        for (int r = 0; r < R; ++r) H[r] = s2{0, 0};
+        for (int r = 0; r < R; ++r) H[r] = P::from(0u);
 #pragma unroll
-        for (int r = 0; r < (AFFINE ? R : 1); ++r) E[r] = s2{0, 0};
+        for (int r = 0; r < (AFFINE ? R : 1); ++r) E[r] = P::from(0u);
         uint32_t dtop = 0;                 // packed H of row -1 at the previous step
         uint32_t dl_h[SG], dl_f[SG];       // low strip's bottom row, SG steps back
         uint32_t bin[SG], bin_n[SG];       // HBM boundary in (H | F << 16), this / next sub-group
@@ -402,12 +467,12 @@ __global__ __launch_bounds__(256) void sw_inter_x2s(InterArgs a) {
                 load_codes<SG>(rn, a.residues + base + noff, next_lo);
                 if (!first && next_lo) load_pairs<SG>(bin_n, reinterpret_cast<const int32_t*>(bnd) + base + noff);
             }
-            s2 up = {0, 0}, diag = {0, 0}, f = {0, 0};
+            V up = P::from(0u), diag = P::from(0u), f = P::from(0u);
 #pragma unroll
             for (int t = 0; t < STEPS; ++t) {
                 const int jj = t / NCH;
                 const int k = t % NCH;
-                const uint32_t dep = as_u32(k == 0 ? H[R - 1] : H[16 * k - 1]);
+                const uint32_t dep = P::bits(k == 0 ? H[R - 1] : H[16 * k - 1]);
                 if (t + 1 < STEPS) {
                     const int jn = (t + 1) / NCH, kn = (t + 1) % NCH;
                     read_x2<R>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(rc, jn), code_of(rp, jn), kn, dep);
@@ -418,18 +483,27 @@ __global__ __launch_bounds__(256) void sw_inter_x2s(InterArgs a) {
                     // row -1 inputs: low strip from HBM (previous pass), high
                     // strip from the low strip's bottom row 8 steps back
                     const uint32_t u = lo_lo(bin[jj], dl_h[jj]);
-                    up = as_s2(u);
-                    diag = as_s2(dtop);
+                    up = P::from(u);
+                    diag = P::from(dtop);
                     dtop = u;
-                    if constexpr (AFFINE) f = as_s2(lo_lo(bin[jj] >> 16, dl_f[jj]));
+                    if constexpr (AFFINE) f = P::from(lo_lo(bin[jj] >> 16, dl_f[jj]));
                 }
                 const int4(&pl)[4] = PL[t & 1];
                 const int4(&ph)[4] = PH[t & 1];
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const int r = 16 * k + i;
-                    const s2 sc = as_s2(word(pl, i) | word(ph, i));
-                    if constexpr (!AFFINE) {
+                    const V sc = P::from(word(pl, i) | word(ph, i));
+                    if constexpr (F16) {
+                        const h2 h = max3h(E[r], f, diag + sc);
+                        const h2 n = h - go_h;
+                        E[r] = max3h(E[r] - ge_h, n, zero_h);
+                        f = max3h(f - ge_h, n, zero_h);
+                        diag = H[r];
+                        H[r] = h;
+                        up = h;
+                        best = __builtin_elementwise_maximum(best, h);
+                    } else if constexpr (!AFFINE) {
                         const s2 h = usub2(max2(max2(H[r], up), diag + sc), go2);
                         diag = H[r];
                         H[r] = h;
@@ -447,7 +521,7 @@ __global__ __launch_bounds__(256) void sw_inter_x2s(InterArgs a) {
                     }
                 }
                 if (k == NCH - 1) {
-                    const uint32_t oh = as_u32(up), of = AFFINE ? as_u32(f) : 0u;
+                    const uint32_t oh = P::bits(up), of = AFFINE ? P::bits(f) : 0u;
                     dl_h[jj] = oh;
                     if constexpr (AFFINE) dl_f[jj] = of;
                     hb[jj] = AFFINE ? hi_hi(oh, of) : (oh >> 16);
@@ -472,15 +546,21 @@ __global__ __launch_bounds__(256) void sw_inter_x2s(InterArgs a) {
             }
         }
     }
-    const int b = max(static_cast<int>(best.x), static_cast<int>(best.y));
+    int b;
+    if constexpr (F16)
+        b = static_cast<int>(static_cast<float>(__builtin_elementwise_maximum(best.x, best.y)));
+    else
+        b = max(static_cast<int>(best.x), static_cast<int>(best.y));
     const int id = a.lane_ids[static_cast<size_t>(blk) * kLanes + lane];
     if (id >= 0) a.scores[id] = b;
-    // Guarded mode (queries too long for the static int16 bound): H grows by
-    // at most max S per cell, so a lane whose values could have wrapped has
-    // its running maximum in [kSat16, 32767] first (or, after a wrap, stays
-    // flagged); its block is re-scored by the int32 kernel from the list.
+    // Guarded mode: H grows by at most max S per cell, so a lane whose values
+    // could have left the exact range has its running maximum in the guard
+    // band first — int16: [kSat16, 32767] (or wrapped: negative); fp16:
+    // >= a.sat_limit = 2048 - 2 max S, computed exactly — and its block is
+    // re-scored from the list by the next stage (int16 packed, then int32).
     if (a.rescue_list) {
-        const uint64_t m = __builtin_amdgcn_ballot_w64(b >= kSat16 || b < 0);
+        const bool sat = F16 ? (b >= a.sat_limit) : (b >= kSat16 || b < 0);
+        const uint64_t m = __builtin_amdgcn_ballot_w64(sat);
         if (m && lane == 0) a.rescue_list[atomicAdd(a.rescue_count, 1)] = blk;
     }
 }
@@ -488,18 +568,34 @@ __global__ __launch_bounds__(256) void sw_inter_x2s(InterArgs a) {
 template <int R, int SG>
 static hipError_t launch_x2s_shape(const InterArgs& a, bool affine, hipStream_t s) {
     const dim3 grid((a.nblocks - a.blk_first + kWavesPerWG - 1) / kWavesPerWG), block(kWavesPerWG * kLanes);
-    if (affine) hipLaunchKernelGGL((sw_inter_x2s<R, SG, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((sw_inter_x2s<R, SG, false>), grid, block, 0, s, a);
+    if (affine) hipLaunchKernelGGL((sw_inter_x2s<R, SG, true, false, false>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((sw_inter_x2s<R, SG, false, false, false>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_inter_x2s(const InterArgs& a, int R, int SG, bool affine, hipStream_t s) {
+hipError_t launch_inter_x2s(const InterArgs& a, int R, int SG, bool affine, bool f16, hipStream_t s) {
     if (a.nblocks - a.blk_first <= 0 || a.qpad <= 0) return hipSuccess;
+    if (f16) {
+        if (!(affine && R == 32 && SG == 8)) return hipErrorInvalidValue;
+        const dim3 grid((a.nblocks - a.blk_first + kWavesPerWG - 1) / kWavesPerWG), block(kWavesPerWG * kLanes);
+        hipLaunchKernelGGL((sw_inter_x2s<32, 8, true, true, false>), grid, block, 0, s, a);
+        return hipGetLastError();
+    }
     if (R == 32 && SG == 8) return launch_x2s_shape<32, 8>(a, affine, s);
     if (R == 32 && SG == 4) return launch_x2s_shape<32, 4>(a, affine, s);
     if (R == 16 && SG == 8) return launch_x2s_shape<16, 8>(a, affine, s);
     if (R == 48 && SG == 4) return launch_x2s_shape<48, 4>(a, affine, s);
     return hipErrorInvalidValue;
+}
+
+// The int16 packed kernel over a device-side block list (fp16 rescue stage 2):
+// a fixed grid walks the list; an empty list costs one tiny launch.
+hipError_t launch_inter_x2s_list(const InterArgs& a, bool affine, hipStream_t s) {
+    if (a.qpad <= 0) return hipSuccess;
+    const dim3 grid(64), block(kWavesPerWG * kLanes);
+    if (affine) hipLaunchKernelGGL((sw_inter_x2s<32, 8, true, false, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((sw_inter_x2s<48, 4, false, false, true>), grid, block, 0, s, a);
+    return hipGetLastError();
 }
 
 template <int R, int SG>

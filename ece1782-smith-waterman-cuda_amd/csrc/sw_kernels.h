@@ -65,6 +65,8 @@ struct InterArgs {
     // blocks [0, blk_first) are handled by the cooperative kernel; the
     // one-block-per-wave kernels start at blk_first
     int32_t blk_first;
+    // fp16 kernel: a lane whose running maximum reaches this flags its block
+    int32_t sat_limit;
 };
 
 // Long subjects: one wave per subject, query rows spread over the 64 lanes,
@@ -122,7 +124,13 @@ hipError_t launch_inter_x2(const InterArgs& a, int R, int SG, bool affine, hipSt
 // One subject per lane, two R-row query strips per pass in the two int16
 // halves (sw_inter_x2.hip); qpad is a multiple of 2R; boundary rows are
 // (H | F << 16) dwords in bnd_h.
-hipError_t launch_inter_x2s(const InterArgs& a, int R, int SG, bool affine, hipStream_t s);
+hipError_t launch_inter_x2s(const InterArgs& a, int R, int SG, bool affine, bool f16, hipStream_t s);
+// true if the chosen inter kernel computes in fp16 (affine, guarded; its
+// flagged blocks go to the int16 packed kernel in list mode, then int32).
+bool inter_uses_f16(bool affine, int x2_ok);
+// The int16 packed kernel in list mode (blk_list / blk_count set): the
+// second stage of the fp16 rescue chain.
+hipError_t launch_inter_x2s_list(const InterArgs& a, bool affine, hipStream_t s);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.
 constexpr int kSat16 = 32767 - 1152;
 // true if the chosen inter kernel may flag blocks for int32 re-scoring

@@ -762,7 +762,7 @@ __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
 // ---------------------------------------------------------------------------
 // Inter-kernel shape: R query rows per strip x SG columns per software-
 // pipelined sub-group.  SW_INTER_VARIANT="RxSG" overrides (tuning only).
-struct InterShape { int R, SG; bool p32; bool i16; bool pk; bool skew = false; bool x2 = false; bool x2s = false; };
+struct InterShape { int R, SG; bool p32; bool i16; bool pk; bool skew = false; bool x2 = false; bool x2s = false; bool f16 = false; };
 static InterShape inter_shape(bool affine, int x2_ok) {
     // measured on MI355X (scripts/tune_inter.py, profiles/r01_tune_inter.jsonl):
     // 64x8 is fastest for the linear kernel (170 VGPRs, 2 waves/SIMD, half
@@ -780,9 +780,13 @@ static InterShape inter_shape(bool affine, int x2_ok) {
     // x2_ok: 2 = int16 provably exact, 1 = guarded int16 allowed, 0 = int32 only
     const char* ge = std::getenv("SW_INT16_GUARD");
     const bool y_ok = x2_ok == 2 || (x2_ok == 1 && !(ge && ge[0] == '0'));
-    InterShape v = affine ? (y_ok ? InterShape{64, 8, false, false, false, false, false, true}
+    // Affine: the fp16 form of the two-strips kernel (v_pk_maximum3_f16;
+    // 7.1 TCUPS on C2 vs 6.25 int16, profiles/r01_fp16/), always guarded
+    // (rescue chain fp16 -> int16 -> int32).  Linear: int16 y32x8 (3 waves
+    // per SIMD; 10.3 TCUPS).
+    InterShape v = affine ? (y_ok ? InterShape{64, 8, false, false, false, false, false, true, true}
                                   : InterShape{32, 8, false, false, false})
-                          : (y_ok ? InterShape{96, 4, false, false, false, false, false, true}
+                          : (y_ok ? InterShape{64, 8, false, false, false, false, false, true}
                                   : InterShape{64, 8, false, false, false});
     if (const char* e = std::getenv("SW_INTER_VARIANT")) {
         int r = 0, g = 0;
@@ -795,6 +799,8 @@ static InterShape inter_shape(bool affine, int x2_ok) {
         else if (std::sscanf(e, "p%dx%d", &r, &g) == 2 && !affine &&
             ((r == 64 && (g == 8 || g == 4)) || (r == 32 && g == 8) || (r == 48 && g == 8)))
             v = InterShape{r, g, true, false, false};
+        else if (std::sscanf(e, "f%dx%d", &r, &g) == 2 && y_ok && affine && r == 32 && g == 8)
+            v = InterShape{64, 8, false, false, false, false, false, true, true};
         else if (std::sscanf(e, "y%dx%d", &r, &g) == 2 && y_ok &&
                  ((r == 32 && (g == 8 || g == 4)) || (r == 16 && g == 8) || (r == 48 && g == 4)))
             v = InterShape{2 * r, g, false, false, false, false, false, true};  // R = rows per pass
@@ -821,8 +827,12 @@ bool inter_uses_x2(bool affine, int x2_ok) {
 
 bool inter_needs_rescue(bool affine, int x2_ok) {
     const InterShape v = inter_shape(affine, x2_ok);
-    return v.i16 || (v.x2s && x2_ok != 2);
+    return v.i16 || v.f16 || (v.x2s && x2_ok != 2);
 }
+
+bool inter_uses_f16(bool affine, int x2_ok) { return inter_shape(affine, x2_ok).f16; }
+
+
 
 int inter_coop_divisor(bool affine, int x2_ok) {
     // blocks at least residues / divisor columns wide go to the cooperative
@@ -837,7 +847,8 @@ const char* inter_kernel_name(bool affine, int x2_ok) {
     const InterShape v = inter_shape(affine, x2_ok);
     if (v.x2s) {
         static thread_local char b2[64];
-        std::snprintf(b2, sizeof b2, "sw_inter_x2s<%d,%d,%s>", v.R / 2, v.SG, affine ? "affine" : "linear");
+        std::snprintf(b2, sizeof b2, "sw_inter_x2s<%d,%d,%s%s>", v.R / 2, v.SG, affine ? "affine" : "linear",
+                      v.f16 ? ",fp16" : "");
         return b2;
     }
     const char* kind = v.x2 ? "sw_inter_x2" : v.pk ? "sw_inter_pk" : v.i16 ? "sw_inter16" : v.p32 ? "sw_inter_p32"
@@ -884,7 +895,7 @@ hipError_t launch_inter(const InterArgs& a, bool affine, int x2_ok, hipStream_t 
     const dim3 block(kWavesPerWG * kLanes);
     const InterShape v = inter_shape(affine, x2_ok);
     if (v.x2) return launch_inter_x2(a, v.R, v.SG, affine, s);
-    if (v.x2s) return launch_inter_x2s(a, v.R / 2, v.SG, affine, s);
+    if (v.x2s) return launch_inter_x2s(a, v.R / 2, v.SG, affine, v.f16, s);
     if (v.pk) return launch_inter_pk(a, v.R, v.SG, s);
     if (v.i16) return launch_inter16(a, v.R, v.SG, s);
     if (v.p32) {

@@ -132,7 +132,8 @@ def test_long_query_self_hit_int32(sw, oracle, handle):
 
 @pytest.mark.parametrize("mid,go,ge,ww,reps", [(0, 2, 2, 15, 2100), (0, 2, 2, 15, 2190), (0, 2, 2, 15, 2300),
                                               (1, 12, 1, 11, 2870), (1, 12, 1, 11, 2990), (1, 12, 1, 11, 3100)])
-def test_int16_saturation_rescue(sw, oracle, handle, mid, go, ge, ww, reps):
+@pytest.mark.parametrize("variant", ["", "f32x8"])
+def test_int16_saturation_rescue(sw, oracle, handle, monkeypatch, mid, go, ge, ww, reps, variant):
     """Scores at/above the 16-bit kernels' saturation guard are re-scored at
     int32 (block-level rescue), next to ordinary subjects in the same block;
     linear (BLOSUM50, W-W = 15) and affine (BLOSUM62, W-W = 11) scoring."""
@@ -186,7 +187,7 @@ def test_device_topk(sw, handle, n, k):
 
 INTER_VARIANTS = ["32x8", "s32x8", "32x16", "s32x16", "48x8", "s48x8", "64x8", "s64x8", "16x16", "s16x16",
                   "x16x8", "x16x16", "x32x8", "x48x8", "y16x8", "y32x8", "y32x4",
-                  "y48x4"]
+                  "y48x4", "f32x8"]
 
 
 @pytest.mark.parametrize("variant", INTER_VARIANTS)
@@ -245,12 +246,12 @@ def test_default_kernel_selection(sw, handle, monkeypatch):
     db = sw.Database(handle, r, o)
     q = sw.synth.query(375, shard=4)
     db.scan(q, sw.capi.builtin_matrix(1), 12, 1)
-    assert handle.last_kernel() == "sw_inter_x2s<32,8,affine>"
+    assert handle.last_kernel() == "sw_inter_x2s<32,8,affine,fp16>"
     db.scan(q)
-    assert handle.last_kernel() == "sw_inter_x2s<48,4,linear>"
+    assert handle.last_kernel() == "sw_inter_x2s<32,8,linear>"
     # beyond the static int16 bound but inside the guard band: guarded packed
     db.scan(q, sw.capi.builtin_matrix(0), 100, 1)
-    assert handle.last_kernel() == "sw_inter_x2s<32,8,affine>"
+    assert handle.last_kernel() == "sw_inter_x2s<32,8,affine,fp16>"
     # max S + gap open >= 1000: int32
     db.scan(q, sw.capi.builtin_matrix(0), 1000, 1)
     assert handle.last_kernel() == "sw_inter<32,8,affine>"
@@ -296,3 +297,23 @@ def test_db_save_load_roundtrip(sw, oracle, handle, tmp_path):
     open(str(tmp_path / "trunc.swdb"), "wb").write(open(p, "rb").read()[:100])
     with pytest.raises(sw.capi.SWError):
         sw.Database.load(handle, str(tmp_path / "trunc.swdb"))
+
+
+@pytest.mark.parametrize("qlen,selfhit", [(375, True), (900, True), (2400, False)])
+def test_fp16_guard_band(sw, oracle, handle, monkeypatch, qlen, selfhit):
+    """The fp16 kernel is exact below 2048 - 2 max S and flags its block
+    otherwise: subjects scoring around and far above 2048 (planted near-copies
+    of the query) next to ordinary ones, BLOSUM62 11/1, against the oracle."""
+    monkeypatch.setenv("SW_INTER_VARIANT", "f32x8")
+    r, o = sw.synth.database(300, shard=qlen)
+    q = sw.synth.query(qlen, shard=qlen + 5)
+    extra = [q[: qlen // 2], q] if selfhit else [q[:400], q[:190]]
+    r2 = np.concatenate([r] + extra)
+    o2 = np.concatenate([o, o[-1] + np.cumsum([len(x) for x in extra])])
+    db = sw.Database(handle, r2, o2, long_threshold=4000)
+    m = sw.capi.builtin_matrix(1)
+    got = db.scan(q, m, 12, 1)
+    want = oracle.scan(q, r2, o2, mat=m, gap_open=12, gap_extend=1)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    assert handle.last_kernel() == "sw_inter_x2s<32,8,affine,fp16>"
+    assert want.max() > 1000
