@@ -13,10 +13,13 @@ linear gap 2) is timed the same way right after and reported under
 "reference_scoring".
 
 --config c3: the 20 shipped queries (144..5478 aa, sum 41,752) as one batch
-against the same database (configs[2]); --config c5: a 5,000-residue
-synthetic query against 10,000 subjects of N(2000, 200) residues
-(configs[4]).  These are the other BASELINE configurations, measured with
-the same code; the driver's headline is the default (c2).
+against the same database (configs[2]); --config c4: P07327 against a
+50,000,000-subject database split over the ranks (configs[3]; strong
+scaling), each rank's shard generated in its GPU's HBM from (seed, global
+id) by the counter-based generator (sw_db_create_synthetic); --config c5: a
+5,000-residue synthetic query against 10,000 subjects of N(2000, 200)
+residues (configs[4]).  These are the other BASELINE configurations,
+measured with the same code; the driver's headline is the default (c2).
 
 One step = one pass of the hot path over the rank's resident shard: build the
 query profile(s), run the scan kernels (intra-sequence for subjects longer
@@ -68,6 +71,8 @@ VALU_MODEL = {
     "sw_inter<32,8,affine>": (2.82 * 2.45 + 1.83 * 4.37 + 1.5 * 4.4 + 4.2) / 64,
 }
 MATRICES = {"blosum50": 0, "blosum62": 1}
+SEED = 1782
+C4_TOTAL = 50_000_000
 C3_QUERIES = ["P02232", "P05013", "P14942", "P07327", "P01008", "P03435", "P42357", "P21177",
               "Q38941", "P27895", "P07756", "P04775", "P19096", "P28167", "P0C6B8", "P20930",
               "P08519", "Q7TMA5", "P33450", "Q9UKN1"]
@@ -100,24 +105,48 @@ def valu_roofline(kernel, cells_rank, scan_ms, kernel_gcups):
             "kernel_alone_gcups_while_concurrent": round(kernel_gcups, 1)}
 
 
-def cpu_baseline(sw, queries, res, offs, gpu_scores, seconds, threads, scoring):
+def host_sampler(res, offs):
+    """Subjects idx of a host-generated shard as (residues, offsets)."""
+    def take(idx):
+        lens = offs[idx + 1] - offs[idx]
+        so = np.zeros(len(idx) + 1, dtype=np.int64)
+        so[1:] = np.cumsum(lens)
+        sr = np.concatenate([res[offs[i]:offs[i + 1]] for i in idx]) if len(idx) else np.zeros(0, np.uint8)
+        return sr, so
+    return take
+
+
+def counter_sampler(sw, seed, id_base):
+    """Subjects idx of a device-generated shard, regenerated on the CPU by
+    the counter-based restatement (synth.counter_*)."""
+    L, lut = sw.capi.synth_tables()
+
+    def take(idx):
+        gids = id_base + np.asarray(idx, dtype=np.int64)
+        lens = sw.synth.counter_lengths(seed, gids, L)
+        so = np.zeros(len(idx) + 1, dtype=np.int64)
+        so[1:] = np.cumsum(lens)
+        sr = np.concatenate([sw.synth.counter_residues(seed, int(g), int(m), lut) for g, m in zip(gids, lens)]) \
+            if len(idx) else np.zeros(0, np.uint8)
+        return sr, so
+    return take
+
+
+def cpu_baseline(sw, queries, sampler, n, gpu_scores, seconds, threads, scoring):
     """The oracle (C restatement of cpu.cpp's recurrence, Gotoh for affine;
     kind "port") on a bounded random sample of the same shard, every query of
     the workload, on this host's cores, with the same scoring as the GPU run.
-    gpu_scores: [nq][n] scores of the measured run (parity check)."""
+    sampler(idx) -> (residues, offsets) of shard subjects idx; gpu_scores:
+    [nq][n] scores of the measured run (parity check)."""
     mat, go, ge = scoring
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import sw_oracle
-    n = len(offs) - 1
     rng = np.random.default_rng(1782)
     perm = rng.permutation(n)
 
     def sample(m):
         idx = np.sort(perm[:m])
-        lens = offs[idx + 1] - offs[idx]
-        so = np.zeros(m + 1, dtype=np.int64)
-        so[1:] = np.cumsum(lens)
-        sr = np.concatenate([res[offs[i]:offs[i + 1]] for i in idx]) if m else np.zeros(0, np.uint8)
+        sr, so = sampler(idx)
         return idx, sr, so
 
     def run(sr, so):
@@ -155,6 +184,10 @@ def make_workload(sw, args, rank):
         res, offs = sw.synth.database(args.db_seqs, shard=rank)
         return [sw.encode(read_query(args.query))], [args.query], res, offs, \
             "C2: query %s (%d aa) vs synthetic Swiss-Prot-sized db" % (args.query, len(read_query(args.query)))
+    if args.config == "c4":
+        return [sw.encode(read_query(args.query))], [args.query], None, None, \
+            "C4: query %s (%d aa) vs a %d-subject synthetic db generated on the devices" % (
+                args.query, len(read_query(args.query)), C4_TOTAL)
     if args.config == "c3":
         res, offs = sw.synth.database(args.db_seqs, shard=rank)
         qs = [sw.encode(read_query(n)) for n in C3_QUERIES]
@@ -170,11 +203,12 @@ def make_workload(sw, args, rank):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5"],
-                    help="c2 = the headline (BASELINE configs[1]); c3 / c5 = configs[2] / [4]")
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"],
+                    help="c2 = the headline (BASELINE configs[1]); c3 / c4 / c5 = configs[2] / [3] / [4]")
     ap.add_argument("--steps", type=int, default=None, help="default 10 (c2, c5) / 3 (c3)")
     ap.add_argument("--warmup", type=int, default=None, help="default 2 (c2, c5) / 1 (c3)")
-    ap.add_argument("--db-seqs", type=int, default=None, help="subjects per rank (default 570000; c5: 10000)")
+    ap.add_argument("--db-seqs", type=int, default=None,
+                    help="subjects per rank (default 570000; c4: 50M / ranks; c5: 10000)")
     ap.add_argument("--query", default="P07327")
     ap.add_argument("--topk", type=int, default=100)
     ap.add_argument("--matrix", default="blosum62", choices=sorted(MATRICES))
@@ -195,8 +229,9 @@ def main():
         args.steps = 3 if args.config == "c3" else 10
     if args.warmup is None:
         args.warmup = 1 if args.config == "c3" else 2
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if args.db_seqs is None:
-        args.db_seqs = 10000 if args.config == "c5" else 570000
+        args.db_seqs = {"c5": 10000, "c4": -(-C4_TOTAL // world_env)}.get(args.config, 570000)
 
     import torch
     import torch.distributed as dist
@@ -220,11 +255,8 @@ def main():
 
     t0 = time.perf_counter()
     queries, qnames, res, offs, desc = make_workload(sw, args, rank)
-    n = len(offs) - 1
-    residues = int(offs[-1])
     nq = len(queries)
     qtot = sum(len(q) for q in queries)
-    log("rank %d: shard %d subjects, %d residues, generated in %.1fs" % (rank, n, residues, time.perf_counter() - t0))
 
     handle = sw.Handle(gpu)
     # The library launches on a torch stream (not the legacy null stream,
@@ -233,10 +265,22 @@ def main():
     stream = torch.cuda.Stream(dev)
     handle.set_stream(stream.cuda_stream)
     torch.cuda.set_stream(stream)
-    t0 = time.perf_counter()
-    db = sw.Database(handle, res, offs, long_threshold=(args.long_threshold or None))
+    if res is None:  # c4: the shard is generated in this GPU's HBM
+        id_base = rank * args.db_seqs
+        db = sw.Database.synthetic(handle, SEED, args.db_seqs, id_base=id_base,
+                                   long_threshold=(args.long_threshold or None))
+        lens, _ = db.subjects()
+        offs = np.zeros(len(lens) + 1, dtype=np.int64)
+        offs[1:] = np.cumsum(lens)
+        sampler = counter_sampler(sw, SEED, id_base)
+    else:
+        db = sw.Database(handle, res, offs, long_threshold=(args.long_threshold or None))
+        sampler = host_sampler(res, offs)
+    n = len(offs) - 1
+    residues = int(offs[-1])
     st = db.stats()
-    log("rank %d: packed + uploaded in %.1fs: %s" % (rank, time.perf_counter() - t0, st))
+    log("rank %d: shard %d subjects, %d residues, generated + packed + resident in %.1fs: %s"
+        % (rank, n, residues, time.perf_counter() - t0, st))
 
     scores = torch.zeros((nq, n), dtype=torch.int32, device=dev)
     K = min(args.topk, n)
@@ -358,7 +402,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.config == "c4" else "weak",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic",
@@ -394,7 +438,7 @@ def main():
             out["reference_scoring"] = ref
         if gs is not None:
             threads = min(args.cpu_threads, os.cpu_count() or 1)
-            cb, parity = cpu_baseline(sw, queries, res, offs, gs, args.cpu_seconds, threads,
+            cb, parity = cpu_baseline(sw, queries, sampler, n, gs, args.cpu_seconds, threads,
                                       scoring=(mat, args.gap_open, args.gap_extend))
             out["cpu_baseline"] = cb
             out["parity_sample_ok"] = parity

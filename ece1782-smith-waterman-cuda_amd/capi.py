@@ -27,7 +27,8 @@ EXPORTED = (
     "sw_scan", "sw_scan_device", "sw_scan_batch", "sw_scan_batch_device", "sw_get_timing",
     "sw_timing_reset", "sw_timing_total", "sw_last_kernel",
     "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_score_pair", "sw_align",
-    "sw_db_save", "sw_db_load", "sw_db_subjects",
+    "sw_db_save", "sw_db_load", "sw_db_subjects", "sw_db_create_synthetic", "sw_synth_tables",
+    "sw_synth_lengths",
 )
 
 
@@ -110,6 +111,10 @@ def lib():
         "sw_timing_total": (ctypes.c_int, [vp, ctypes.POINTER(Timing), i32p]),
         "sw_last_kernel": (ctypes.c_char_p, [vp]),
         "sw_db_save": (ctypes.c_int, [vp, ctypes.c_char_p]),
+        "sw_db_create_synthetic": (ctypes.c_int, [vp, ctypes.c_uint64, i64, i64, ctypes.POINTER(vp)]),
+        "sw_synth_tables": (ctypes.c_int, [i32p, u8p]),
+        "sw_synth_lengths": (ctypes.c_int, [ctypes.c_uint64, i64, i64, i32p]),
+        "sw_db_subjects": (ctypes.c_int, [vp, i64p, i32p]),
         "sw_db_load": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.POINTER(vp)]),
         "sw_align": (ctypes.c_int, [vp, vp, u8p, i32, ctypes.POINTER(Scoring), i32p, i32,
                                     ctypes.POINTER(Alignment), ctypes.c_char_p, ctypes.c_int64]),
@@ -263,6 +268,32 @@ class Database:
             self.set_long_threshold(long_threshold)
 
     @classmethod
+    def synthetic(cls, handle, seed, n, id_base=0, long_threshold=None):
+        """A synthetic database generated in HBM (sw_db_create_synthetic):
+        subject k (result id k) has global id id_base + k; see synth.counter_*
+        for the CPU restatement."""
+        self = cls.__new__(cls)
+        self.handle = handle
+        d = ctypes.c_void_p()
+        _check(lib().sw_db_create_synthetic(handle.ptr, seed, id_base, n, ctypes.byref(d)))
+        self._d = d
+        self.n = n
+        self.n_out = n
+        handle._dbs.add(self)
+        if long_threshold is not None:
+            self.set_long_threshold(long_threshold)
+        return self
+
+    def subjects(self):
+        """(lengths int64[n], ids int32[n]) in database order (sw_db_subjects)."""
+        n = self.stats()["n_subjects"]
+        L = np.zeros(n, dtype=np.int64)
+        ids = np.zeros(n, dtype=np.int32)
+        _check(lib().sw_db_subjects(self._d, L.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                    ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return L, ids
+
+    @classmethod
     def load(cls, handle, path, long_threshold=None):
         """A database from a sw_db_save file (one read, no FASTA parsing)."""
         self = cls.__new__(cls)
@@ -369,6 +400,22 @@ class Database:
                                    offs.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), len(queries),
                                    sc.ptr(), out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
         return out
+
+
+def synth_tables():
+    """(length quantile table int32[4096], u16 -> residue table uint8[65536])
+    of the library's synthetic databases."""
+    L = np.zeros(4096, dtype=np.int32)
+    lut = np.zeros(65536, dtype=np.uint8)
+    _check(lib().sw_synth_tables(L.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                 lut.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+    return L, lut
+
+
+def synth_lengths(seed, id_base, n):
+    out = np.zeros(n, dtype=np.int32)
+    _check(lib().sw_synth_lengths(seed, id_base, n, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+    return out
 
 
 def topk(scores, k):

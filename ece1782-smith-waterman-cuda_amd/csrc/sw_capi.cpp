@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -238,6 +239,11 @@ struct sw_db {
     std::unordered_map<int32_t, int64_t> id_index;  // result id -> subject (built on first sw_align)
     bool built = false;
     size_t device_bytes = 0;
+    // synthetic database (sw_db_create_synthetic): residues are generated
+    // on the device from (seed, id_base + local id); h_residues stays empty
+    bool synthetic = false;
+    uint64_t seed = 0;
+    int64_t id_base = 0;
 };
 
 namespace {
@@ -288,6 +294,90 @@ int upload(T** dptr, const std::vector<T>& v, hipStream_t s, size_t* acc) {
     return SW_OK;
 }
 
+// ---- synthetic databases -------------------------
+// Swiss-Prot composition (percent), codes 0..19 = A R N D C Q E G H I L K M F
+// P S T W Y V (the same table as synth.py).
+const double kSwissProtFreq[20] = {8.25, 5.53, 4.06, 5.45, 1.37, 3.93, 6.75, 7.07, 2.27, 5.96,
+                                   9.66, 5.84, 2.42, 3.86, 4.70, 6.56, 5.34, 1.08, 2.92, 6.87};
+constexpr uint64_t kLenSalt = 0x4C454E475448ull;  // "LENGTH"
+
+// Acklam's rational approximation of the standard normal quantile.
+double norm_quantile(double p) {
+    static const double a[6] = {-3.969683028665376e+01, 2.209460984245205e+02, -2.759285104469687e+02,
+                                1.383577518672690e+02, -3.066479806614716e+01, 2.506628277459239e+00};
+    static const double b[5] = {-5.447609879822406e+01, 1.615858368580409e+02, -1.556989798598866e+02,
+                                6.680131188771972e+01, -1.328068155288572e+01};
+    static const double c[6] = {-7.784894002430293e-03, -3.223964580411365e-01, -2.400758277161838e+00,
+                                -2.549732539343734e+00, 4.374664141464968e+00, 2.938163982698783e+00};
+    static const double d[4] = {7.784695709041462e-03, 3.224671290700398e-01, 2.445134137142996e+00,
+                                3.754408661907416e+00};
+    const double pl = 0.02425;
+    if (p < pl) {
+        const double q = std::sqrt(-2 * std::log(p));
+        return (((((c[0] * q + c[1]) * q + c[2]) * q + c[3]) * q + c[4]) * q + c[5]) /
+               ((((d[0] * q + d[1]) * q + d[2]) * q + d[3]) * q + 1);
+    }
+    if (p > 1 - pl) {
+        const double q = std::sqrt(-2 * std::log(1 - p));
+        return -(((((c[0] * q + c[1]) * q + c[2]) * q + c[3]) * q + c[4]) * q + c[5]) /
+               ((((d[0] * q + d[1]) * q + d[2]) * q + d[3]) * q + 1);
+    }
+    const double q = p - 0.5, r = q * q;
+    return (((((a[0] * r + a[1]) * r + a[2]) * r + a[3]) * r + a[4]) * r + a[5]) * q /
+           (((((b[0] * r + b[1]) * r + b[2]) * r + b[3]) * r + b[4]) * r + 1);
+}
+
+struct SynthTables {
+    int32_t len[4096];     // log-normal length quantiles: median 290, sigma 0.657, in [5, 35213]
+    uint8_t lut[65536];    // uniform u16 -> residue code
+    SynthTables() {
+        for (int k = 0; k < 4096; ++k) {
+            const double z = norm_quantile((k + 0.5) / 4096.0);
+            const double L = std::nearbyint(std::exp(std::log(290.0) + 0.657 * z));
+            len[k] = static_cast<int32_t>(std::min(35213.0, std::max(5.0, L)));
+        }
+        double sum = 0, acc = 0;
+        for (double f : kSwissProtFreq) sum += f;
+        int64_t edges[20];
+        for (int c = 0; c < 20; ++c) {
+            acc += kSwissProtFreq[c] / sum;
+            edges[c] = static_cast<int64_t>(std::nearbyint(acc * 65536.0));
+        }
+        edges[19] = 65536;
+        int c = 0;
+        for (int v = 0; v < 65536; ++v) {
+            while (c < 19 && edges[c] <= v) ++c;
+            lut[v] = static_cast<uint8_t>(c);
+        }
+    }
+};
+
+const SynthTables& synth_tables() {
+    static const SynthTables t;
+    return t;
+}
+
+int32_t synth_length(uint64_t seed, uint64_t gid) {
+    return synth_tables().len[swk::synth_hash(seed, gid, kLenSalt) >> 52];
+}
+
+void synth_residues(uint64_t seed, uint64_t gid, int64_t L, uint8_t* out) {
+    const uint8_t* lut = synth_tables().lut;
+    for (int64_t j = 0; j < L; j += 4) {
+        const uint64_t h = swk::synth_hash(seed, gid, static_cast<uint64_t>(j >> 2));
+        for (int e = 0; e < 4 && j + e < L; ++e) out[j + e] = lut[(h >> (16 * e)) & 0xffffu];
+    }
+}
+
+// Residues of subject k (host): stored, or regenerated for synthetic dbs.
+void subject_residues(const sw_db* db, int64_t k, uint8_t* out) {
+    const int64_t L = db->h_offsets[k + 1] - db->h_offsets[k];
+    if (db->synthetic)
+        synth_residues(db->seed, static_cast<uint64_t>(db->id_base + db->h_ids[k]), L, out);
+    else
+        std::memcpy(out, db->h_residues.data() + db->h_offsets[k], L);
+}
+
 // Pack: sort by length (descending, stable), route subjects longer than the
 // threshold to the intra kernel, deal the rest into 64-lane blocks of
 // 16-residue groups.  Lanes past a subject's end hold kPadCode.
@@ -312,11 +402,12 @@ int build_db(sw_db* db) {
         lid[k] = db->h_ids[src];
         ltotal += round_up(len(src), 64);
     }
-    std::vector<uint8_t> lres(ltotal, swk::kPadCode);
-    parallel_for(nlong, [&](int64_t k) {
-        const int64_t src = order[k];
-        std::memcpy(lres.data() + loff[k], db->h_residues.data() + db->h_offsets[src], len(src));
-    });
+    std::vector<uint8_t> lres(db->synthetic ? 0 : ltotal, swk::kPadCode);
+    if (!db->synthetic)
+        parallel_for(nlong, [&](int64_t k) {
+            const int64_t src = order[k];
+            std::memcpy(lres.data() + loff[k], db->h_residues.data() + db->h_offsets[src], len(src));
+        });
 
     // ---- inter part
     const int64_t nshort = n - nlong;
@@ -333,16 +424,21 @@ int build_db(sw_db* db) {
         blk_groups[b] = static_cast<uint32_t>(w / swk::kGroupCols);
         total += static_cast<uint64_t>(blk_groups[b]) * swk::kGroupBytes;
     }
-    std::vector<uint8_t> res(total, swk::kPadCode);
+    std::vector<uint8_t> res(db->synthetic ? 0 : total, swk::kPadCode);
+    std::vector<int32_t> lane_len(db->synthetic ? nblocks * swk::kLanes : 0, 0);
     parallel_for(nblocks, [&](int64_t b) {
         for (int l = 0; l < swk::kLanes; ++l) {
             const int64_t k = nlong + b * swk::kLanes + l;
             if (k >= n) break;
             const int64_t src = order[k];
             lane_ids[b * swk::kLanes + l] = db->h_ids[src];
-            const uint8_t* p = db->h_residues.data() + db->h_offsets[src];
             const int64_t L = len(src);
             blk_res[b] += L;
+            if (db->synthetic) {
+                lane_len[b * swk::kLanes + l] = static_cast<int32_t>(L);
+                continue;
+            }
+            const uint8_t* p = db->h_residues.data() + db->h_offsets[src];
             for (int64_t j = 0; j < L; ++j)
                 res[blk_off[b] + (j / swk::kGroupCols) * swk::kGroupBytes + l * swk::kGroupCols +
                     (j % swk::kGroupCols)] = p[j];
@@ -351,14 +447,50 @@ int build_db(sw_db* db) {
 
     size_t acc = 0;
     int rc;
-    if ((rc = upload(&db->d_res, res, s, &acc))) return rc;
+    if (db->synthetic) {
+        // residues generated in HBM from (seed, global id); ids in lane_ids
+        // and lid are local (0..n-1), global = id_base + local
+        if (total) HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_res), total));
+        if (ltotal) HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lres), ltotal));
+        acc += total + ltotal;
+    } else {
+        if ((rc = upload(&db->d_res, res, s, &acc))) return rc;
+    }
     if ((rc = upload(&db->d_blk_off, blk_off, s, &acc))) return rc;
     if ((rc = upload(&db->d_blk_groups, blk_groups, s, &acc))) return rc;
     if ((rc = upload(&db->d_lane_ids, lane_ids, s, &acc))) return rc;
-    if ((rc = upload(&db->d_lres, lres, s, &acc))) return rc;
+    if (!db->synthetic && (rc = upload(&db->d_lres, lres, s, &acc))) return rc;
     if ((rc = upload(&db->d_loff, loff, s, &acc))) return rc;
     if ((rc = upload(&db->d_llen, llen, s, &acc))) return rc;
     if ((rc = upload(&db->d_lid, lid, s, &acc))) return rc;
+    if (db->synthetic) {
+        int32_t* d_lane_len = nullptr;
+        uint8_t* d_lut = nullptr;
+        size_t tmp = 0;
+        if ((rc = upload(&d_lane_len, lane_len, s, &tmp))) return rc;
+        const SynthTables& T = synth_tables();
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&d_lut), sizeof T.lut));
+        HIPCHECK(hipMemcpyAsync(d_lut, T.lut, sizeof T.lut, hipMemcpyHostToDevice, s));
+        swk::SynthFill f{};
+        f.res = db->d_res;
+        f.blk_off = db->d_blk_off;
+        f.blk_groups = db->d_blk_groups;
+        f.lane_local = db->d_lane_ids;
+        f.lane_len = d_lane_len;
+        f.nblocks = nblocks;
+        f.lres = db->d_lres;
+        f.loff = db->d_loff;
+        f.llen = db->d_llen;
+        f.lid = db->d_lid;
+        f.nlong = static_cast<int32_t>(nlong);
+        f.seed = db->seed;
+        f.id_base = db->id_base;
+        f.lut = d_lut;
+        HIPCHECK(swk::launch_synth_fill(f, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        if (d_lane_len) HIPCHECK(hipFree(d_lane_len));
+        HIPCHECK(hipFree(d_lut));
+    }
     HIPCHECK(hipStreamSynchronize(s));  // host vectors go out of scope
     db->h_blk_groups = blk_groups;
     db->h_blk_res = blk_res;
@@ -908,7 +1040,7 @@ int sw_db_save(const sw_db* db, const char* path) {
     std::vector<uint8_t> res(static_cast<size_t>(db->residues));
     for (int64_t k = 0; k < n; ++k) {
         const int64_t src = order[k];
-        std::memcpy(res.data() + offs[k], db->h_residues.data() + db->h_offsets[src], len(src));
+        subject_residues(db, src, res.data() + offs[k]);
         offs[k + 1] = offs[k] + len(src);
         ids[k] = db->h_ids[src];
     }
@@ -967,6 +1099,51 @@ int sw_db_load(sw_handle* h, const char* path, sw_db** out) {
     if (fnv1a(f, res.data(), res.size()) != hd.fnv || offs.back() != hd.residues)
         return fail(SW_E_IO, std::string("database file checksum mismatch: ") + path);
     return sw_db_create(h, res.data(), offs.data(), hd.n, ids.data(), out);
+}
+
+int sw_synth_tables(int32_t* len4096, uint8_t* lut65536) {
+    const SynthTables& T = synth_tables();
+    if (len4096) std::memcpy(len4096, T.len, sizeof T.len);
+    if (lut65536) std::memcpy(lut65536, T.lut, sizeof T.lut);
+    return SW_OK;
+}
+
+int sw_synth_lengths(uint64_t seed, int64_t id_base, int64_t n, int32_t* lengths) {
+    if (n < 0 || (n > 0 && !lengths) || id_base < 0) return fail(SW_E_INVALID, "null argument");
+    parallel_for(n, [&](int64_t k) { lengths[k] = synth_length(seed, static_cast<uint64_t>(id_base + k)); });
+    return SW_OK;
+}
+
+int sw_db_create_synthetic(sw_handle* h, uint64_t seed, int64_t id_base, int64_t n, sw_db** out) {
+    if (!h || !out || n < 0 || id_base < 0 || n > (int64_t(1) << 31) - 1) return fail(SW_E_INVALID, "bad argument");
+    *out = nullptr;
+    auto* db = new (std::nothrow) sw_db();
+    if (!db) return fail(SW_E_NOMEM, "out of host memory");
+    db->h = h;
+    db->n = n;
+    db->synthetic = true;
+    db->seed = seed;
+    db->id_base = id_base;
+    try {
+        std::vector<int32_t> L(n);
+        sw_synth_lengths(seed, id_base, n, L.data());
+        db->h_offsets.assign(n + 1, 0);
+        for (int64_t k = 0; k < n; ++k) db->h_offsets[k + 1] = db->h_offsets[k] + L[k];
+        db->h_ids.resize(n);
+        for (int64_t k = 0; k < n; ++k) db->h_ids[k] = static_cast<int32_t>(k);
+        for (int64_t k = 0; k < n; ++k) db->max_len = std::max(db->max_len, L[k]);
+    } catch (...) {
+        delete db;
+        return fail(SW_E_NOMEM, "out of host memory");
+    }
+    db->residues = db->h_offsets[n];
+    db->max_id = static_cast<int32_t>(n - 1);
+    db->long_threshold = default_long_threshold(db);
+    HIPCHECK(hipSetDevice(h->device));
+    int rc = build_db(db);
+    if (rc) { free_dev(db); delete db; return rc; }
+    *out = db;
+    return SW_OK;
 }
 
 int sw_db_subjects(const sw_db* db, int64_t* lengths, int32_t* ids) {
@@ -1207,7 +1384,7 @@ int sw_align(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen,
         int64_t dacc = 0;
         for (int32_t k = 0; k < m; ++k) {
             const int64_t src = sidx[k0 + k], L = slen_of(src);
-            std::memcpy(hsub.data() + hoff[k], db->h_residues.data() + db->h_offsets[src], L);
+            subject_residues(db, src, hsub.data() + hoff[k]);
             hoff[k + 1] = hoff[k] + L;
             hdoff[k] = dacc;
             dacc += (qlen + L + 1) * W1;

@@ -160,6 +160,26 @@ struct AlignArgs {
 };
 hipError_t launch_align(const AlignArgs& a, hipStream_t s);
 
+// Synthetic databases generated on the device (sw_synth.hip).
+struct SynthFill {
+    uint8_t* res;                // packed inter residues (layout of InterArgs)
+    const uint64_t* blk_off;
+    const uint32_t* blk_groups;
+    const int32_t* lane_local;   // [nblocks][64] local subject id, -1 = empty
+    const int32_t* lane_len;     // [nblocks][64] subject length
+    int64_t nblocks;
+    uint8_t* lres;               // intra residues (IntraArgs layout)
+    const uint64_t* loff;
+    const int32_t* llen;
+    const int32_t* lid;          // local ids
+    int32_t nlong;
+    uint64_t seed;
+    int64_t id_base;             // global id = id_base + local id
+    const uint8_t* lut;          // [65536] uniform u16 -> residue code
+};
+hipError_t launch_synth_fill(const SynthFill& f, hipStream_t s);
+uint64_t synth_hash(uint64_t seed, uint64_t id, uint64_t k);
+
 // Device top-K (sw_topk.hip): keys = score << 32 | (2^31 - 1 - id), best first.
 size_t topk_workspace_bytes(int64_t n, int k);
 hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, int k,

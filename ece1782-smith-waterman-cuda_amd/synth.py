@@ -67,3 +67,45 @@ def fixed_length_database(n, mean, sd, seed=SEED, shard=0, lo=1):
 
 def query(length, seed=SEED, shard=99):
     return residues(length, seed, shard)
+
+
+# ---------------------------------------------------------------------------
+# Counter-based generator: a pure-numpy restatement
+# of the library's on-device generator (sw_db_create_synthetic, sw_synth.hip),
+# so any sampled subject of a device-generated shard can be regenerated on a
+# CPU.  Integer-only; the two tables come from the library (sw_synth_tables).
+# ---------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+LEN_SALT = 0x4C454E475448
+
+
+def _mix(z):
+    """splitmix64's finaliser (arithmetic mod 2^64)."""
+    with np.errstate(over="ignore"):
+        z = np.asarray(z, dtype=np.uint64)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def counter_hash(seed, ids, k):
+    """h(seed, id, k) = mix(seed * G1 + mix(id * G2 + k)) mod 2^64."""
+    with np.errstate(over="ignore"):
+        ids = np.asarray(ids, dtype=np.uint64)
+        k = np.asarray(k, dtype=np.uint64)
+        inner = _mix(ids * np.uint64(0xD6E8FEB86659FD93) + k)
+        return _mix(np.uint64((seed * 0x9E3779B97F4A7C15) & _M64) + inner)
+
+
+def counter_lengths(seed, gids, len_table):
+    h = counter_hash(seed, gids, LEN_SALT)
+    return len_table[(h >> np.uint64(52)).astype(np.int64)]
+
+
+def counter_residues(seed, gid, length, lut):
+    """Residue codes of global subject `gid` (length from counter_lengths)."""
+    words = (length + 3) // 4
+    h = counter_hash(seed, np.full(words, gid, dtype=np.uint64), np.arange(words, dtype=np.uint64))
+    parts = [(h >> np.uint64(16 * e)) & np.uint64(0xFFFF) for e in range(4)]
+    idx = np.stack(parts, axis=1).reshape(-1)[:length].astype(np.int64)
+    return lut[idx]

@@ -134,6 +134,21 @@ SW_API int sw_db_get_stats(const sw_db* db, sw_db_stats* out);
  * gives a database whose scans produce identical scores[id].            */
 SW_API int sw_db_save(const sw_db* db, const char* path);
 SW_API int sw_db_load(sw_handle* h, const char* path, sw_db** out);
+/* Synthetic database generated in HBM: subject
+ * k (k = 0..n-1, result id k) has global id id_base + k; its length is
+ * len4096[h(seed, gid, "LENGTH") >> 52] and residue j is
+ * lut65536[(h(seed, gid, j >> 2) >> 16 (j & 3)) & 0xffff], with
+ * h(seed, id, k) = mix(seed * 0x9E3779B97F4A7C15 + mix(id * 0xD6E8FEB86659FD93
+ * + k)) and mix = splitmix64's finaliser (all mod 2^64).  Lengths are
+ * log-normal (median 290, sigma 0.657, [5, 35213]), residues Swiss-Prot
+ * frequencies.  Only O(n) metadata is computed on the host; the residues
+ * are written by device kernels (no host copy, no PCIe transfer).  Any
+ * subject can be regenerated on a CPU from the two tables (sw_synth_tables)
+ * and the formula above, e.g. to check sampled scores.                  */
+SW_API int sw_db_create_synthetic(sw_handle* h, uint64_t seed, int64_t id_base, int64_t n,
+                                  sw_db** out);
+SW_API int sw_synth_tables(int32_t* len4096, uint8_t* lut65536);
+SW_API int sw_synth_lengths(uint64_t seed, int64_t id_base, int64_t n, int32_t* lengths);
 /* Per-subject lengths and result ids in the database's order (the order of
  * sw_db_create's input, or of the file for sw_db_load); either may be NULL. */
 SW_API int sw_db_subjects(const sw_db* db, int64_t* lengths, int32_t* ids);
