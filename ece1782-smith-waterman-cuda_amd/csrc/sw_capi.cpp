@@ -171,6 +171,7 @@ struct sw_handle {
     hipStream_t side = nullptr;
     hipStream_t side2 = nullptr;  // the cooperative wide-block kernel
     hipEvent_t coop_done = nullptr;
+    hipEvent_t fork2 = nullptr;  // side2 starts after the rescue counters are reset
     // per-query workspace: profiles (inter: [32][stride]; intra: lane-slotted
     // chunks) built in pinned host buffers, copied once per query
     // A ring of profile slots (pinned staging + device copy): building the
@@ -652,6 +653,22 @@ int32_t coop_blocks(const sw_db* db, int divisor) {
     return n;
 }
 
+// Leading (widest) blocks of a two-strips scan handled by wave pairs
+// (sw_inter_x2p): blocks at least `width` columns wide, width =
+// residues / kPairDivisor (SW_PAIR_WIDTH overrides; 0 disables).
+constexpr int64_t kPairDivisor = 200000;
+
+int32_t pair_blocks(const sw_db* db) {
+    int64_t wmin = std::max<int64_t>(256, db->residues / kPairDivisor);
+    if (const char* e = std::getenv("SW_PAIR_WIDTH")) wmin = std::atoll(e);
+    if (wmin <= 0) return 0;
+    int32_t n = 0;
+    while (n < static_cast<int32_t>(db->h_blk_groups.size()) &&
+           static_cast<int64_t>(db->h_blk_groups[n]) * swk::kGroupCols >= wmin)
+        ++n;
+    return n;
+}
+
 int next_events(sw_handle* h) {
     if (h->nscans >= 4096) h->nscans = 0;  // bound the pool; older sums are dropped
     if (h->nscans == h->evpool.size()) {
@@ -719,8 +736,12 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     const bool f16 = swk::inter_uses_f16(affine, x2_ok);
     const int32_t qpad_rescue = rescue ? static_cast<int32_t>(round_up(qlen, swk::rescue_rows(affine))) : 0;
     // widest blocks first, one cooperative workgroup each (int32, int8-profile paths)
-    const int32_t ncoop = (!i16 && !p32 && db->nblocks) ? coop_blocks(db, swk::inter_coop_divisor(affine, x2_ok)) : 0;
-    db->last_ncoop = ncoop;
+    // two-strips scans: the widest blocks by wave pairs (at least two passes)
+    const int32_t npair =
+        (db->nblocks && swk::inter_has_pair(affine, x2_ok) && qpad_inter > R) ? pair_blocks(db) : 0;
+    const int32_t ncoop =
+        (!npair && !i16 && !p32 && db->nblocks) ? coop_blocks(db, swk::inter_coop_divisor(affine, x2_ok)) : 0;
+    db->last_ncoop = ncoop ? ncoop : npair;
     const int32_t qpad_coop = ncoop ? static_cast<int32_t>(round_up(qlen, swk::inter_coop_rows())) : 0;
     if ((rc = build_profiles(h, query, qlen, mat, go, affine, std::max({qpad_inter, qpad_rescue, qpad_coop}), i16 || x2,
                              p32, ri, qpad_intra, &P)))
@@ -793,6 +814,19 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             HIPCHECK(hipEventRecord(h->coop_done, h->side2));
             ++h->launches;
             a.blk_first = ncoop;
+        } else if (npair) {
+            // the widest blocks by wave pairs, beside the per-wave kernel
+            // (after the list counters above are reset: they share listA)
+            swk::InterArgs c = a;
+            c.nblocks = npair;
+            HIPCHECK(hipEventRecord(h->fork2, h->stream));
+            HIPCHECK(hipStreamWaitEvent(h->side2, h->fork2, 0));
+            HIPCHECK(hipEventRecord(h->ev[4], h->side2));
+            HIPCHECK(swk::launch_inter_x2p(c, affine, f16, h->side2));
+            HIPCHECK(hipEventRecord(h->ev[5], h->side2));
+            HIPCHECK(hipEventRecord(h->coop_done, h->side2));
+            ++h->launches;
+            a.blk_first = npair;
         } else {
             HIPCHECK(hipEventRecord(h->ev[4], h->stream));
             HIPCHECK(hipEventRecord(h->ev[5], h->stream));
@@ -802,7 +836,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         h->last_kernel = swk::inter_kernel_name(affine, x2_ok);
         HIPCHECK(hipEventRecord(h->ev[7], h->stream));
         ++h->launches;
-        if (ncoop) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
+        if (ncoop || npair) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
         if (f16) {
             // fp16 chain, stage 2: the int16 packed kernel re-scores the
             // blocks the fp16 kernel flagged (scores near 2048) and flags
@@ -919,6 +953,7 @@ int sw_create(int32_t device, sw_handle** out) {
     for (auto& S : h->prof)
         if (e == hipSuccess) e = hipEventCreateWithFlags(&S.copied, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->coop_done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->fork2, hipEventDisableTiming);
     if (e != hipSuccess) { delete h; return fail(SW_E_HIP, hipGetErrorString(e)); }
     *out = h;
     return SW_OK;
@@ -943,6 +978,7 @@ int sw_destroy(sw_handle* h) {
     if (h->side) (void)hipStreamDestroy(h->side);
     if (h->side2) (void)hipStreamDestroy(h->side2);
     if (h->coop_done) (void)hipEventDestroy(h->coop_done);
+    if (h->fork2) (void)hipEventDestroy(h->fork2);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return SW_OK;

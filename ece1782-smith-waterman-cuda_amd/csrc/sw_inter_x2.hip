@@ -402,15 +402,65 @@ __global__ __launch_bounds__(256) void sw_inter_x2s(InterArgs a) {
     x2s_block<R, SG, AFFINE, F16>(a, blk, L, lane);
 }
 
-template <int R, int SG, bool AFFINE, bool F16>
-__device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>& L, int lane) {
+// Score and guard of one block (lane = subject).
+// Guarded mode: H grows by at most max S per cell, so a lane whose values
+// could have left the exact range has its running maximum in the guard
+// band first — int16: [kSat16, 32767] (or wrapped: negative); fp16:
+// >= a.sat_limit = 2048 - 2 max S, computed exactly — and its block is
+// re-scored from the list by the next stage (int16 packed, then int32).
+template <bool F16>
+__device__ __forceinline__ void x2s_finish(const InterArgs& a, int blk, int lane, typename PkCell<F16>::V best) {
+    int b;
+    if constexpr (F16)
+        b = static_cast<int>(static_cast<float>(__builtin_elementwise_maximum(best.x, best.y)));
+    else
+        b = max(static_cast<int>(best.x), static_cast<int>(best.y));
+    const int id = a.lane_ids[static_cast<size_t>(blk) * kLanes + lane];
+    if (id >= 0) a.scores[id] = b;
+    if (a.rescue_list) {
+        const bool sat = F16 ? (b >= a.sat_limit) : (b >= kSat16 || b < 0);
+        const uint64_t m = __builtin_amdgcn_ballot_w64(sat);
+        if (m && lane == 0) a.rescue_list[atomicAdd(a.rescue_count, 1)] = blk;
+    }
+}
+
+
+// LDS ring between the two waves of a pair (sw_inter_x2p): kRingSlots
+// sub-groups of boundary dwords, lane-contiguous int4s (conflict-free b128).
+constexpr int kRingSlots = 4;
+
+template <int SG>
+__device__ __forceinline__ void ring_store(int4* ring, int slot, int lane, const uint32_t (&v)[SG]) {
+#pragma unroll
+    for (int q = 0; q < SG / 4; ++q)
+        ring[(slot * (SG / 4) + q) * kLanes + lane] = make_int4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+
+template <int SG>
+__device__ __forceinline__ void ring_load(uint32_t (&v)[SG], const int4* ring, int slot, int lane) {
+#pragma unroll
+    for (int q = 0; q < SG / 4; ++q) {
+        const int4 t = ring[(slot * (SG / 4) + q) * kLanes + lane];
+        v[4 * q] = static_cast<uint32_t>(t.x);
+        v[4 * q + 1] = static_cast<uint32_t>(t.y);
+        v[4 * q + 2] = static_cast<uint32_t>(t.z);
+        v[4 * q + 3] = static_cast<uint32_t>(t.w);
+    }
+}
+
+// One pass (rows [s0, s0 + 2R)) of one 64-subject block.  PAIR: the pass
+// is part of a wave pair's pipeline (sw_inter_x2p): the boundary comes from /
+// goes to the partner wave through an LDS ring instead of HBM when in_ring /
+// out_ring, and every sub-group ends with one workgroup barrier (a tick).
+template <int R, int SG, bool AFFINE, bool F16, bool PAIR>
+__device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32_t ncols, uint64_t base, int lane,
+                                         int s0, typename PkCell<F16>::V& best, int4* ring, bool in_ring,
+                                         bool out_ring, int* tick) {
     // SG: sub-group width = the lag (columns) between the two strips
     constexpr int NCH = R / 16;
     constexpr int STEPS = SG * NCH;
     using P = PkCell<F16>;
     using V = typename P::V;
-    const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
-    const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
     const int16_t* prof16 = reinterpret_cast<const int16_t*>(a.prof);
     const u2 go2 = {static_cast<unsigned short>(a.gap_open), static_cast<unsigned short>(a.gap_open)};
     const u2 ge2 = {static_cast<unsigned short>(a.gap_extend), static_cast<unsigned short>(a.gap_extend)};
@@ -422,147 +472,244 @@ __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>&
         ge_h = h2{static_cast<_Float16>(a.gap_extend), static_cast<_Float16>(a.gap_extend)};
         zero_h = h2{static_cast<_Float16>(0), static_cast<_Float16>(0)};
     }
-    V best = P::from(0u);
+    const bool first = (s0 == 0);
+    const bool last = (s0 + 2 * R >= a.qpad);
+    stage_x2s<R, F16>(L, prof16, a.prof_stride, s0, lane);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 
-    for (int s0 = 0; s0 < a.qpad && ncols > 0; s0 += 2 * R) {
-        const bool first = (s0 == 0);
-        const bool last = (s0 + 2 * R >= a.qpad);
-        stage_x2s<R, F16>(L, prof16, a.prof_stride, s0, lane);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    V H[R];
+    V E[AFFINE ? R : 1];
+#pragma unroll
+    for (int r = 0; r < R; ++r) H[r] = P::from(0u);
+#pragma unroll
+    for (int r = 0; r < (AFFINE ? R : 1); ++r) E[r] = P::from(0u);
+    uint32_t dtop = 0;                 // packed H of row -1 at the previous step
+    uint32_t dl_h[SG], dl_f[SG];       // low strip's bottom row, SG steps back
+    uint32_t bin[SG], bin_n[SG];       // HBM boundary in (H | F << 16), this / next sub-group
+    uint32_t hb[SG];                   // HBM boundary out (high strip's bottom row)
+    uint32_t rc[SG / 4], rp[SG / 4], rn[SG / 4];  // codes: current (low), previous (high), next
+#pragma unroll
+    for (int q = 0; q < SG; ++q) {
+        dl_h[q] = 0;
+        dl_f[q] = 0;
+        bin[q] = 0;
+        bin_n[q] = 0;
+    }
+#pragma unroll
+    for (int q = 0; q < SG / 4; ++q) rp[q] = 0x19191919u;  // virtual columns before the subject
+    load_codes<SG>(rc, a.residues + base, true);
+    if (!first) {
+        if (PAIR && in_ring) ring_load<SG>(bin, ring, 0, lane);
+        else load_pairs<SG>(bin, reinterpret_cast<const int32_t*>(bnd) + base);
+    }
+    int4 PL[2][4], PH[2][4];
+    read_x2<R>(PL[0], PH[0], L, code_of(rc, 0), code_of(rp, 0), 0, 0);
 
-        V H[R];
-        V E[AFFINE ? R : 1];
-#pragma unroll
-        for (int r = 0; r < R; ++r) H[r] = P::from(0u);
-#pragma unroll
-        for (int r = 0; r < (AFFINE ? R : 1); ++r) E[r] = P::from(0u);
-        uint32_t dtop = 0;                 // packed H of row -1 at the previous step
-        uint32_t dl_h[SG], dl_f[SG];       // low strip's bottom row, SG steps back
-        uint32_t bin[SG], bin_n[SG];       // HBM boundary in (H | F << 16), this / next sub-group
-        uint32_t hb[SG];                   // HBM boundary out (high strip's bottom row)
-        uint32_t rc[SG / 4], rp[SG / 4], rn[SG / 4];  // codes: current (low), previous (high), next
-#pragma unroll
-        for (int q = 0; q < SG; ++q) {
-            dl_h[q] = 0;
-            dl_f[q] = 0;
-            bin[q] = 0;
-            bin_n[q] = 0;
+    // sub-groups 0 .. ncols/SG: the last one runs the high strip only
+    for (uint32_t col0 = 0; col0 <= ncols; col0 += SG) {
+        const bool has_next = col0 + SG <= ncols;          // another sub-group follows
+        const bool next_lo = col0 + SG < ncols;            // ... with real low-strip columns
+        const uint32_t ncol = col0 + SG;
+        const uint64_t noff = (ncol >> 4) * kGroupBytes + (ncol & 15);
+        if (has_next) {
+            load_codes<SG>(rn, a.residues + base + noff, next_lo);
+            if (!first && next_lo) {
+                if (PAIR && in_ring) ring_load<SG>(bin_n, ring, (ncol / SG) % kRingSlots, lane);
+                else load_pairs<SG>(bin_n, reinterpret_cast<const int32_t*>(bnd) + base + noff);
+            }
         }
+        V up = P::from(0u), diag = P::from(0u), f = P::from(0u);
 #pragma unroll
-        for (int q = 0; q < SG / 4; ++q) rp[q] = 0x19191919u;  // virtual columns before the subject
-        load_codes<SG>(rc, a.residues + base, true);
-        if (!first) load_pairs<SG>(bin, reinterpret_cast<const int32_t*>(bnd) + base);
-        int4 PL[2][4], PH[2][4];
-        read_x2<R>(PL[0], PH[0], L, code_of(rc, 0), code_of(rp, 0), 0, 0);
-
-        // sub-groups 0 .. ncols/SG: the last one runs the high strip only
-        for (uint32_t col0 = 0; col0 <= ncols; col0 += SG) {
-            const bool has_next = col0 + SG <= ncols;          // another sub-group follows
-            const bool next_lo = col0 + SG < ncols;            // ... with real low-strip columns
-            const uint32_t ncol = col0 + SG;
-            const uint64_t noff = (ncol >> 4) * kGroupBytes + (ncol & 15);
-            if (has_next) {
-                load_codes<SG>(rn, a.residues + base + noff, next_lo);
-                if (!first && next_lo) load_pairs<SG>(bin_n, reinterpret_cast<const int32_t*>(bnd) + base + noff);
+        for (int t = 0; t < STEPS; ++t) {
+            const int jj = t / NCH;
+            const int k = t % NCH;
+            const uint32_t dep = P::bits(k == 0 ? H[R - 1] : H[16 * k - 1]);
+            if (t + 1 < STEPS) {
+                const int jn = (t + 1) / NCH, kn = (t + 1) % NCH;
+                read_x2<R>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(rc, jn), code_of(rp, jn), kn, dep);
+            } else if (has_next) {
+                read_x2<R>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(rn, 0), code_of(rc, 0), 0, dep);
             }
-            V up = P::from(0u), diag = P::from(0u), f = P::from(0u);
-#pragma unroll
-            for (int t = 0; t < STEPS; ++t) {
-                const int jj = t / NCH;
-                const int k = t % NCH;
-                const uint32_t dep = P::bits(k == 0 ? H[R - 1] : H[16 * k - 1]);
-                if (t + 1 < STEPS) {
-                    const int jn = (t + 1) / NCH, kn = (t + 1) % NCH;
-                    read_x2<R>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(rc, jn), code_of(rp, jn), kn, dep);
-                } else if (has_next) {
-                    read_x2<R>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(rn, 0), code_of(rc, 0), 0, dep);
-                }
-                if (k == 0) {
-                    // row -1 inputs: low strip from HBM (previous pass), high
-                    // strip from the low strip's bottom row 8 steps back
-                    const uint32_t u = lo_lo(bin[jj], dl_h[jj]);
-                    up = P::from(u);
-                    diag = P::from(dtop);
-                    dtop = u;
-                    if constexpr (AFFINE) f = P::from(lo_lo(bin[jj] >> 16, dl_f[jj]));
-                }
-                const int4(&pl)[4] = PL[t & 1];
-                const int4(&ph)[4] = PH[t & 1];
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int r = 16 * k + i;
-                    const V sc = P::from(word(pl, i) | word(ph, i));
-                    if constexpr (F16) {
-                        const h2 h = max3h(E[r], f, diag + sc);
-                        const h2 n = h - go_h;
-                        E[r] = max3h(E[r] - ge_h, n, zero_h);
-                        f = max3h(f - ge_h, n, zero_h);
-                        diag = H[r];
-                        H[r] = h;
-                        up = h;
-                        best = __builtin_elementwise_maximum(best, h);
-                    } else if constexpr (!AFFINE) {
-                        const s2 h = usub2(max2(max2(H[r], up), diag + sc), go2);
-                        diag = H[r];
-                        H[r] = h;
-                        up = h;
-                        best = max2(best, h);
-                    } else {
-                        const s2 h = max2(max2(E[r], f), diag + sc);
-                        const s2 n = usub2(h, go2);
-                        E[r] = max2(usub2(E[r], ge2), n);
-                        f = max2(usub2(f, ge2), n);
-                        diag = H[r];
-                        H[r] = h;
-                        up = h;
-                        best = max2(best, h);
-                    }
-                }
-                if (k == NCH - 1) {
-                    const uint32_t oh = P::bits(up), of = AFFINE ? P::bits(f) : 0u;
-                    dl_h[jj] = oh;
-                    if constexpr (AFFINE) dl_f[jj] = of;
-                    hb[jj] = AFFINE ? hi_hi(oh, of) : (oh >> 16);
-                }
-                asm volatile("" : "+v"(best));
-                __builtin_amdgcn_sched_barrier(0);
+            if (k == 0) {
+                // row -1 inputs: low strip from HBM (previous pass), high
+                // strip from the low strip's bottom row 8 steps back
+                const uint32_t u = lo_lo(bin[jj], dl_h[jj]);
+                up = P::from(u);
+                diag = P::from(dtop);
+                dtop = u;
+                if constexpr (AFFINE) f = P::from(lo_lo(bin[jj] >> 16, dl_f[jj]));
             }
-            // the high strip just finished columns [col0 - SG, col0)
-            if (!last && col0 >= SG) {
-                const uint32_t pc = col0 - SG;
+            const int4(&pl)[4] = PL[t & 1];
+            const int4(&ph)[4] = PH[t & 1];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int r = 16 * k + i;
+                const V sc = P::from(word(pl, i) | word(ph, i));
+                if constexpr (F16) {
+                    const h2 h = max3h(E[r], f, diag + sc);
+                    const h2 n = h - go_h;
+                    E[r] = max3h(E[r] - ge_h, n, zero_h);
+                    f = max3h(f - ge_h, n, zero_h);
+                    diag = H[r];
+                    H[r] = h;
+                    up = h;
+                    best = __builtin_elementwise_maximum(best, h);
+                } else if constexpr (!AFFINE) {
+                    const s2 h = usub2(max2(max2(H[r], up), diag + sc), go2);
+                    diag = H[r];
+                    H[r] = h;
+                    up = h;
+                    best = max2(best, h);
+                } else {
+                    const s2 h = max2(max2(E[r], f), diag + sc);
+                    const s2 n = usub2(h, go2);
+                    E[r] = max2(usub2(E[r], ge2), n);
+                    f = max2(usub2(f, ge2), n);
+                    diag = H[r];
+                    H[r] = h;
+                    up = h;
+                    best = max2(best, h);
+                }
+            }
+            if (k == NCH - 1) {
+                const uint32_t oh = P::bits(up), of = AFFINE ? P::bits(f) : 0u;
+                dl_h[jj] = oh;
+                if constexpr (AFFINE) dl_f[jj] = of;
+                hb[jj] = AFFINE ? hi_hi(oh, of) : (oh >> 16);
+            }
+            asm volatile("" : "+v"(best));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // the high strip just finished columns [col0 - SG, col0)
+        if (!last && col0 >= SG) {
+            const uint32_t pc = col0 - SG;
+            if (PAIR && out_ring) {
+                ring_store<SG>(ring, (pc / SG) % kRingSlots, lane, hb);
+            } else {
                 const uint64_t poff = (pc >> 4) * kGroupBytes + (pc & 15);
                 store_pairs<SG>(reinterpret_cast<int32_t*>(bnd) + base + poff, hb);
             }
-            if (has_next) {
+        }
+        if (has_next) {
 #pragma unroll
-                for (int q = 0; q < SG / 4; ++q) {
-                    rp[q] = rc[q];
-                    rc[q] = rn[q];
-                }
-#pragma unroll
-                for (int q = 0; q < SG; ++q) bin[q] = (first || !next_lo) ? 0u : bin_n[q];
+            for (int q = 0; q < SG / 4; ++q) {
+                rp[q] = rc[q];
+                rc[q] = rn[q];
             }
+#pragma unroll
+            for (int q = 0; q < SG; ++q) bin[q] = (first || !next_lo) ? 0u : bin_n[q];
+        }
+        if constexpr (PAIR) {
+            __syncthreads();  // one tick of the pair's clock
+            ++*tick;
         }
     }
-    int b;
-    if constexpr (F16)
-        b = static_cast<int>(static_cast<float>(__builtin_elementwise_maximum(best.x, best.y)));
-    else
-        b = max(static_cast<int>(best.x), static_cast<int>(best.y));
-    const int id = a.lane_ids[static_cast<size_t>(blk) * kLanes + lane];
-    if (id >= 0) a.scores[id] = b;
-    // Guarded mode: H grows by at most max S per cell, so a lane whose values
-    // could have left the exact range has its running maximum in the guard
-    // band first — int16: [kSat16, 32767] (or wrapped: negative); fp16:
-    // >= a.sat_limit = 2048 - 2 max S, computed exactly — and its block is
-    // re-scored from the list by the next stage (int16 packed, then int32).
-    if (a.rescue_list) {
-        const bool sat = F16 ? (b >= a.sat_limit) : (b >= kSat16 || b < 0);
-        const uint64_t m = __builtin_amdgcn_ballot_w64(sat);
-        if (m && lane == 0) a.rescue_list[atomicAdd(a.rescue_count, 1)] = blk;
+}
+
+template <int R, int SG, bool AFFINE, bool F16>
+__device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>& L, int lane) {
+    using P = PkCell<F16>;
+    using V = typename P::V;
+    const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
+    const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
+    V best = P::from(0u);
+    for (int s0 = 0; s0 < a.qpad && ncols > 0; s0 += 2 * R)
+        x2s_pass<R, SG, AFFINE, F16, false>(a, L, ncols, base, lane, s0, best, nullptr, false, false, nullptr);
+    x2s_finish<F16>(a, blk, lane, best);
+}
+
+// ---------------------------------------------------------------------------
+// sw_inter_x2p: a wave PAIR per wide block
+// ---------------------------------------------------------------------------
+// The single-wave kernel runs a block's passes one after another, so a wide
+// block's latency is passes x width and the widest blocks (and the last,
+// ragged round of short ones) bound the scan (profiles/r01_tail/).  Here the
+// two waves of a pair split the passes: wave 0 runs passes 0, 2, 4, ..., wave 1
+// passes 1, 3, 5, ..., kPairLag sub-groups behind.  Within a round the
+// boundary (H | F << 16) goes from wave 0 to wave 1 through an LDS ring; from
+// one round to the next (wave 1 -> wave 0) through HBM as in the single-wave
+// kernel.  All four waves of the workgroup (two pairs, two blocks) share one
+// clock: one __syncthreads per sub-group.  Schedule of a block whose pass
+// takes S = width / SG + 1 ticks: round r of wave w starts at tick
+// r * max(S, 2 kPairLag) + kPairLag w, so
+//   * wave 1 reads sub-group g of the ring 2 ticks after wave 0 wrote it and
+//     wave 0 overwrites that slot only 3 ticks after the read (4 slots);
+//   * wave 0 of round r+1 prefetches from HBM what wave 1 of round r stored
+//     at least one tick earlier (period >= 6).
+// Block latency drops from 2P x S to P x S + kPairLag ticks for 2P passes;
+// the extra cost is one barrier per sub-group and the idle lag, so only the
+// widest blocks use it (sw_capi.cpp pair_blocks).
+constexpr int kPairLag = 3;
+
+__device__ __forceinline__ int pair_ticks(uint32_t ncols, int passes, int SG) {
+    if (ncols == 0 || passes <= 0) return 0;
+    const int S = static_cast<int>(ncols) / SG + 1;
+    const int per = max(S, 2 * kPairLag);
+    return ((passes + 1) / 2 - 1) * per + S + (passes > 1 ? kPairLag : 0);
+}
+
+template <int R, int SG, bool AFFINE, bool F16>
+__global__ __launch_bounds__(256) void sw_inter_x2p(InterArgs a) {
+    static_assert(R % 16 == 0 && SG % 4 == 0, "shape");
+    static_assert(AFFINE || !F16, "the fp16 cell is affine only");
+    __shared__ __attribute__((aligned(16))) X2Lds<R> lds[kWavesPerWG];
+    __shared__ int4 ring[kWavesPerWG / 2][kRingSlots * (SG / 4) * kLanes];
+    __shared__ uint32_t part[kWavesPerWG / 2][kLanes];
+    using P = PkCell<F16>;
+    using V = typename P::V;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int pr = wave >> 1, w = wave & 1;
+    const int passes = (a.qpad + 2 * R - 1) / (2 * R);
+    // the workgroup's clock runs to the longer of its two blocks
+    int tmax = 0;
+    for (int q = 0; q < 2; ++q) {
+        const int b = blockIdx.x * 2 + q;
+        if (b < a.nblocks) tmax = max(tmax, pair_ticks(a.blk_groups[b] * kGroupCols, passes, SG));
     }
+    const int blk = blockIdx.x * 2 + pr;
+    V best = P::from(0u);
+    int tick = 0;
+    if (blk < a.nblocks) {
+        const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
+        const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
+        const int per = max(static_cast<int>(ncols) / SG + 1, 2 * kPairLag);
+        for (int p = w; p < passes && ncols > 0; p += 2) {
+            const int start = (p >> 1) * per + kPairLag * w;
+            while (tick < start) {
+                __syncthreads();
+                ++tick;
+            }
+            x2s_pass<R, SG, AFFINE, F16, true>(a, lds[wave], ncols, base, lane, p * 2 * R, best, ring[pr], w == 1,
+                                               w == 0, &tick);
+        }
+    }
+    while (tick < tmax) {
+        __syncthreads();
+        ++tick;
+    }
+    if (blk < a.nblocks && w == 1) part[pr][lane] = P::bits(best);
+    __syncthreads();
+    if (blk < a.nblocks && w == 0) {
+        const V o = P::from(part[pr][lane]);
+        if constexpr (F16) best = __builtin_elementwise_maximum(best, o);
+        else best = max2(best, o);
+        x2s_finish<F16>(a, blk, lane, best);
+    }
+}
+
+// Blocks [0, a.nblocks) by wave pairs (the caller passes the pair count as
+// nblocks); the two-strips 32x8 shapes only.
+hipError_t launch_inter_x2p(const InterArgs& a, bool affine, bool f16, hipStream_t s) {
+    if (a.nblocks <= 0 || a.qpad <= 0) return hipSuccess;
+    const dim3 grid((a.nblocks + 1) / 2), block(kWavesPerWG * kLanes);
+    if (f16 && affine) hipLaunchKernelGGL((sw_inter_x2p<32, 8, true, true>), grid, block, 0, s, a);
+    else if (f16) return hipErrorInvalidValue;
+    else if (affine) hipLaunchKernelGGL((sw_inter_x2p<32, 8, true, false>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((sw_inter_x2p<32, 8, false, false>), grid, block, 0, s, a);
+    return hipGetLastError();
 }
 
 template <int R, int SG>

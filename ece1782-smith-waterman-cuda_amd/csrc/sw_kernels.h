@@ -131,6 +131,11 @@ bool inter_uses_f16(bool affine, int x2_ok);
 // The int16 packed kernel in list mode (blk_list / blk_count set): the
 // second stage of the fp16 rescue chain.
 hipError_t launch_inter_x2s_list(const InterArgs& a, bool affine, hipStream_t s);
+// Wave pairs over the widest blocks [0, nblocks) of a two-strips 32x8 scan
+// (sw_inter_x2p): same results as launch_inter_x2s, half the block latency.
+hipError_t launch_inter_x2p(const InterArgs& a, bool affine, bool f16, hipStream_t s);
+// true if the chosen inter kernel has a wave-pair form (two-strips 32x8).
+bool inter_has_pair(bool affine, int x2_ok);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.
 constexpr int kSat16 = 32767 - 1152;
 // true if the chosen inter kernel may flag blocks for int32 re-scoring

@@ -832,6 +832,11 @@ bool inter_needs_rescue(bool affine, int x2_ok) {
 
 bool inter_uses_f16(bool affine, int x2_ok) { return inter_shape(affine, x2_ok).f16; }
 
+bool inter_has_pair(bool affine, int x2_ok) {
+    const InterShape v = inter_shape(affine, x2_ok);
+    return v.x2s && v.R == 64 && v.SG == 8;
+}
+
 
 
 int inter_coop_divisor(bool affine, int x2_ok) {

@@ -317,3 +317,37 @@ def test_fp16_guard_band(sw, oracle, handle, monkeypatch, qlen, selfhit):
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
     assert handle.last_kernel() == "sw_inter_x2s<32,8,affine,fp16>"
     assert want.max() > 1000
+
+
+@pytest.mark.parametrize("variant", ["f32x8", "y32x8"])
+@pytest.mark.parametrize("width", ["16", "300"])
+def test_wave_pair_kernel(sw, oracle, handle, monkeypatch, variant, width):
+    """sw_inter_x2p (the widest blocks by wave pairs; width 16 = every block):
+    1 to 15 passes (odd and even counts), narrow blocks (the 6-tick period
+    floor), an odd number of pair blocks, linear and affine, and planted
+    near-copies of the query whose blocks the fp16 kernel flags for the
+    rescue chain — all against the oracle."""
+    monkeypatch.setenv("SW_INTER_VARIANT", variant)
+    monkeypatch.setenv("SW_PAIR_WIDTH", width)
+    r, o = sw.synth.database(1000, shard=17)
+    q0 = sw.synth.query(900, shard=3)
+    extra = [q0, q0[:450], q0[100:700]]
+    r2 = np.concatenate([r] + extra)
+    o2 = np.concatenate([o, o[-1] + np.cumsum([len(x) for x in extra])])
+    db = sw.Database(handle, r2, o2, long_threshold=4000)
+    for qlen, mid, go, ge in [(375, 1, 12, 1), (150, 1, 12, 1), (97, 1, 11, 2), (40, 1, 12, 1), (900, 1, 12, 1),
+                              (375, 0, 2, 2), (260, 0, 2, 2)]:
+        q = q0[:qlen]
+        m = sw.capi.builtin_matrix(mid)
+        got = db.scan(q, m, go, ge)
+        want = oracle.scan(q, r2, o2, mat=m, gap_open=go, gap_extend=ge)
+        assert np.array_equal(got, want), (qlen, mid, go, ge, np.nonzero(got != want)[0][:10])
+        k = handle.last_kernel()
+        assert k.startswith("sw_inter_x2s<32,8,"), k
+        pairs = db.stats()["coop_blocks"]
+        if qlen > 64:
+            assert pairs > 0 and (width == "300" or pairs == db.stats()["n_blocks"]), pairs
+        else:
+            assert pairs == 0
+        if qlen == 900:
+            assert want.max() > 2048  # the fp16 guard band is crossed
