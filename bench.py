@@ -70,6 +70,12 @@ VALU_MODEL = {
     # per 64 cells: 2.82 v_sub clamp, 1.83 v_max, 1.5 v_max3, 1 v_add_sdwa
     "sw_inter<32,8,affine>": (2.82 * 2.45 + 1.83 * 4.37 + 1.5 * 4.4 + 4.2) / 64,
 }
+# sw_intra_x2<RI> (two long subjects per wave, packed fp16): per lane-step,
+# RI rows x (4 v_pk_add_f16 + 3.5 v_pk_maximum3_f16 + 1 v_perm_b32) for
+# 2 x 64 cells, plus ~75 cycles of conveyor overhead (3 DPP moves, 5
+# readlanes, 7 moves, compares/selects; hipcc -S of sw_intra_x2.hip)
+for _ri in (4, 8, 12, 16):
+    VALU_MODEL["sw_intra_x2<%d>" % _ri] = (_ri * (7.5 * 4.25 + 4.25) + 75.0) / (128 * _ri)
 MATRICES = {"blosum50": 0, "blosum62": 1}
 SEED = 1782
 C4_TOTAL = 50_000_000
@@ -339,10 +345,10 @@ def main():
             tmax = t.clone()
             dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
-            return float(tmax[0]), float(t[1]), kt, handle.last_kernel()
-        return elapsed, cells_rank, kt, handle.last_kernel()
+            return float(tmax[0]), float(t[1]), kt, (handle.last_kernel(), handle.last_intra_kernel())
+        return elapsed, cells_rank, kt, (handle.last_kernel(), handle.last_intra_kernel())
 
-    elapsed_max, cells_all, kt, kernel = timed_loop()
+    elapsed_max, cells_all, kt, (kernel, intra_kernel) = timed_loop()
     st = db.stats()  # the coop split of the timed scans
     final_keys = (final if world > 1 else top).cpu().numpy()
     top_ids, top_scores = sw.capi.decode_keys(final_keys[0])
@@ -355,7 +361,8 @@ def main():
         r_n = max(r_kt["scans"], 1)
         ref = {"scoring": "BLOSUM50 (SWSolver.cu:54-81), linear gap 2 (the reference's own)",
                "value": round(r_cells * args.steps / r_elapsed / 1e9, 2), "unit": "GCUPS",
-               "ms_per_step": round(r_elapsed * 1e3 / args.steps, 3), "kernel": r_kernel,
+               "ms_per_step": round(r_elapsed * 1e3 / args.steps, 3), "kernel": r_kernel[0],
+               "intra_kernel": r_kernel[1],
                "kernel_ms_per_scan": {"sw_inter": round(r_kt["wave_ms"] / r_n, 4),
                                       "sw_inter_coop": round(r_kt["coop_ms"] / r_n, 4),
                                       "sw_intra": round(r_kt["intra_ms"] / r_n, 4),
@@ -382,14 +389,23 @@ def main():
         n_coop = min(st["coop_blocks"] * 64, n_inter)
         wave_res = inter_res - st["coop_residues"]
         alg_bytes = wave_res + 12 * (n_inter - n_coop)
-        achieved = alg_bytes / (wave_ms * 1e-3) / 1e9 if wave_ms > 0 else 0.0
+        kernel_ms = wave_ms
         wave_gcups = float(qtot) / nq * wave_res / (wave_ms * 1e-3) / 1e9 if wave_ms > 0 else 0.0
+        intra_res = residues - inter_res
+        roof_kernel = kernel
+        if intra_res > inter_res:
+            # long-subject regime (C5): the intra kernel scans most cells
+            roof_kernel = intra_kernel
+            alg_bytes = intra_res + 12 * st["n_long"]
+            kernel_ms = intra_ms
+            wave_gcups = float(qtot) / nq * intra_res / (intra_ms * 1e-3) / 1e9 if intra_ms > 0 else 0.0
+        achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
         traffic = None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             if (args.config == "c2" and tj.get("workload_key") == workload_key(args, qtot)
-                    and tj.get("kernel") == kernel):
+                    and tj.get("kernel") == roof_kernel):
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -429,9 +445,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": traffic,
-                         "kernel": kernel,
-                         "alg_bytes_per_launch": int(alg_bytes), "kernel_ms": round(wave_ms, 4)},
-            "valu_roofline": valu_roofline(kernel, cells_all / world, kt["total_ms"] / nsc * nq, wave_gcups),
+                         "kernel": roof_kernel,
+                         "alg_bytes_per_launch": int(alg_bytes), "kernel_ms": round(kernel_ms, 4)},
+            "valu_roofline": valu_roofline(roof_kernel, cells_all / world, kt["total_ms"] / nsc * nq, wave_gcups),
+            "kernels": {"inter": kernel, "intra": intra_kernel},
             "top_hit": {"id": int(top_ids[0]), "score": int(top_scores[0])},
         }
         if ref is not None:

@@ -25,7 +25,7 @@ EXPORTED = (
     "sw_create", "sw_destroy", "sw_stream", "sw_set_stream",
     "sw_db_create", "sw_db_free", "sw_db_get_stats", "sw_db_set_long_threshold",
     "sw_scan", "sw_scan_device", "sw_scan_batch", "sw_scan_batch_device", "sw_get_timing",
-    "sw_timing_reset", "sw_timing_total", "sw_last_kernel",
+    "sw_timing_reset", "sw_timing_total", "sw_last_kernel", "sw_last_intra_kernel",
     "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_score_pair", "sw_align",
     "sw_db_save", "sw_db_load", "sw_db_subjects", "sw_db_create_synthetic", "sw_synth_tables",
     "sw_synth_lengths",
@@ -110,6 +110,7 @@ def lib():
         "sw_timing_reset": (ctypes.c_int, [vp]),
         "sw_timing_total": (ctypes.c_int, [vp, ctypes.POINTER(Timing), i32p]),
         "sw_last_kernel": (ctypes.c_char_p, [vp]),
+        "sw_last_intra_kernel": (ctypes.c_char_p, [vp]),
         "sw_db_save": (ctypes.c_int, [vp, ctypes.c_char_p]),
         "sw_db_create_synthetic": (ctypes.c_int, [vp, ctypes.c_uint64, i64, i64, ctypes.POINTER(vp)]),
         "sw_synth_tables": (ctypes.c_int, [i32p, u8p]),
@@ -215,6 +216,10 @@ class Handle:
     def last_kernel(self):
         """Per-wave inter kernel of the last scan, e.g. 'sw_inter_x2<16,16,affine>'."""
         return lib().sw_last_kernel(self._h).decode()
+
+    def last_intra_kernel(self):
+        """Long-subject kernel of the last scan, e.g. 'sw_intra_x2<16>'; 'none'."""
+        return lib().sw_last_intra_kernel(self._h).decode()
 
     def timing_total(self):
         """Kernel ms summed over all scans since timing_reset(); waits."""

@@ -193,6 +193,7 @@ struct sw_handle {
     size_t scores_cap = 0;
     int64_t* d_topk_work = nullptr;  // device top-K workspace
     std::string last_kernel = "none";  // per-wave inter kernel of the last scan
+    std::string last_intra = "none";   // long-subject kernel of the last scan
     size_t topk_cap = 0;
     bool timed = false;
     bool had_intra = false;
@@ -220,6 +221,7 @@ struct sw_db {
     // 16-bit kernels' flagged blocks (list A), and the fp16 chain's second
     // stage's (list B)
     int32_t* d_rescue = nullptr;
+    int32_t* d_lrescue = nullptr;        // [count, subjects...] flagged by sw_intra_x2
     std::vector<uint32_t> h_blk_groups;  // block widths (16-column groups), widest first
     std::vector<int64_t> h_blk_res;      // unpadded residues per block
     int32_t last_ncoop = 0;              // blocks the last scan gave the coop kernel
@@ -276,12 +278,14 @@ int32_t default_long_threshold(const sw_db* db) {
 
 void free_dev(sw_db* db) {
     void* ptrs[] = {db->d_res, db->d_blk_off, db->d_blk_groups, db->d_lane_ids, db->d_bnd_h, db->d_bnd_f,
-                    db->d_rescue, db->d_lres, db->d_loff, db->d_llen, db->d_lid, db->d_lbnd_h, db->d_lbnd_f};
+                    db->d_rescue, db->d_lres, db->d_loff, db->d_llen, db->d_lid, db->d_lbnd_h, db->d_lbnd_f,
+                    db->d_lrescue};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     db->d_res = nullptr; db->d_blk_off = nullptr; db->d_blk_groups = nullptr; db->d_lane_ids = nullptr;
     db->d_bnd_h = nullptr; db->d_bnd_f = nullptr; db->d_rescue = nullptr; db->d_lres = nullptr; db->d_loff = nullptr;
     db->d_llen = nullptr; db->d_lid = nullptr; db->d_lbnd_h = nullptr; db->d_lbnd_f = nullptr;
+    db->d_lrescue = nullptr;
     db->device_bytes = 0;
     db->built = false;
 }
@@ -508,7 +512,7 @@ int build_db(sw_db* db) {
 
 // Boundary rows are only needed when the query spans more than one strip;
 // allocate on first need and keep.
-int ensure_bnd(sw_db* db, bool affine) {
+int ensure_bnd(sw_db* db, bool affine, bool intra_f) {
     if (db->res_bytes && !db->d_bnd_h) {
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_bnd_h), db->res_bytes * 4));
         db->device_bytes += db->res_bytes * 4;
@@ -521,7 +525,7 @@ int ensure_bnd(sw_db* db, bool affine) {
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lbnd_h), db->lres_bytes * 4));
         db->device_bytes += db->lres_bytes * 4;
     }
-    if (affine && db->lres_bytes && !db->d_lbnd_f) {
+    if ((affine || intra_f) && db->lres_bytes && !db->d_lbnd_f) {
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lbnd_f), db->lres_bytes * 4));
         db->device_bytes += db->lres_bytes * 4;
     }
@@ -655,8 +659,9 @@ int32_t coop_blocks(const sw_db* db, int divisor) {
 
 // Leading (widest) blocks of a two-strips scan handled by wave pairs
 // (sw_inter_x2p): blocks at least `width` columns wide, width =
-// residues / kPairDivisor (SW_PAIR_WIDTH overrides; 0 disables).
-constexpr int64_t kPairDivisor = 200000;
+// residues / kPairDivisor (512 on C2: best of 16..1536, profiles/r01_pair*/,
+// r01_ix2/; SW_PAIR_WIDTH overrides; 0 disables).
+constexpr int64_t kPairDivisor = 400000;
 
 int32_t pair_blocks(const sw_db* db) {
     int64_t wmin = std::max<int64_t>(256, db->residues / kPairDivisor);
@@ -716,10 +721,18 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     const int32_t qpad_inter = static_cast<int32_t>(round_up(qlen, R));
     const int ri = db->nlong ? swk::intra_rows_for(qlen, db->long_max) : 0;
     const int32_t qpad_intra = ri ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri)) : 0;
+    // Long subjects: two per wave in packed fp16 (sw_intra_x2) when the guard
+    // applies, with the int32 sw_intra re-scoring the subjects it flags
+    // (SW_INTRA_X2=0: int32 only).
+    const char* ix = std::getenv("SW_INTRA_X2");
+    const bool intra_x2 = db->nlong && x2_ok >= 1 && !(ix && ix[0] == '0');
+    const int ri2 = intra_x2 ? swk::intra_x2_rows_for(qlen, db->long_max) : 0;
+    const int32_t qpad_intra2 = ri2 ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri2)) : 0;
     // Empty query: every score is 0 (the reference's kernel leaves maxScore 0).
     if (qlen == 0) {
         db->last_ncoop = 0;
         h->last_kernel = "none";
+        h->last_intra = "none";
         HIPCHECK(hipEventRecord(h->ev[0], h->stream));
         if (db->max_id >= 0)
             HIPCHECK(hipMemsetAsync(scores_dev, 0, static_cast<size_t>(db->max_id + 1) * 4, h->stream));
@@ -735,15 +748,21 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     const bool rescue = swk::inter_needs_rescue(affine, x2_ok);
     const bool f16 = swk::inter_uses_f16(affine, x2_ok);
     const int32_t qpad_rescue = rescue ? static_cast<int32_t>(round_up(qlen, swk::rescue_rows(affine))) : 0;
+    // fp16 chain stage 2 (the int16 two-strips 32x8 kernel): 64-row passes
+    const int32_t qpad_list = f16 ? static_cast<int32_t>(round_up(qlen, 64)) : 0;
     // widest blocks first, one cooperative workgroup each (int32, int8-profile paths)
     // two-strips scans: the widest blocks by wave pairs (at least two passes)
     const int32_t npair =
         (db->nblocks && swk::inter_has_pair(affine, x2_ok) && qpad_inter > R) ? pair_blocks(db) : 0;
+    // pairs and single waves in one launch (default) or two concurrent ones
+    const char* pm = std::getenv("SW_PAIR_MERGED");
+    const bool pair_merged = !(pm && pm[0] == '0');
     const int32_t ncoop =
         (!npair && !i16 && !p32 && db->nblocks) ? coop_blocks(db, swk::inter_coop_divisor(affine, x2_ok)) : 0;
     db->last_ncoop = ncoop ? ncoop : npair;
     const int32_t qpad_coop = ncoop ? static_cast<int32_t>(round_up(qlen, swk::inter_coop_rows())) : 0;
-    if ((rc = build_profiles(h, query, qlen, mat, go, affine, std::max({qpad_inter, qpad_rescue, qpad_coop}), i16 || x2,
+    if ((rc = build_profiles(h, query, qlen, mat, go, affine, std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2}),
+                             i16 || x2 || intra_x2,
                              p32, ri, qpad_intra, &P)))
         return rc;
     if (rescue && db->nblocks && !db->d_rescue) {
@@ -751,12 +770,17 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         db->device_bytes += (db->nblocks + 1) * sizeof(int32_t);
     }
     const bool multi_inter = qpad_inter > R || qpad_rescue > swk::rescue_rows(affine) ||
-                             qpad_coop > swk::inter_coop_rows();
-    const bool multi_intra = ri && qpad_intra > swk::kLanes * ri;
-    if ((multi_inter || multi_intra) && (rc = ensure_bnd(db, affine))) return rc;
+                             qpad_coop > swk::inter_coop_rows() || qpad_list > 64;
+    const bool multi_intra = (ri && qpad_intra > swk::kLanes * ri) || (ri2 && qpad_intra2 > swk::kLanes * ri2);
+    if ((multi_inter || multi_intra) && (rc = ensure_bnd(db, affine, intra_x2))) return rc;
+    if (intra_x2 && !db->d_lrescue) {
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lrescue), (db->nlong + 1) * sizeof(int32_t)));
+        db->device_bytes += (db->nlong + 1) * sizeof(int32_t);
+    }
 
     // fork: the side stream starts when the main stream reaches ev[0]
     HIPCHECK(hipEventRecord(h->ev[0], h->stream));
+    h->last_intra = "none";
     if (db->nlong) {
         HIPCHECK(hipStreamWaitEvent(h->side, h->ev[0], 0));
         swk::IntraArgs ia{};
@@ -772,8 +796,26 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         ia.bnd_h = db->d_lbnd_h;
         ia.bnd_f = db->d_lbnd_f;
         ia.scores = scores_dev;
+        if (intra_x2) {
+            swk::IntraArgs x = ia;
+            x.prof = P.dev + P.off16;
+            x.prof_stride = P.stride;
+            x.bias = affine ? 0 : go;  // the linear profile holds S + gap
+            x.qpad = qpad_intra2;
+            x.sat_limit = 2048 - 2 * std::max(max_s, 1);
+            x.rescue_count = db->d_lrescue;
+            x.rescue_list = db->d_lrescue + 1;
+            HIPCHECK(hipMemsetAsync(db->d_lrescue, 0, sizeof(int32_t), h->side));
+            HIPCHECK(swk::launch_intra_x2(x, ri2, h->side));
+            // int32 re-scoring of the flagged subjects (device-side list)
+            ia.list_count = db->d_lrescue;
+            ia.subj_list = db->d_lrescue + 1;
+            h->launches += 2;
+        }
         HIPCHECK(swk::launch_intra(ia, ri, affine, h->side));
         ++h->launches;
+        h->last_intra = intra_x2 ? "sw_intra_x2<" + std::to_string(ri2) + ">"
+                                 : "sw_intra<" + std::to_string(ri) + (affine ? ",affine>" : ",linear>");
         h->had_intra = true;
     }
     HIPCHECK(hipEventRecord(h->ev[1], db->nlong ? h->side : h->stream));
@@ -814,7 +856,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             HIPCHECK(hipEventRecord(h->coop_done, h->side2));
             ++h->launches;
             a.blk_first = ncoop;
-        } else if (npair) {
+        } else if (npair && !pair_merged) {
             // the widest blocks by wave pairs, beside the per-wave kernel
             // (after the list counters above are reset: they share listA)
             swk::InterArgs c = a;
@@ -822,7 +864,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             HIPCHECK(hipEventRecord(h->fork2, h->stream));
             HIPCHECK(hipStreamWaitEvent(h->side2, h->fork2, 0));
             HIPCHECK(hipEventRecord(h->ev[4], h->side2));
-            HIPCHECK(swk::launch_inter_x2p(c, affine, f16, h->side2));
+            HIPCHECK(swk::launch_inter_x2p(c, affine, f16, false, h->side2));
             HIPCHECK(hipEventRecord(h->ev[5], h->side2));
             HIPCHECK(hipEventRecord(h->coop_done, h->side2));
             ++h->launches;
@@ -832,16 +874,23 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             HIPCHECK(hipEventRecord(h->ev[5], h->stream));
         }
         HIPCHECK(hipEventRecord(h->ev[6], h->stream));
-        HIPCHECK(swk::launch_inter(a, affine, x2_ok, h->stream));
+        if (npair && pair_merged) {
+            // one launch: pairs for blocks [0, npair), one wave per block after
+            a.blk_first = npair;
+            HIPCHECK(swk::launch_inter_x2p(a, affine, f16, true, h->stream));
+        } else {
+            HIPCHECK(swk::launch_inter(a, affine, x2_ok, h->stream));
+        }
         h->last_kernel = swk::inter_kernel_name(affine, x2_ok);
         HIPCHECK(hipEventRecord(h->ev[7], h->stream));
         ++h->launches;
-        if (ncoop || npair) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
+        if (ncoop || (npair && !pair_merged)) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
         if (f16) {
             // fp16 chain, stage 2: the int16 packed kernel re-scores the
             // blocks the fp16 kernel flagged (scores near 2048) and flags
             // its own near-32767 ones into list B for the int32 stage
             swk::InterArgs r = a;
+            r.qpad = qpad_list;
             r.blk_list = listA + 1;
             r.blk_count = listA;
             r.rescue_list = listB + 1;
@@ -1331,6 +1380,7 @@ int sw_get_timing(sw_handle* h, sw_timing* out) {
 }
 
 const char* sw_last_kernel(sw_handle* h) { return h ? h->last_kernel.c_str() : "none"; }
+const char* sw_last_intra_kernel(sw_handle* h) { return h ? h->last_intra.c_str() : "none"; }
 
 int sw_timing_reset(sw_handle* h) {
     if (!h) return fail(SW_E_INVALID, "null argument");

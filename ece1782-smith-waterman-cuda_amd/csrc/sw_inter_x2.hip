@@ -85,16 +85,16 @@ __device__ __forceinline__ void stage_x2(X2Lds<R>& L, const int16_t* __restrict_
 // 16 rows [16k, 16k+16) of one column from both images (code ca for the low
 // half, cb for the high half).  `dep` ties the read to a value computed by
 // the previous step so the compiler cannot hoist every unrolled read.
-template <int R>
-__device__ __forceinline__ void read_x2(int4 (&pl)[4], int4 (&ph)[4], const X2Lds<R>& L, uint32_t ca, uint32_t cb,
+template <int R, int N = 4>
+__device__ __forceinline__ void read_x2(int4 (&pl)[N], int4 (&ph)[N], const X2Lds<R>& L, uint32_t ca, uint32_t cb,
                                         int k, uint32_t dep) {
     constexpr int RD = x2_row_dwords(R);
-    uint32_t oa = ca * (RD * 4) + 64 * k, ob = cb * (RD * 4) + 64 * k;
+    uint32_t oa = ca * (RD * 4) + 16 * N * k, ob = cb * (RD * 4) + 16 * N * k;
     asm volatile("" : "+v"(oa), "+v"(ob) : "v"(dep));
     const int4* a = reinterpret_cast<const int4*>(reinterpret_cast<const uint8_t*>(L.lo) + oa);
     const int4* b = reinterpret_cast<const int4*>(reinterpret_cast<const uint8_t*>(L.hi) + ob);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < N; ++q) {
         pl[q] = a[q];
         ph[q] = b[q];
     }
@@ -378,14 +378,14 @@ __device__ __forceinline__ h2 max3h(h2 a, h2 b, h2 c) {
     return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
 
-template <int R, int SG, bool AFFINE, bool F16>
+template <int R, int SG, bool AFFINE, bool F16, int CR = 16>
 __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>& L, int lane);
 
 // LIST: a rescue stage walking the device-side block list (a separate
 // instantiation, so the list loop costs the scan kernels no registers).
-template <int R, int SG, bool AFFINE, bool F16, bool LIST>
+template <int R, int SG, bool AFFINE, bool F16, bool LIST, int CR = 16>
 __global__ __launch_bounds__(256) void sw_inter_x2s(InterArgs a) {
-    static_assert(R % 16 == 0 && SG % 4 == 0, "shape");
+    static_assert(R % CR == 0 && SG % 4 == 0, "shape");
     static_assert(AFFINE || !F16, "the fp16 cell is affine only");
     __shared__ __attribute__((aligned(16))) X2Lds<R> lds[kWavesPerWG];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -394,12 +394,12 @@ __global__ __launch_bounds__(256) void sw_inter_x2s(InterArgs a) {
     if constexpr (LIST) {
         const int n = __builtin_amdgcn_readfirstlane(*a.blk_count);
         for (int i = blockIdx.x * kWavesPerWG + wave; i < n; i += gridDim.x * kWavesPerWG)
-            x2s_block<R, SG, AFFINE, F16>(a, __builtin_amdgcn_readfirstlane(a.blk_list[i]), L, lane);
+            x2s_block<R, SG, AFFINE, F16, CR>(a, __builtin_amdgcn_readfirstlane(a.blk_list[i]), L, lane);
         return;
     }
     const int blk = a.blk_first + blockIdx.x * kWavesPerWG + wave;
     if (blk >= a.nblocks) return;  // wave-uniform; waves never synchronise
-    x2s_block<R, SG, AFFINE, F16>(a, blk, L, lane);
+    x2s_block<R, SG, AFFINE, F16, CR>(a, blk, L, lane);
 }
 
 // Score and guard of one block (lane = subject).
@@ -452,12 +452,15 @@ __device__ __forceinline__ void ring_load(uint32_t (&v)[SG], const int4* ring, i
 // is part of a wave pair's pipeline (sw_inter_x2p): the boundary comes from /
 // goes to the partner wave through an LDS ring instead of HBM when in_ring /
 // out_ring, and every sub-group ends with one workgroup barrier (a tick).
-template <int R, int SG, bool AFFINE, bool F16, bool PAIR>
+template <int R, int SG, bool AFFINE, bool F16, bool PAIR, int CR = 16>
 __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32_t ncols, uint64_t base, int lane,
                                          int s0, typename PkCell<F16>::V& best, int4* ring, bool in_ring,
                                          bool out_ring, int* tick) {
     // SG: sub-group width = the lag (columns) between the two strips
-    constexpr int NCH = R / 16;
+    // CR: profile rows per LDS chunk (16: 2 x 4 ds_read_b128 in flight; 8
+    // halves the chunk registers)
+    constexpr int CQ = CR / 4;
+    constexpr int NCH = R / CR;
     constexpr int STEPS = SG * NCH;
     using P = PkCell<F16>;
     using V = typename P::V;
@@ -488,7 +491,6 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     uint32_t dtop = 0;                 // packed H of row -1 at the previous step
     uint32_t dl_h[SG], dl_f[SG];       // low strip's bottom row, SG steps back
     uint32_t bin[SG], bin_n[SG];       // HBM boundary in (H | F << 16), this / next sub-group
-    uint32_t hb[SG];                   // HBM boundary out (high strip's bottom row)
     uint32_t rc[SG / 4], rp[SG / 4], rn[SG / 4];  // codes: current (low), previous (high), next
 #pragma unroll
     for (int q = 0; q < SG; ++q) {
@@ -504,8 +506,8 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
         if (PAIR && in_ring) ring_load<SG>(bin, ring, 0, lane);
         else load_pairs<SG>(bin, reinterpret_cast<const int32_t*>(bnd) + base);
     }
-    int4 PL[2][4], PH[2][4];
-    read_x2<R>(PL[0], PH[0], L, code_of(rc, 0), code_of(rp, 0), 0, 0);
+    int4 PL[2][CQ], PH[2][CQ];
+    read_x2<R, CQ>(PL[0], PH[0], L, code_of(rc, 0), code_of(rp, 0), 0, 0);
 
     // sub-groups 0 .. ncols/SG: the last one runs the high strip only
     for (uint32_t col0 = 0; col0 <= ncols; col0 += SG) {
@@ -525,12 +527,12 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
         for (int t = 0; t < STEPS; ++t) {
             const int jj = t / NCH;
             const int k = t % NCH;
-            const uint32_t dep = P::bits(k == 0 ? H[R - 1] : H[16 * k - 1]);
+            const uint32_t dep = P::bits(k == 0 ? H[R - 1] : H[CR * k - 1]);
             if (t + 1 < STEPS) {
                 const int jn = (t + 1) / NCH, kn = (t + 1) % NCH;
-                read_x2<R>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(rc, jn), code_of(rp, jn), kn, dep);
+                read_x2<R, CQ>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(rc, jn), code_of(rp, jn), kn, dep);
             } else if (has_next) {
-                read_x2<R>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(rn, 0), code_of(rc, 0), 0, dep);
+                read_x2<R, CQ>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(rn, 0), code_of(rc, 0), 0, dep);
             }
             if (k == 0) {
                 // row -1 inputs: low strip from HBM (previous pass), high
@@ -541,11 +543,11 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
                 dtop = u;
                 if constexpr (AFFINE) f = P::from(lo_lo(bin[jj] >> 16, dl_f[jj]));
             }
-            const int4(&pl)[4] = PL[t & 1];
-            const int4(&ph)[4] = PH[t & 1];
+            const int4(&pl)[CQ] = PL[t & 1];
+            const int4(&ph)[CQ] = PH[t & 1];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int r = 16 * k + i;
+            for (int i = 0; i < CR; ++i) {
+                const int r = CR * k + i;
                 const V sc = P::from(word(pl, i) | word(ph, i));
                 if constexpr (F16) {
                     const h2 h = max3h(E[r], f, diag + sc);
@@ -577,13 +579,16 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
                 const uint32_t oh = P::bits(up), of = AFFINE ? P::bits(f) : 0u;
                 dl_h[jj] = oh;
                 if constexpr (AFFINE) dl_f[jj] = of;
-                hb[jj] = AFFINE ? hi_hi(oh, of) : (oh >> 16);
             }
             asm volatile("" : "+v"(best));
             __builtin_amdgcn_sched_barrier(0);
         }
         // the high strip just finished columns [col0 - SG, col0)
         if (!last && col0 >= SG) {
+            // boundary out = the high halves of the delay line just written
+            uint32_t hb[SG];
+#pragma unroll
+            for (int q = 0; q < SG; ++q) hb[q] = AFFINE ? hi_hi(dl_h[q], dl_f[q]) : (dl_h[q] >> 16);
             const uint32_t pc = col0 - SG;
             if (PAIR && out_ring) {
                 ring_store<SG>(ring, (pc / SG) % kRingSlots, lane, hb);
@@ -608,7 +613,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     }
 }
 
-template <int R, int SG, bool AFFINE, bool F16>
+template <int R, int SG, bool AFFINE, bool F16, int CR>
 __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>& L, int lane) {
     using P = PkCell<F16>;
     using V = typename P::V;
@@ -616,7 +621,7 @@ __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>&
     const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
     V best = P::from(0u);
     for (int s0 = 0; s0 < a.qpad && ncols > 0; s0 += 2 * R)
-        x2s_pass<R, SG, AFFINE, F16, false>(a, L, ncols, base, lane, s0, best, nullptr, false, false, nullptr);
+        x2s_pass<R, SG, AFFINE, F16, false, CR>(a, L, ncols, base, lane, s0, best, nullptr, false, false, nullptr);
     x2s_finish<F16>(a, blk, lane, best);
 }
 
@@ -650,7 +655,12 @@ __device__ __forceinline__ int pair_ticks(uint32_t ncols, int passes, int SG) {
     return ((passes + 1) / 2 - 1) * per + S + (passes > 1 ? kPairLag : 0);
 }
 
-template <int R, int SG, bool AFFINE, bool F16>
+// MERGED: one launch for the whole scan — workgroups [0, (P+1)/2) run the
+// P = a.blk_first widest blocks by wave pairs, the rest run blocks
+// [P, nblocks) one per wave (x2s_block), so the dispatcher hands out work
+// widest-first across both forms (the LDS of the pair form, 53 KB, still
+// leaves 2 workgroups per CU, the register-bound occupancy of both).
+template <int R, int SG, bool AFFINE, bool F16, bool MERGED>
 __global__ __launch_bounds__(256) void sw_inter_x2p(InterArgs a) {
     static_assert(R % 16 == 0 && SG % 4 == 0, "shape");
     static_assert(AFFINE || !F16, "the fp16 cell is affine only");
@@ -661,18 +671,24 @@ __global__ __launch_bounds__(256) void sw_inter_x2p(InterArgs a) {
     using V = typename P::V;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
+    const int npair = MERGED ? a.blk_first : a.nblocks;  // blocks [0, npair) by pairs
+    if (MERGED && static_cast<int>(blockIdx.x) >= (npair + 1) / 2) {
+        const int blk = npair + (blockIdx.x - (npair + 1) / 2) * kWavesPerWG + wave;
+        if (blk < a.nblocks) x2s_block<R, SG, AFFINE, F16>(a, blk, lds[wave], lane);
+        return;  // workgroup-uniform branch: no barrier below is skipped by part of it
+    }
     const int pr = wave >> 1, w = wave & 1;
     const int passes = (a.qpad + 2 * R - 1) / (2 * R);
     // the workgroup's clock runs to the longer of its two blocks
     int tmax = 0;
     for (int q = 0; q < 2; ++q) {
         const int b = blockIdx.x * 2 + q;
-        if (b < a.nblocks) tmax = max(tmax, pair_ticks(a.blk_groups[b] * kGroupCols, passes, SG));
+        if (b < npair) tmax = max(tmax, pair_ticks(a.blk_groups[b] * kGroupCols, passes, SG));
     }
     const int blk = blockIdx.x * 2 + pr;
     V best = P::from(0u);
     int tick = 0;
-    if (blk < a.nblocks) {
+    if (blk < npair) {
         const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
         const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
         const int per = max(static_cast<int>(ncols) / SG + 1, 2 * kPairLag);
@@ -690,9 +706,9 @@ __global__ __launch_bounds__(256) void sw_inter_x2p(InterArgs a) {
         __syncthreads();
         ++tick;
     }
-    if (blk < a.nblocks && w == 1) part[pr][lane] = P::bits(best);
+    if (blk < npair && w == 1) part[pr][lane] = P::bits(best);
     __syncthreads();
-    if (blk < a.nblocks && w == 0) {
+    if (blk < npair && w == 0) {
         const V o = P::from(part[pr][lane]);
         if constexpr (F16) best = __builtin_elementwise_maximum(best, o);
         else best = max2(best, o);
@@ -700,16 +716,25 @@ __global__ __launch_bounds__(256) void sw_inter_x2p(InterArgs a) {
     }
 }
 
-// Blocks [0, a.nblocks) by wave pairs (the caller passes the pair count as
-// nblocks); the two-strips 32x8 shapes only.
-hipError_t launch_inter_x2p(const InterArgs& a, bool affine, bool f16, hipStream_t s) {
-    if (a.nblocks <= 0 || a.qpad <= 0) return hipSuccess;
-    const dim3 grid((a.nblocks + 1) / 2), block(kWavesPerWG * kLanes);
-    if (f16 && affine) hipLaunchKernelGGL((sw_inter_x2p<32, 8, true, true>), grid, block, 0, s, a);
+// merged = false: blocks [0, a.nblocks) by wave pairs (the caller passes the
+// pair count as nblocks).  merged = true: the whole scan in one launch, blocks
+// [0, a.blk_first) by pairs and [a.blk_first, a.nblocks) one per wave.  The
+// two-strips 32x8 shapes only.
+template <bool M>
+static hipError_t launch_x2p(const InterArgs& a, bool affine, bool f16, hipStream_t s) {
+    const int np = M ? a.blk_first : a.nblocks;
+    const int nwg = (np + 1) / 2 + (M ? (a.nblocks - np + kWavesPerWG - 1) / kWavesPerWG : 0);
+    const dim3 grid(nwg), block(kWavesPerWG * kLanes);
+    if (f16 && affine) hipLaunchKernelGGL((sw_inter_x2p<32, 8, true, true, M>), grid, block, 0, s, a);
     else if (f16) return hipErrorInvalidValue;
-    else if (affine) hipLaunchKernelGGL((sw_inter_x2p<32, 8, true, false>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((sw_inter_x2p<32, 8, false, false>), grid, block, 0, s, a);
+    else if (affine) hipLaunchKernelGGL((sw_inter_x2p<32, 8, true, false, M>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((sw_inter_x2p<32, 8, false, false, M>), grid, block, 0, s, a);
     return hipGetLastError();
+}
+
+hipError_t launch_inter_x2p(const InterArgs& a, bool affine, bool f16, bool merged, hipStream_t s) {
+    if (a.nblocks <= 0 || a.qpad <= 0) return hipSuccess;
+    return merged ? launch_x2p<true>(a, affine, f16, s) : launch_x2p<false>(a, affine, f16, s);
 }
 
 template <int R, int SG>
@@ -723,9 +748,12 @@ static hipError_t launch_x2s_shape(const InterArgs& a, bool affine, hipStream_t 
 hipError_t launch_inter_x2s(const InterArgs& a, int R, int SG, bool affine, bool f16, hipStream_t s) {
     if (a.nblocks - a.blk_first <= 0 || a.qpad <= 0) return hipSuccess;
     if (f16) {
-        if (!(affine && R == 32 && SG == 8)) return hipErrorInvalidValue;
+        if (!(affine && ((R == 32 && (SG == 8 || SG == 4)) || (R == 24 && SG == 4))))
+            return hipErrorInvalidValue;
         const dim3 grid((a.nblocks - a.blk_first + kWavesPerWG - 1) / kWavesPerWG), block(kWavesPerWG * kLanes);
-        hipLaunchKernelGGL((sw_inter_x2s<32, 8, true, true, false>), grid, block, 0, s, a);
+        if (R == 32 && SG == 8) hipLaunchKernelGGL((sw_inter_x2s<32, 8, true, true, false>), grid, block, 0, s, a);
+        else if (R == 24) hipLaunchKernelGGL((sw_inter_x2s<24, 4, true, true, false, 8>), grid, block, 0, s, a);
+        else if (R == 32) hipLaunchKernelGGL((sw_inter_x2s<32, 4, true, true, false, 8>), grid, block, 0, s, a);
         return hipGetLastError();
     }
     if (R == 32 && SG == 8) return launch_x2s_shape<32, 8>(a, affine, s);

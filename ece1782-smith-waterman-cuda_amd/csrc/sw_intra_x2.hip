@@ -1,0 +1,238 @@
+// sw_intra_x2.hip — intra-sequence wavefront, TWO subjects per wave, packed
+// fp16 cell (the long-subject path; config C5).
+//
+// The anti-diagonal wavefront of sw_intra (sw_kernels.hip): lane t owns query
+// rows [c0 + t·RI, c0 + (t+1)·RI) of a 64·RI-row chunk and handles column
+// k − t at step k; the bottom row (H, F) and the residue codes move one lane
+// per step with DPP wave_shr:1, lane 0 is fed from the previous chunk pass's
+// boundary row, lane 63's output is collected for the next pass.  Here every
+// value is a PAIR: the low fp16 half belongs to subject 2p, the high half to
+// subject 2p+1 (adjacent in the length-sorted order, so their lengths are
+// close; the shorter one runs pad columns, score 0, to the longer one's end).
+// The cell is the two-strips kernel's (sw_inter_x2.hip) Farrar form on
+// v_pk_add_f16 / v_pk_maximum3_f16, so linear gaps run it with open = extend:
+//   h = max3(E, F, H_diag + S);  n = h − go;
+//   E = max3(E − ge, n, 0);      F = max3(F − ge, n, 0)
+// and the substitution pair is one v_perm_b32 of the two subjects' profile
+// words.  The four waves of a workgroup share one fp16 image of the chunk's
+// profile in LDS, [code][4-row quarter][lane][4 halves]: a lane's quarter is
+// 8 bytes at lane·8 within a 512-byte row, so a ds_read_b64 is bank-conflict
+// free whatever code each lane reads.  The waves stage each chunk together
+// and meet at one barrier per chunk (their subjects have near-equal lengths).
+//
+// Exactness: fp16 holds every integer up to 2048.  H grows by at most max S
+// per cell, so a subject whose running maximum reaches a.sat_limit =
+// 2048 − 2·max S (computed exactly) is appended to a.rescue_list and re-scored
+// by the int32 sw_intra in list mode (sw_capi.cpp).
+#include "sw_kernels.h"
+
+namespace swk {
+
+namespace {
+
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ h2 as_h2(uint32_t x) { return __builtin_bit_cast(h2, x); }
+__device__ __forceinline__ uint32_t h2_bits(h2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ h2 hmax3(h2 a, h2 b, h2 c) {
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
+__device__ __forceinline__ uint32_t f16_bits(int v) {
+    return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, static_cast<_Float16>(v)));
+}
+
+// DPP wave_shr:1 (lane t gets lane t-1's value; lane 0 keeps `old`)
+__device__ __forceinline__ uint32_t shr1u(uint32_t old, uint32_t src) {
+    return static_cast<uint32_t>(
+        __builtin_amdgcn_update_dpp(static_cast<int>(old), static_cast<int>(src), 0x138, 0xf, 0xf, false));
+}
+
+constexpr int kCodes = kPadCode + 1;  // residue codes 0..24 and the pad code
+
+}  // namespace
+
+template <int RI>
+__global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
+    static_assert(RI % 4 == 0 && RI <= 16, "rows per lane");
+    constexpr int CH = kLanes * RI;  // query rows per chunk
+    constexpr int NQ = RI / 4;       // 4-row quarters per lane
+    __shared__ int2 img[kCodes * NQ * kLanes];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int p = blockIdx.x * kWavesPerWG + wave;  // subject pair
+    const int sa = 2 * p, sb = 2 * p + 1;
+    const bool hasA = sa < a.nsubj, hasB = sb < a.nsubj;
+    const int LA = hasA ? a.subj_len[sa] : 0;
+    const int LB = hasB ? a.subj_len[sb] : 0;
+    const int L = max(LA, LB);  // = LA (length-sorted), kept general
+    const uint64_t offA = hasA ? a.subj_off[sa] : 0;
+    const uint8_t* __restrict__ resA = a.residues + offA;
+    const uint8_t* __restrict__ resB = a.residues + (hasB ? a.subj_off[sb] : 0);
+    // the pair's boundary rows live in the longer subject's slots
+    uint32_t* bnd_h = reinterpret_cast<uint32_t*>(a.bnd_h) + (LA >= LB ? offA : (hasB ? a.subj_off[sb] : 0));
+    uint32_t* bnd_f = reinterpret_cast<uint32_t*>(a.bnd_f) + (LA >= LB ? offA : (hasB ? a.subj_off[sb] : 0));
+    const int16_t* prof16 = reinterpret_cast<const int16_t*>(a.prof);
+    const h2 go = {static_cast<_Float16>(a.gap_open), static_cast<_Float16>(a.gap_open)};
+    const h2 ge = {static_cast<_Float16>(a.gap_extend), static_cast<_Float16>(a.gap_extend)};
+    const h2 zero = {static_cast<_Float16>(0), static_cast<_Float16>(0)};
+    h2 best = zero;
+    constexpr uint32_t kPadPair = kPadCode | (kPadCode << 8);
+
+    for (int c0 = 0; c0 < a.qpad; c0 += CH) {
+        const bool first = (c0 == 0);
+        const bool last = (c0 + CH >= a.qpad);
+        __syncthreads();  // the previous chunk's LDS reads are done
+        // stage rows [c0, c0 + CH) of codes 0..25 as fp16 (raw S: the linear
+        // profile is biased by the gap, a.bias)
+        for (int t = threadIdx.x; t < kCodes * NQ * kLanes; t += kWavesPerWG * kLanes) {
+            const int code = t / (NQ * kLanes);
+            const int u = t % (NQ * kLanes);
+            const int qq = u / kLanes, ln = u % kLanes;
+            const int2 v = *reinterpret_cast<const int2*>(prof16 + static_cast<size_t>(code) * a.prof_stride + c0 +
+                                                          ln * RI + 4 * qq);
+            const uint32_t w0 = static_cast<uint32_t>(v.x), w1 = static_cast<uint32_t>(v.y);
+            const int b = a.bias;
+            const uint32_t o0 = f16_bits(static_cast<int16_t>(w0 & 0xffffu) - b) |
+                                (f16_bits(static_cast<int16_t>(w0 >> 16) - b) << 16);
+            const uint32_t o1 = f16_bits(static_cast<int16_t>(w1 & 0xffffu) - b) |
+                                (f16_bits(static_cast<int16_t>(w1 >> 16) - b) << 16);
+            img[t] = make_int2(static_cast<int>(o0), static_cast<int>(o1));
+        }
+        __syncthreads();
+        if (!hasA && !hasB) continue;  // wave-uniform; the barriers above are shared
+
+        h2 H[RI], E[RI];
+#pragma unroll
+        for (int r = 0; r < RI; ++r) {
+            H[r] = zero;
+            E[r] = zero;
+        }
+        uint32_t hl = 0, fl = 0;       // this lane's bottom row (H, F-next) at its last column
+        uint32_t up_prev = 0;          // H of the row above at column j-1 (diag of row 0)
+        uint32_t rc = kPadPair;        // codes (A | B << 8) of this lane's current column
+        uint32_t in_res = kPadPair, in_bh = 0, in_bf = 0, out_h = 0, out_f = 0;
+        const int nsteps = L + kLanes - 1;
+        const int2* lrow = img + lane;
+
+        for (int k0 = 0; k0 < nsteps; k0 += kLanes) {
+            // lane-0 conveyors for steps k0 .. k0+63 (column k = step)
+            {
+                const int col = k0 + lane;
+                const uint32_t ca = col < LA ? resA[col] : kPadCode;
+                const uint32_t cb = col < LB ? resB[col] : kPadCode;
+                in_res = ca | (cb << 8);
+                in_bh = (!first && col < L) ? bnd_h[col] : 0u;
+                in_bf = (!first && col < L) ? bnd_f[col] : 0u;
+            }
+            const int mend = min(kLanes, nsteps - k0);
+            for (int m = 0; m < mend; ++m) {
+                const uint32_t sres = __builtin_amdgcn_readlane(in_res, m);
+                const uint32_t sbh = __builtin_amdgcn_readlane(in_bh, m);
+                const uint32_t sbf = __builtin_amdgcn_readlane(in_bf, m);
+                rc = shr1u(sres, rc);
+                const uint32_t up0 = shr1u(sbh, hl);
+                h2 f = as_h2(shr1u(sbf, fl));
+                const int2* pa = lrow + (rc & 0xffu) * (NQ * kLanes);
+                const int2* pb = lrow + ((rc >> 8) & 0xffu) * (NQ * kLanes);
+                int2 wa[NQ], wb[NQ];
+#pragma unroll
+                for (int qq = 0; qq < NQ; ++qq) {
+                    wa[qq] = pa[qq * kLanes];
+                    wb[qq] = pb[qq * kLanes];
+                }
+                // H_diag + S for every row first (from the previous column's
+                // H), so H is then updated in place: no register rotation
+                h2 T[RI];
+#pragma unroll
+                for (int r = 0; r < RI; ++r) {
+                    const int2 xa = wa[r >> 2], xb = wb[r >> 2];
+                    const uint32_t ua = static_cast<uint32_t>((r & 2) ? xa.y : xa.x);
+                    const uint32_t ub = static_cast<uint32_t>((r & 2) ? xb.y : xb.x);
+                    // low half: subject A's S for row r, high half: subject B's
+                    const h2 sc = as_h2(__builtin_amdgcn_perm(ub, ua, (r & 1) ? 0x07060302u : 0x05040100u));
+                    T[r] = (r == 0 ? as_h2(up_prev) : H[r - 1]) + sc;
+                }
+                up_prev = up0;
+#pragma unroll
+                for (int r = 0; r < RI; ++r) {
+                    const h2 h = hmax3(E[r], f, T[r]);
+                    const h2 n = h - go;
+                    E[r] = hmax3(E[r] - ge, n, zero);
+                    f = hmax3(f - ge, n, zero);
+                    H[r] = h;
+                    if (r & 1) best = hmax3(best, H[r - 1], h);
+                }
+                hl = h2_bits(H[RI - 1]);
+                fl = h2_bits(f);
+                if (!last) {
+                    // lane 63 finished column k - 63: collect it for the next pass
+                    const int oc = k0 + m - (kLanes - 1);
+                    if (oc >= 0) {
+                        const int slot = oc & (kLanes - 1);
+                        const uint32_t vh = __builtin_amdgcn_readlane(hl, kLanes - 1);
+                        const uint32_t vf = __builtin_amdgcn_readlane(fl, kLanes - 1);
+                        out_h = lane == slot ? vh : out_h;
+                        out_f = lane == slot ? vf : out_f;
+                        if (slot == kLanes - 1 || oc == L - 1) {
+                            const int col = (oc & ~(kLanes - 1)) + lane;
+                            if (col <= oc) {
+                                bnd_h[col] = out_h;
+                                bnd_f[col] = out_f;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+    // wave max-reduction of the packed maxima
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(h2_bits(best)), off));
+        best = __builtin_elementwise_maximum(best, as_h2(o));
+    }
+    if (lane == 0) {
+        const int ba = static_cast<int>(static_cast<float>(best.x));
+        const int bb = static_cast<int>(static_cast<float>(best.y));
+        if (hasA) {
+            a.scores[a.subj_id[sa]] = ba;
+            if (a.rescue_list && ba >= a.sat_limit) a.rescue_list[atomicAdd(a.rescue_count, 1)] = sa;
+        }
+        if (hasB) {
+            a.scores[a.subj_id[sb]] = bb;
+            if (a.rescue_list && bb >= a.sat_limit) a.rescue_list[atomicAdd(a.rescue_count, 1)] = sb;
+        }
+    }
+}
+
+int intra_x2_rows_for(int qlen, int longest) {
+    // chunks x steps x (cell pairs per lane-step + conveyor/hand-off overhead)
+    int best_ri = 16;
+    double best_cost = 1e300;
+    for (int ri = 4; ri <= 16; ri += 4) {
+        const int chunk = kLanes * ri;
+        const int nch = (qlen + chunk - 1) / chunk;
+        const double cost = static_cast<double>(nch) * (longest + kLanes - 1) * (ri * 4.5 + 18.0);
+        if (cost < best_cost) {
+            best_cost = cost;
+            best_ri = ri;
+        }
+    }
+    return best_ri;
+}
+
+hipError_t launch_intra_x2(const IntraArgs& a, int ri, hipStream_t s) {
+    if (a.nsubj <= 0 || a.qpad <= 0) return hipSuccess;
+    const int npairs = (a.nsubj + 1) / 2;
+    const dim3 grid((npairs + kWavesPerWG - 1) / kWavesPerWG), block(kWavesPerWG * kLanes);
+    switch (ri) {
+        case 4: hipLaunchKernelGGL((sw_intra_x2<4>), grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((sw_intra_x2<8>), grid, block, 0, s, a); break;
+        case 12: hipLaunchKernelGGL((sw_intra_x2<12>), grid, block, 0, s, a); break;
+        case 16: hipLaunchKernelGGL((sw_intra_x2<16>), grid, block, 0, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace swk

@@ -84,6 +84,16 @@ struct IntraArgs {
     int32_t* bnd_h;              // per subject: subj_off-indexed int32 rows
     int32_t* bnd_f;
     int32_t* scores;
+    // sw_intra_x2 (packed fp16): the int16 profile [kProfileRows][prof_stride]
+    // in `prof`, minus `bias` (the linear profile's gap bias) = raw S
+    int32_t prof_stride = 0;
+    int32_t bias = 0;
+    int32_t sat_limit = 0;       // flag subjects whose maximum reaches this
+    int32_t* rescue_list = nullptr;
+    int32_t* rescue_count = nullptr;
+    // sw_intra in list mode: only subjects subj_list[0 .. *list_count)
+    const int32_t* subj_list = nullptr;
+    const int32_t* list_count = nullptr;
 };
 
 // Strip heights (query rows held in registers per lane) the kernels are
@@ -131,9 +141,11 @@ bool inter_uses_f16(bool affine, int x2_ok);
 // The int16 packed kernel in list mode (blk_list / blk_count set): the
 // second stage of the fp16 rescue chain.
 hipError_t launch_inter_x2s_list(const InterArgs& a, bool affine, hipStream_t s);
-// Wave pairs over the widest blocks [0, nblocks) of a two-strips 32x8 scan
-// (sw_inter_x2p): same results as launch_inter_x2s, half the block latency.
-hipError_t launch_inter_x2p(const InterArgs& a, bool affine, bool f16, hipStream_t s);
+// Wave pairs over the widest blocks of a two-strips 32x8 scan (sw_inter_x2p):
+// same results as launch_inter_x2s, half the block latency.  merged: one
+// launch, blocks [0, blk_first) by pairs, [blk_first, nblocks) one per wave;
+// otherwise blocks [0, nblocks) by pairs only.
+hipError_t launch_inter_x2p(const InterArgs& a, bool affine, bool f16, bool merged, hipStream_t s);
 // true if the chosen inter kernel has a wave-pair form (two-strips 32x8).
 bool inter_has_pair(bool affine, int x2_ok);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.
@@ -146,6 +158,9 @@ bool inter_needs_rescue(bool affine, int x2_ok);
 int rescue_rows(bool affine);
 hipError_t launch_inter_rescue(const InterArgs& a, bool affine, hipStream_t s);
 hipError_t launch_intra(const IntraArgs& a, int ri, bool affine, hipStream_t s);
+// Two subjects per wave, packed fp16 (sw_intra_x2.hip); rows per lane 4..16.
+hipError_t launch_intra_x2(const IntraArgs& a, int ri, hipStream_t s);
+int intra_x2_rows_for(int qlen, int longest);
 
 // Traceback of chosen hits (sw_align.hip), linear gap, cpu.cpp's tie rules.
 struct AlignArgs {

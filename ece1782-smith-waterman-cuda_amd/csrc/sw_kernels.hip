@@ -637,15 +637,27 @@ __device__ __forceinline__ int shr1(int old, int src) {
 __host__ __device__ constexpr int intra_stride(int RI) { return kLanes * intra_rip(RI) + 4; }
 
 template <int RI, bool AFFINE>
+__device__ __forceinline__ void intra_subject(const IntraArgs& a, int sid, uint8_t* lds);
+
+template <int RI, bool AFFINE>
 __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kProfileRows * intra_stride(RI)];
+    if (a.list_count) {
+        // list mode: a fixed grid re-scores the subjects a packed kernel flagged
+        const int n = __builtin_amdgcn_readfirstlane(*a.list_count);
+        for (int i = blockIdx.x; i < n; i += gridDim.x) intra_subject<RI, AFFINE>(a, a.subj_list[i], lds);
+        return;
+    }
+    if (static_cast<int>(blockIdx.x) < a.nsubj) intra_subject<RI, AFFINE>(a, blockIdx.x, lds);
+}
+
+template <int RI, bool AFFINE>
+__device__ __forceinline__ void intra_subject(const IntraArgs& a, int sid, uint8_t* lds) {
     constexpr int CH = kLanes * RI;  // query rows per chunk
     constexpr int RIP = intra_rip(RI);
     constexpr int S = intra_stride(RI);
     constexpr int CHUNK_BYTES = kProfileRows * kLanes * RIP;  // one chunk of the host profile
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kProfileRows * S];
     const int lane = threadIdx.x;
-    const int sid = blockIdx.x;
-    if (sid >= a.nsubj) return;
     const int L = a.subj_len[sid];
     const uint8_t* __restrict__ res = a.residues + a.subj_off[sid];
     int32_t* bnd_h = a.bnd_h + a.subj_off[sid];
@@ -755,6 +767,7 @@ __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) best = max(best, __shfl_xor(best, off));
     if (lane == 0) a.scores[a.subj_id[sid]] = best;
+    __syncthreads();  // list mode: the next subject restages the LDS profile
 }
 
 // ---------------------------------------------------------------------------
@@ -799,8 +812,9 @@ static InterShape inter_shape(bool affine, int x2_ok) {
         else if (std::sscanf(e, "p%dx%d", &r, &g) == 2 && !affine &&
             ((r == 64 && (g == 8 || g == 4)) || (r == 32 && g == 8) || (r == 48 && g == 8)))
             v = InterShape{r, g, true, false, false};
-        else if (std::sscanf(e, "f%dx%d", &r, &g) == 2 && y_ok && affine && r == 32 && g == 8)
-            v = InterShape{64, 8, false, false, false, false, false, true, true};
+        else if (std::sscanf(e, "f%dx%d", &r, &g) == 2 && y_ok && affine &&
+                 ((r == 32 && (g == 8 || g == 4)) || (r == 24 && g == 4)))
+            v = InterShape{2 * r, g, false, false, false, false, false, true, true};
         else if (std::sscanf(e, "y%dx%d", &r, &g) == 2 && y_ok &&
                  ((r == 32 && (g == 8 || g == 4)) || (r == 16 && g == 8) || (r == 48 && g == 4)))
             v = InterShape{2 * r, g, false, false, false, false, false, true};  // R = rows per pass
@@ -935,10 +949,12 @@ hipError_t launch_inter(const InterArgs& a, bool affine, int x2_ok, hipStream_t 
 
 template <int RI>
 static void launch_intra_ri(const IntraArgs& a, bool affine, hipStream_t s) {
+    // list mode: 256 workgroups walk the device-side list (usually empty)
+    const dim3 grid(a.list_count ? std::min(a.nsubj, 256) : a.nsubj);
     if (affine)
-        hipLaunchKernelGGL((sw_intra<RI, true>), dim3(a.nsubj), dim3(kLanes), 0, s, a);
+        hipLaunchKernelGGL((sw_intra<RI, true>), grid, dim3(kLanes), 0, s, a);
     else
-        hipLaunchKernelGGL((sw_intra<RI, false>), dim3(a.nsubj), dim3(kLanes), 0, s, a);
+        hipLaunchKernelGGL((sw_intra<RI, false>), grid, dim3(kLanes), 0, s, a);
 }
 
 hipError_t launch_intra(const IntraArgs& a, int ri, bool affine, hipStream_t s) {

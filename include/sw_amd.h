@@ -202,6 +202,11 @@ SW_API int sw_timing_total(sw_handle* h, sw_timing* out, int32_t* nscans);
  * "sw_inter<32,8,affine>" (int32); "none" before any scan.  Valid until the
  * next scan on the handle.                                                  */
 SW_API const char* sw_last_kernel(sw_handle* h);
+/* Name of the intra-sequence (long-subject) kernel of the last scan:
+ * "sw_intra_x2<16>" (two subjects per wave, packed fp16, with int32
+ * re-scoring of flagged subjects), "sw_intra<6,affine>" (int32), or "none"
+ * when the database has no long subjects.                                   */
+SW_API const char* sw_last_intra_kernel(sw_handle* h);
 
 /* ---- ranking ---------------------------------------------------------------
  * Top-k of a score vector (score descending, id ascending on ties).

@@ -187,7 +187,7 @@ def test_device_topk(sw, handle, n, k):
 
 INTER_VARIANTS = ["32x8", "s32x8", "32x16", "s32x16", "48x8", "s48x8", "64x8", "s64x8", "16x16", "s16x16",
                   "x16x8", "x16x16", "x32x8", "x48x8", "y16x8", "y32x8", "y32x4",
-                  "y48x4", "f32x8"]
+                  "y48x4", "f32x8", "f32x4", "f24x4"]
 
 
 @pytest.mark.parametrize("variant", INTER_VARIANTS)
@@ -351,3 +351,31 @@ def test_wave_pair_kernel(sw, oracle, handle, monkeypatch, variant, width):
             assert pairs == 0
         if qlen == 900:
             assert want.max() > 2048  # the fp16 guard band is crossed
+
+
+@pytest.mark.parametrize("packed", ["1", "0"])
+def test_intra_two_subjects_per_wave(sw, oracle, handle, monkeypatch, packed):
+    """sw_intra_x2 (two long subjects per wave, packed fp16; SW_INTRA_X2=0:
+    int32 sw_intra only): rows per lane 4..16 (query lengths 40..2100, one to
+    several chunk passes), an odd number of long subjects, pairs of unequal
+    length, linear and affine scoring, and planted near-copies of the query
+    whose fp16 maxima cross 2048 (re-scored by sw_intra in list mode)."""
+    monkeypatch.setenv("SW_INTRA_X2", packed)
+    rng = np.random.default_rng(7)
+    q0 = sw.synth.query(2100, shard=8)
+    lens = rng.integers(70, 900, size=40)
+    subs = [sw.synth.query(int(n), shard=100 + k) for k, n in enumerate(lens)]
+    subs += [q0, q0[:1000], q0[300:1500]]   # 43 subjects: odd count
+    r = np.concatenate(subs).astype(np.uint8)
+    o = np.concatenate([[0], np.cumsum([len(x) for x in subs])]).astype(np.int64)
+    db = sw.Database(handle, r, o, long_threshold=64)
+    assert db.stats()["n_long"] == len(subs)
+    for qlen, mid, go, ge in [(40, 1, 12, 1), (375, 1, 12, 1), (700, 1, 11, 2), (1500, 0, 2, 2),
+                              (2100, 1, 12, 1), (260, 0, 8, 8)]:
+        q = q0[:qlen]
+        m = sw.capi.builtin_matrix(mid)
+        got = db.scan(q, m, go, ge)
+        want = oracle.scan(q, r, o, mat=m, gap_open=go, gap_extend=ge)
+        assert np.array_equal(got, want), (qlen, mid, go, ge, np.nonzero(got != want)[0][:10])
+        if qlen >= 1500:
+            assert want.max() > 2048
