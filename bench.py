@@ -59,6 +59,10 @@ VALU_MODEL = {
     "sw_inter_x2s<32,8,affine,fp16>": ((3.875 + 3.375) * 4.25 + 2.7) / 128,
     # per 2 x 64 cells: 3 v_pk_max_i16, 1 v_pk_sub_u16, 1 v_pk_add_u16, 1 v_or_b32
     "sw_inter_x2s<32,8,linear>": ((3 + 1 + 1) * 4.25 + 2.7) / 128,
+    # the same cells with the widest blocks run by wave pairs in the same launch
+    "sw_inter_x2p<32,8,affine,fp16>": ((3.875 + 3.375) * 4.25 + 2.7) / 128,
+    "sw_inter_x2p<32,8,linear>": ((3 + 1 + 1) * 4.25 + 2.7) / 128,
+    "sw_inter_x2p<32,8,affine>": ((4.83 + 2.83 + 1) * 4.25 + 2.7) / 128,
     # per 2 x 64 cells: 4.83 v_pk_max_i16, 2.83 v_pk_sub_u16, 1 v_pk_add_u16, 1 v_or_b32
     "sw_inter_x2s<32,8,affine>": ((4.83 + 2.83 + 1) * 4.25 + 2.7) / 128,
     # per 2 x 64 cells: 3 v_pk_max_i16, 1 v_pk_sub_u16, 1 v_pk_add_u16, 1 v_or_b32
@@ -386,8 +390,12 @@ def main():
         lens_desc = np.sort(offs[1:] - offs[:-1])[::-1]
         n_inter = n - st["n_long"]
         inter_res = residues - int(lens_desc[:st["n_long"]].sum())
-        n_coop = min(st["coop_blocks"] * 64, n_inter)
-        wave_res = inter_res - st["coop_residues"]
+        # blocks of a separate cooperative / wave-pair launch are not the
+        # dominant kernel's; merged pairs are part of it
+        side_blocks = st["coop_blocks"] + (0 if st["pair_merged"] else st["pair_blocks"])
+        side_res = st["coop_residues"] + (0 if st["pair_merged"] else st["pair_residues"])
+        n_coop = min(side_blocks * 64, n_inter)
+        wave_res = inter_res - side_res
         alg_bytes = wave_res + 12 * (n_inter - n_coop)
         kernel_ms = wave_ms
         wave_gcups = float(qtot) / nq * wave_res / (wave_ms * 1e-3) / 1e9 if wave_ms > 0 else 0.0
@@ -440,7 +448,7 @@ def main():
                                    "sw_inter_coop": round(coop_ms, 4), "sw_intra": round(intra_ms, 4),
                                    "scan_total": round(kt["total_ms"] / nsc, 4)},
             "cells_split_per_step": {"sw_inter": float(qtot) * wave_res,
-                                     "sw_inter_coop": float(qtot) * st["coop_residues"],
+                                     "sw_inter_coop": float(qtot) * side_res,
                                      "sw_intra": float(qtot) * (residues - inter_res)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),

@@ -48,7 +48,8 @@ class DbStats(ctypes.Structure):
                 ("n_long", ctypes.c_int64), ("device_bytes", ctypes.c_int64),
                 ("max_length", ctypes.c_int32), ("long_threshold", ctypes.c_int32),
                 ("coop_blocks", ctypes.c_int32), ("coop_residues", ctypes.c_int64),
-                ("max_id", ctypes.c_int32)]
+                ("max_id", ctypes.c_int32), ("pair_blocks", ctypes.c_int32),
+                ("pair_merged", ctypes.c_int32), ("pair_residues", ctypes.c_int64)]
 
 
 class Alignment(ctypes.Structure):

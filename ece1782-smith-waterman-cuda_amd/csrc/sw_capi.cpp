@@ -225,6 +225,8 @@ struct sw_db {
     std::vector<uint32_t> h_blk_groups;  // block widths (16-column groups), widest first
     std::vector<int64_t> h_blk_res;      // unpadded residues per block
     int32_t last_ncoop = 0;              // blocks the last scan gave the coop kernel
+    int32_t last_npair = 0;              // blocks the last scan ran by wave pairs
+    bool last_pair_merged = false;
     // intra part (long subjects)
     int64_t nlong = 0;
     int32_t long_max = 0;
@@ -731,6 +733,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // Empty query: every score is 0 (the reference's kernel leaves maxScore 0).
     if (qlen == 0) {
         db->last_ncoop = 0;
+        db->last_npair = 0;
         h->last_kernel = "none";
         h->last_intra = "none";
         HIPCHECK(hipEventRecord(h->ev[0], h->stream));
@@ -759,7 +762,9 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     const bool pair_merged = !(pm && pm[0] == '0');
     const int32_t ncoop =
         (!npair && !i16 && !p32 && db->nblocks) ? coop_blocks(db, swk::inter_coop_divisor(affine, x2_ok)) : 0;
-    db->last_ncoop = ncoop ? ncoop : npair;
+    db->last_ncoop = ncoop;
+    db->last_npair = npair;
+    db->last_pair_merged = npair && pair_merged;
     const int32_t qpad_coop = ncoop ? static_cast<int32_t>(round_up(qlen, swk::inter_coop_rows())) : 0;
     if ((rc = build_profiles(h, query, qlen, mat, go, affine, std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2}),
                              i16 || x2 || intra_x2,
@@ -882,6 +887,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             HIPCHECK(swk::launch_inter(a, affine, x2_ok, h->stream));
         }
         h->last_kernel = swk::inter_kernel_name(affine, x2_ok);
+        if (npair) h->last_kernel.replace(0, std::strlen("sw_inter_x2s"), "sw_inter_x2p");  // + wave pairs
         HIPCHECK(hipEventRecord(h->ev[7], h->stream));
         ++h->launches;
         if (ncoop || (npair && !pair_merged)) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
@@ -1263,6 +1269,10 @@ int sw_db_get_stats(const sw_db* db, sw_db_stats* out) {
     out->coop_blocks = db->built ? db->last_ncoop : 0;
     out->coop_residues = 0;
     for (int32_t b = 0; b < out->coop_blocks; ++b) out->coop_residues += db->h_blk_res[b];
+    out->pair_blocks = db->built ? db->last_npair : 0;
+    out->pair_merged = db->built && db->last_pair_merged ? 1 : 0;
+    out->pair_residues = 0;
+    for (int32_t b = 0; b < out->pair_blocks; ++b) out->pair_residues += db->h_blk_res[b];
     out->max_id = db->max_id;
     return SW_OK;
 }

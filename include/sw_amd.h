@@ -85,6 +85,11 @@ typedef struct sw_db_stats {
                                 depends on the scoring) */
     int64_t coop_residues;   /* unpadded residues in those blocks */
     int32_t max_id;          /* largest result id (-1 if empty): score arrays hold max_id+1 */
+    int32_t pair_blocks;     /* widest blocks run by wave pairs (sw_inter_x2p) in
+                                the most recent scan; in the default merged
+                                launch they belong to the main inter kernel */
+    int32_t pair_merged;     /* 1: pairs and single-wave blocks were one launch */
+    int64_t pair_residues;   /* unpadded residues in the pair blocks */
 } sw_db_stats;
 
 typedef struct sw_timing {
