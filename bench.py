@@ -55,18 +55,19 @@ SIMDS, CLOCK_HZ = 1024, 2.4e9   # 256 CUs x 4 SIMDs
 # (v_pk_maximum3_f16 and v_pk_add_f16 too, profiles/r01_f16_rate.txt),
 # v_or_b32 2.7 cycles per wave64 instruction).
 VALU_MODEL = {
-    # per 2 x 64 cells: 3.875 v_pk_add_f16, 3.375 v_pk_maximum3_f16, 1 v_or_b32
-    "sw_inter_x2s<32,8,affine,fp16>": ((3.875 + 3.375) * 4.25 + 2.7) / 128,
-    # per 2 x 64 cells: 3 v_pk_max_i16, 1 v_pk_sub_u16, 1 v_pk_add_u16, 1 v_or_b32
-    "sw_inter_x2s<32,8,linear>": ((3 + 1 + 1) * 4.25 + 2.7) / 128,
+    # per 2 x 64 cells (hipcc -S, the unrolled sub-group: 256 cell pairs):
+    # 3.15 v_pk_maximum3_f16, 2.14 v_pk_add_f16, 0.94 v_pk_fma_f16 (the
+    # column-biased fp16 cell, H_diag + S as lo * hi + diag, rebase included)
+    "sw_inter_x2s<32,8,affine,fp16>": (6.234 * 4.25) / 128,
+    # per 2 x 64 cells: 2.81 v_pk_max_i16, 0.94 v_pk_sub_u16, 0.94 v_pk_mad_u16
+    "sw_inter_x2s<32,8,linear>": (4.688 * 4.25) / 128,
     # the same cells with the widest blocks run by wave pairs in the same launch
-    "sw_inter_x2p<32,8,affine,fp16>": ((3.875 + 3.375) * 4.25 + 2.7) / 128,
-    "sw_inter_x2p<32,8,linear>": ((3 + 1 + 1) * 4.25 + 2.7) / 128,
-    "sw_inter_x2p<32,8,affine>": ((4.83 + 2.83 + 1) * 4.25 + 2.7) / 128,
-    # per 2 x 64 cells: 4.83 v_pk_max_i16, 2.83 v_pk_sub_u16, 1 v_pk_add_u16, 1 v_or_b32
-    "sw_inter_x2s<32,8,affine>": ((4.83 + 2.83 + 1) * 4.25 + 2.7) / 128,
-    # per 2 x 64 cells: 3 v_pk_max_i16, 1 v_pk_sub_u16, 1 v_pk_add_u16, 1 v_or_b32
-    "sw_inter_x2s<48,4,linear>": ((3 + 1 + 1) * 4.25 + 2.7) / 128,
+    "sw_inter_x2p<32,8,affine,fp16>": (6.234 * 4.25) / 128,
+    "sw_inter_x2p<32,8,linear>": (4.688 * 4.25) / 128,
+    # per 2 x 64 cells: 4.53 v_pk_max_i16, 2.65 v_pk_sub_u16, 0.94 v_pk_mad_u16
+    "sw_inter_x2p<32,8,affine>": (8.117 * 4.25) / 128,
+    "sw_inter_x2s<32,8,affine>": (8.117 * 4.25) / 128,
+    "sw_inter_x2s<48,4,linear>": (4.688 * 4.25) / 128,
     "sw_inter_x2<32,8,affine>": ((4.83 + 2.83 + 1) * 4.25 + 2.7) / 128,
     "sw_inter_x2<16,16,affine>": ((4.87 + 2.87 + 1) * 4.25 + 2.7) / 128,
     # per 64 cells: 1.5 v_max3, 1 v_add_sdwa, 1 v_sub clamp
@@ -428,7 +429,10 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if args.config == "c4" else "weak",
             "vs_baseline": None,
-            "dtype": "int32",
+            "dtype": "fp16" if "fp16" in kernel else "int16" if "_x2" in kernel else "int32",
+            "dtype_note": "the DP cells compute in packed 16-bit pairs (fp16 holds every integer up to 2048 "
+                          "exactly; a lane whose maximum nears that bound is re-scored in int16, then int32); "
+                          "scores are bit-exact int32",
             "data": "synthetic",
             "config": {
                 "workload": "%s, %d subjects/rank (%d residues/rank), %s, gap open %d / extend %d%s, top-%d "

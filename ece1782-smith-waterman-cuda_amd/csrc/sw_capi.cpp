@@ -34,6 +34,14 @@ namespace {
 
 thread_local std::string g_err;
 
+// packed fp16 pair (v, v) of a small integer (|v| <= 2048: exact)
+uint32_t f16_pair(int v) {
+    const _Float16 x = static_cast<_Float16>(static_cast<float>(v));
+    uint16_t b;
+    std::memcpy(&b, &x, 2);
+    return static_cast<uint32_t>(b) | (static_cast<uint32_t>(b) << 16);
+}
+
 int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
@@ -716,9 +724,14 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // flag their block for int32 re-scoring) as long as one cell's increment
     // stays far inside the guard band (kSat16 leaves 1152).
     //   m16 = 2: int16 exact; 1: guarded int16 allowed; 0: int32 only
-    const int x2_ok = (static_cast<int64_t>(qlen) + 2) * (max_s + go) < 32767 ? 2
-                      : (max_s + go < 1000 && ge < 1000)                     ? 1
-                                                                             : 0;
+    // Affine 16-bit scans run the fp16 column-biased cell first; its values
+    // sit up to 8 ge above the true ones, so absurd gap / matrix scales (far
+    // beyond any published scheme) go straight to int32.
+    const bool f16_fits = !affine || 2 * max_s + 9 * ge + go < 1024;
+    const int x2_ok = !f16_fits                                                   ? 0
+                      : (static_cast<int64_t>(qlen) + 2) * (max_s + go) < 32767 ? 2
+                      : (max_s + go < 1000 && ge < 1000)                       ? 1
+                                                                               : 0;
     const int R = swk::inter_rows(affine, x2_ok);
     const int32_t qpad_inter = static_cast<int32_t>(round_up(qlen, R));
     const int ri = db->nlong ? swk::intra_rows_for(qlen, db->long_max) : 0;
@@ -846,8 +859,12 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             a.rescue_list = listA + 1;
             HIPCHECK(hipMemsetAsync(listA, 0, sizeof(int32_t), h->stream));
             if (f16) HIPCHECK(hipMemsetAsync(listB, 0, sizeof(int32_t), h->stream));
-            // fp16 exact range: every integer up to 2048; H grows by <= max S per cell
-            a.sat_limit = 2048 - 2 * std::max(max_s, 1);
+            // fp16 exact range: every integer up to 2048; H grows by <= max S
+            // per cell and the column-biased cell stores values up to 8 ge
+            // above the true ones
+            a.sat_limit = 2048 - 2 * std::max(max_s, 1) - 8 * ge;
+            for (int j = 0; j <= 8; ++j) a.f16_step[j] = f16_pair(j * ge);
+            a.f16_gog = f16_pair(go - ge);
         }
         if (ncoop) {
             // on its own stream, so the per-wave kernel fills the GPU beside it

@@ -315,10 +315,12 @@ __device__ __forceinline__ uint32_t to_f16_bits(uint32_t v16) {
     return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, static_cast<_Float16>(static_cast<int16_t>(v16))));
 }
 
+// F16: the images hold S + bias (the column-biased cell's gap extension).
 template <int R, bool F16 = false>
 __device__ __forceinline__ void stage_x2s(X2Lds<R>& L, const int16_t* __restrict__ prof, int stride, int s0,
-                                          int lane) {
+                                          int lane, int bias = 0) {
     constexpr int RD = x2_row_dwords(R);
+    constexpr uint32_t one = F16 ? 0x3c00u : 1u;
     // lo image <- rows [s0, s0+R), hi image <- rows [s0+R, s0+2R)
 #pragma unroll
     for (int t = lane; t < 2 * kProfileRows * (R / 8); t += kLanes) {
@@ -334,11 +336,13 @@ __device__ __forceinline__ void stage_x2s(X2Lds<R>& L, const int16_t* __restrict
         for (int e = 0; e < 4; ++e) {
             uint32_t a0 = w[e] & 0xffffu, a1 = w[e] >> 16;
             if constexpr (F16) {
-                a0 = to_f16_bits(a0);
-                a1 = to_f16_bits(a1);
+                a0 = to_f16_bits(static_cast<uint32_t>(static_cast<int16_t>(a0) + bias));
+                a1 = to_f16_bits(static_cast<uint32_t>(static_cast<int16_t>(a1) + bias));
             }
-            o[2 * e] = img ? a0 << 16 : a0;
-            o[2 * e + 1] = img ? a1 << 16 : a1;
+            // the other half holds 1 (1.0 in fp16): the kernel forms the pair
+            // as lo * hi + H_diag in one v_pk_fma_f16 / v_pk_mad_u16
+            o[2 * e] = img ? (a0 << 16) | one : a0 | (one << 16);
+            o[2 * e + 1] = img ? (a1 << 16) | one : a1 | (one << 16);
         }
         int4* d = reinterpret_cast<int4*>((img ? L.hi : L.lo) + c * RD + 8 * k);
         d[0] = make_int4(o[0], o[1], o[2], o[3]);
@@ -384,7 +388,7 @@ __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>&
 // LIST: a rescue stage walking the device-side block list (a separate
 // instantiation, so the list loop costs the scan kernels no registers).
 template <int R, int SG, bool AFFINE, bool F16, bool LIST, int CR = 16>
-__global__ __launch_bounds__(256) void sw_inter_x2s(InterArgs a) {
+__global__ __launch_bounds__(256, 2) void sw_inter_x2s(InterArgs a) {
     static_assert(R % CR == 0 && SG % 4 == 0, "shape");
     static_assert(AFFINE || !F16, "the fp16 cell is affine only");
     __shared__ __attribute__((aligned(16))) X2Lds<R> lds[kWavesPerWG];
@@ -468,35 +472,42 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     const u2 go2 = {static_cast<unsigned short>(a.gap_open), static_cast<unsigned short>(a.gap_open)};
     const u2 ge2 = {static_cast<unsigned short>(a.gap_extend), static_cast<unsigned short>(a.gap_extend)};
     uint32_t* bnd = reinterpret_cast<uint32_t*>(a.bnd_h);
-    // fp16 gap constants (exact integers; unused by the int16 cell)
-    h2 go_h = {}, ge_h = {}, zero_h = {};
+    // fp16 column-biased cell constants (exact integers, host-built, SGPRs)
+    h2 ge_h = {}, gog_h = {}, reb_h = {};
     if constexpr (F16) {
-        go_h = h2{static_cast<_Float16>(a.gap_open), static_cast<_Float16>(a.gap_open)};
-        ge_h = h2{static_cast<_Float16>(a.gap_extend), static_cast<_Float16>(a.gap_extend)};
-        zero_h = h2{static_cast<_Float16>(0), static_cast<_Float16>(0)};
+        ge_h = __builtin_bit_cast(h2, a.f16_step[1]);
+        gog_h = __builtin_bit_cast(h2, a.f16_gog);
+        reb_h = __builtin_bit_cast(h2, a.f16_step[SG]);
     }
     const bool first = (s0 == 0);
     const bool last = (s0 + 2 * R >= a.qpad);
-    stage_x2s<R, F16>(L, prof16, a.prof_stride, s0, lane);
+    stage_x2s<R, F16>(L, prof16, a.prof_stride, s0, lane, F16 ? a.gap_extend : 0);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 
+    // fp16: every value of column jj of a sub-group carries the bias jj * ge
+    // (see the cell below); "zero" of column jj is f16_step[jj], the zero
+    // boundary row is (H, F') = (jj ge, (jj + 1) ge), and the state of column
+    // -1 is (SG - 1) ge (rebased to -ge before column 0)
+    const uint32_t zcol = F16 ? a.f16_step[SG - 1] : 0u;
     V H[R];
     V E[AFFINE ? R : 1];
 #pragma unroll
-    for (int r = 0; r < R; ++r) H[r] = P::from(0u);
+    for (int r = 0; r < R; ++r) H[r] = P::from(zcol);
 #pragma unroll
     for (int r = 0; r < (AFFINE ? R : 1); ++r) E[r] = P::from(0u);
-    uint32_t dtop = 0;                 // packed H of row -1 at the previous step
+    uint32_t dtop = zcol;              // packed H of row -1 at the previous step
     uint32_t dl_h[SG], dl_f[SG];       // low strip's bottom row, SG steps back
     uint32_t bin[SG], bin_n[SG];       // HBM boundary in (H | F << 16), this / next sub-group
+    uint32_t bz[SG];                   // the zero boundary row
     uint32_t rc[SG / 4], rp[SG / 4], rn[SG / 4];  // codes: current (low), previous (high), next
 #pragma unroll
     for (int q = 0; q < SG; ++q) {
-        dl_h[q] = 0;
-        dl_f[q] = 0;
-        bin[q] = 0;
+        bz[q] = F16 ? lo_lo(a.f16_step[q], a.f16_step[q + 1]) : 0u;
+        dl_h[q] = F16 ? a.f16_step[q] : 0u;
+        dl_f[q] = F16 ? a.f16_step[q + 1] : 0u;
+        bin[q] = bz[q];
         bin_n[q] = 0;
     }
 #pragma unroll
@@ -522,7 +533,82 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
                 else load_pairs<SG>(bin_n, reinterpret_cast<const int32_t*>(bnd) + base + noff);
             }
         }
-        V up = P::from(0u), diag = P::from(0u), f = P::from(0u);
+        if constexpr (F16) {
+            // rebase: column SG-1's bias (SG-1) ge -> column 0's 0, applied to
+            // what crosses the sub-group boundary (H as the next diagonal, E)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                H[r] = H[r] - reb_h;
+                E[r] = E[r] - reb_h;
+            }
+            dtop = P::bits(P::from(dtop) - reb_h);
+        }
+        // One cell pair of column jj.  `up`, `diag`, `f` and `cb` roll down
+        // the column; `bst` is the running maximum of the int16 cells.
+        // (A two-stream schedule — rows [0, 16) of column m beside rows
+        // [16, 32) of column m - 1, 8-row chunks — removes the s_nop gfx950
+        // puts between back-to-back dependent packed ops, 525 -> 50 per
+        // sub-group, but measured 1 % slower affine and 3 % slower linear:
+        // the second wave on the SIMD already hides the nops.)
+        // slo = (S_low strip, 1), shi = (1, S_high strip): slo * shi + diag is
+        // the pair's H_diag + S in one packed op (no v_or_b32 to assemble it).
+        auto cell = [&](V& Hr, V& Er, V& up, V& diag, V& f, V& cb, V& bst, const V slo, const V shi,
+                        const bool top, const int jj) {
+            if constexpr (F16) {
+                // Column-biased Farrar cell.  Column jj of a sub-group holds
+                // H~ = H + jj ge, E' = E + jj ge and F' = F + (jj + 1) ge, so
+                // E's gap extension is the drift of the bias (E' = max(E', m),
+                // no subtraction) and the profile holds S + ge (the diagonal
+                // comes from column jj - 1).  F carries the 0 floor (so
+                // H >= 0): F' = max3(F' - ge, H~ - go + ge, (jj + 1) ge).
+                // 6 packed ops per cell pair instead of 7 (+ 2 per row per
+                // sub-group for the rebase above).
+                const h2 g = f - ge_h;
+                const h2 h = max3h(Er, g, __builtin_elementwise_fma(slo, shi, diag));
+                const h2 m = h - gog_h;
+                Er = __builtin_elementwise_maximum(Er, m);
+                f = max3h(g, m, __builtin_bit_cast(h2, a.f16_step[jj + 1]));
+                diag = Hr;
+                Hr = h;
+                up = h;
+                cb = top ? h : __builtin_elementwise_maximum(cb, h);
+            } else if constexpr (!AFFINE) {
+                const s2 h = usub2(max2(max2(Hr, up), slo * shi + diag), go2);
+                diag = Hr;
+                Hr = h;
+                up = h;
+                bst = max2(bst, h);
+            } else {
+                const s2 h = max2(max2(Er, f), slo * shi + diag);
+                const s2 n = usub2(h, go2);
+                Er = max2(usub2(Er, ge2), n);
+                f = max2(usub2(f, ge2), n);
+                diag = Hr;
+                Hr = h;
+                up = h;
+                bst = max2(bst, h);
+            }
+        };
+        // end of column jj: its bottom row feeds the high strip SG steps later
+        auto col_done = [&](const V up, const V f, V cb, const int jj) {
+            dl_h[jj] = P::bits(up);
+            if constexpr (AFFINE) dl_f[jj] = P::bits(f);
+            if constexpr (F16) {
+                // the column's maximum, unbiased
+                if (jj > 0) cb = cb - __builtin_bit_cast(h2, a.f16_step[jj]);
+                best = __builtin_elementwise_maximum(best, cb);
+            }
+        };
+        // row -1 inputs of column jj: low strip from HBM (previous pass),
+        // high strip from the low strip's bottom row SG steps back
+        auto col_start = [&](V& up, V& diag, V& f, const int jj) {
+            const uint32_t u = lo_lo(bin[jj], dl_h[jj]);
+            up = P::from(u);
+            diag = P::from(dtop);
+            dtop = u;
+            if constexpr (AFFINE) f = P::from(lo_lo(bin[jj] >> 16, dl_f[jj]));
+        };
+        V up = P::from(0u), diag = P::from(0u), f = P::from(0u), cb = P::from(0u);
 #pragma unroll
         for (int t = 0; t < STEPS; ++t) {
             const int jj = t / NCH;
@@ -534,53 +620,17 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
             } else if (has_next) {
                 read_x2<R, CQ>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(rn, 0), code_of(rc, 0), 0, dep);
             }
-            if (k == 0) {
-                // row -1 inputs: low strip from HBM (previous pass), high
-                // strip from the low strip's bottom row 8 steps back
-                const uint32_t u = lo_lo(bin[jj], dl_h[jj]);
-                up = P::from(u);
-                diag = P::from(dtop);
-                dtop = u;
-                if constexpr (AFFINE) f = P::from(lo_lo(bin[jj] >> 16, dl_f[jj]));
-            }
+            if (k == 0) col_start(up, diag, f, jj);
             const int4(&pl)[CQ] = PL[t & 1];
             const int4(&ph)[CQ] = PH[t & 1];
 #pragma unroll
             for (int i = 0; i < CR; ++i) {
                 const int r = CR * k + i;
-                const V sc = P::from(word(pl, i) | word(ph, i));
-                if constexpr (F16) {
-                    const h2 h = max3h(E[r], f, diag + sc);
-                    const h2 n = h - go_h;
-                    E[r] = max3h(E[r] - ge_h, n, zero_h);
-                    f = max3h(f - ge_h, n, zero_h);
-                    diag = H[r];
-                    H[r] = h;
-                    up = h;
-                    best = __builtin_elementwise_maximum(best, h);
-                } else if constexpr (!AFFINE) {
-                    const s2 h = usub2(max2(max2(H[r], up), diag + sc), go2);
-                    diag = H[r];
-                    H[r] = h;
-                    up = h;
-                    best = max2(best, h);
-                } else {
-                    const s2 h = max2(max2(E[r], f), diag + sc);
-                    const s2 n = usub2(h, go2);
-                    E[r] = max2(usub2(E[r], ge2), n);
-                    f = max2(usub2(f, ge2), n);
-                    diag = H[r];
-                    H[r] = h;
-                    up = h;
-                    best = max2(best, h);
-                }
+                cell(H[r], E[AFFINE ? r : 0], up, diag, f, cb, best, P::from(word(pl, i)), P::from(word(ph, i)),
+                     i == 0 && k == 0, jj);
             }
-            if (k == NCH - 1) {
-                const uint32_t oh = P::bits(up), of = AFFINE ? P::bits(f) : 0u;
-                dl_h[jj] = oh;
-                if constexpr (AFFINE) dl_f[jj] = of;
-            }
-            asm volatile("" : "+v"(best));
+            if (k == NCH - 1) col_done(up, f, cb, jj);
+            asm volatile("" : "+v"(best), "+v"(cb));
             __builtin_amdgcn_sched_barrier(0);
         }
         // the high strip just finished columns [col0 - SG, col0)
@@ -604,7 +654,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
                 rc[q] = rn[q];
             }
 #pragma unroll
-            for (int q = 0; q < SG; ++q) bin[q] = (first || !next_lo) ? 0u : bin_n[q];
+            for (int q = 0; q < SG; ++q) bin[q] = (first || !next_lo) ? bz[q] : bin_n[q];
         }
         if constexpr (PAIR) {
             __syncthreads();  // one tick of the pair's clock
@@ -661,7 +711,7 @@ __device__ __forceinline__ int pair_ticks(uint32_t ncols, int passes, int SG) {
 // widest-first across both forms (the LDS of the pair form, 53 KB, still
 // leaves 2 workgroups per CU, the register-bound occupancy of both).
 template <int R, int SG, bool AFFINE, bool F16, bool MERGED>
-__global__ __launch_bounds__(256) void sw_inter_x2p(InterArgs a) {
+__global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
     static_assert(R % 16 == 0 && SG % 4 == 0, "shape");
     static_assert(AFFINE || !F16, "the fp16 cell is affine only");
     __shared__ __attribute__((aligned(16))) X2Lds<R> lds[kWavesPerWG];
