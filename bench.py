@@ -55,15 +55,17 @@ SIMDS, CLOCK_HZ = 1024, 2.4e9   # 256 CUs x 4 SIMDs
 # (v_pk_maximum3_f16 and v_pk_add_f16 too, profiles/r01_f16_rate.txt),
 # v_or_b32 2.7 cycles per wave64 instruction).
 VALU_MODEL = {
-    # per 2 x 64 cells (hipcc -S, the unrolled sub-group: 256 cell pairs):
-    # 3.15 v_pk_maximum3_f16, 2.14 v_pk_add_f16, 0.94 v_pk_fma_f16 (the
-    # column-biased fp16 cell, H_diag + S as lo * hi + diag, rebase included)
-    "sw_inter_x2s<32,8,affine,fp16>": (6.234 * 4.25) / 128,
-    # per 2 x 64 cells: 2.81 v_pk_max_i16, 0.94 v_pk_sub_u16, 0.94 v_pk_mad_u16
-    "sw_inter_x2s<32,8,linear>": (4.688 * 4.25) / 128,
+    # per 2 x 64 cells: every VALU instruction of the sub-group loop (hipcc -S,
+    # the blocks of one 8-column sub-group = 256 cell pairs): the biased fp16
+    # cell (5 packed ops + ~0.53 v_pk_maximum3_f16 for the anti-diagonal
+    # maxima + column rebase + row-group resets) = 5.91 packed, 0.38 other
+    "sw_inter_x2s<32,8,affine,fp16>": (5.91 * 4.25 + 0.38 * 2.7) / 128,
+    # linear int16: 2.81 v_pk_max_i16, 0.94 v_pk_sub_u16, 0.94 v_pk_mad_u16
+    # in the hot block, 5.0 packed + 0.29 other over the whole loop
+    "sw_inter_x2s<32,8,linear>": (5.0 * 4.25 + 0.29 * 2.7) / 128,
     # the same cells with the widest blocks run by wave pairs in the same launch
-    "sw_inter_x2p<32,8,affine,fp16>": (6.234 * 4.25) / 128,
-    "sw_inter_x2p<32,8,linear>": (4.688 * 4.25) / 128,
+    "sw_inter_x2p<32,8,affine,fp16>": (5.91 * 4.25 + 0.38 * 2.7) / 128,
+    "sw_inter_x2p<32,8,linear>": (5.0 * 4.25 + 0.29 * 2.7) / 128,
     # per 2 x 64 cells: 4.53 v_pk_max_i16, 2.65 v_pk_sub_u16, 0.94 v_pk_mad_u16
     "sw_inter_x2p<32,8,affine>": (8.117 * 4.25) / 128,
     "sw_inter_x2s<32,8,affine>": (8.117 * 4.25) / 128,

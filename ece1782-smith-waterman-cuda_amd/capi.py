@@ -11,7 +11,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(PKG_DIR, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libswamd.so")
+# SW_AMD_LIB: an alternative build of the same library (A/B kernel experiments)
+LIB_PATH = os.environ.get("SW_AMD_LIB") or os.path.join(LIB_DIR, "libswamd.so")
 
 SW_OK = 0
 SW_ALPHABET = 25

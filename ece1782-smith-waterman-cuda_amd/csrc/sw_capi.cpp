@@ -724,10 +724,10 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // flag their block for int32 re-scoring) as long as one cell's increment
     // stays far inside the guard band (kSat16 leaves 1152).
     //   m16 = 2: int16 exact; 1: guarded int16 allowed; 0: int32 only
-    // Affine 16-bit scans run the fp16 column-biased cell first; its values
-    // sit up to 8 ge above the true ones, so absurd gap / matrix scales (far
-    // beyond any published scheme) go straight to int32.
-    const bool f16_fits = !affine || 2 * max_s + 9 * ge + go < 1024;
+    // Affine 16-bit scans run the fp16 biased cell first; its values sit up
+    // to 26 ge above the true ones, so absurd gap / matrix scales (far beyond
+    // any published scheme) go straight to int32.
+    const bool f16_fits = !affine || 2 * max_s + 27 * ge + go < 1024;
     const int x2_ok = !f16_fits                                                   ? 0
                       : (static_cast<int64_t>(qlen) + 2) * (max_s + go) < 32767 ? 2
                       : (max_s + go < 1000 && ge < 1000)                       ? 1
@@ -860,10 +860,10 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             HIPCHECK(hipMemsetAsync(listA, 0, sizeof(int32_t), h->stream));
             if (f16) HIPCHECK(hipMemsetAsync(listB, 0, sizeof(int32_t), h->stream));
             // fp16 exact range: every integer up to 2048; H grows by <= max S
-            // per cell and the column-biased cell stores values up to 8 ge
-            // above the true ones
-            a.sat_limit = 2048 - 2 * std::max(max_s, 1) - 8 * ge;
-            for (int j = 0; j <= 8; ++j) a.f16_step[j] = f16_pair(j * ge);
+            // per cell and the biased cell stores values up to 26 ge above
+            // the true ones (bias (15 + 7 + 2) ge, + 2 ge in the profile)
+            a.sat_limit = 2048 - 2 * std::max(max_s, 1) - 26 * ge;
+            for (int j = 0; j < 32; ++j) a.f16_step[j] = f16_pair(j * ge);
             a.f16_gog = f16_pair(go - ge);
         }
         if (ncoop) {

@@ -351,6 +351,31 @@ __device__ __forceinline__ void stage_x2s(X2Lds<R>& L, const int16_t* __restrict
 }
 
 __device__ __forceinline__ uint32_t lo_lo(uint32_t a, uint32_t b) { return (a & 0xffffu) | (b << 16); }
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const v4i lds_int4;
+
+// LDS byte address of a __shared__ object (the low half of its generic address)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p));
+}
+
+// read_x2 for the two-strips images from precomputed LDS byte addresses of
+// the two code rows (one v_mad each per column): the per-step tie to `dep`
+// keeps the reads from being hoisted, and the chunk offset folds into the
+// ds_read_b128 offset field.
+template <int N>
+__device__ __forceinline__ void read_x2a(int4 (&pl)[N], int4 (&ph)[N], uint32_t& aa, uint32_t& ab, int k,
+                                         uint32_t dep) {
+    asm volatile("" : "+v"(aa), "+v"(ab) : "v"(dep));
+    lds_int4* a = reinterpret_cast<lds_int4*>(static_cast<uintptr_t>(aa)) + N * k;
+    lds_int4* b = reinterpret_cast<lds_int4*>(static_cast<uintptr_t>(ab)) + N * k;
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+        pl[q] = __builtin_bit_cast(int4, a[q]);
+        ph[q] = __builtin_bit_cast(int4, b[q]);
+    }
+}
 __device__ __forceinline__ uint32_t hi_hi(uint32_t a, uint32_t b) { return (a >> 16) | (b & 0xffff0000u); }
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
@@ -406,6 +431,44 @@ __global__ __launch_bounds__(256, 2) void sw_inter_x2s(InterArgs a) {
     x2s_block<R, SG, AFFINE, F16, CR>(a, blk, L, lane);
 }
 
+// The fp16 cell's running maximum.  Cell (r, jj) of a sub-group (r = row of
+// the strip, jj = column of the sub-group) holds H + (r % kRowGroup + jj) ge
+// (see x2s_pass), so the maximum is kept per anti-diagonal k = r % 16 + jj:
+// acc[k] gathers the cells of bias k ge, two per v_pk_maximum3_f16 (cell (r,
+// jj) of an odd column with cell (r + 1, jj - 1), still in H[r + 1]).
+constexpr int kRowGroup = 16;
+constexpr int kAcc = kRowGroup + 8 - 1;
+template <bool F16>
+struct Best {
+    typename PkCell<F16>::V v;
+    __device__ __forceinline__ void init() { v = PkCell<F16>::from(0u); }
+    __device__ __forceinline__ typename PkCell<F16>::V value(const InterArgs&) const { return v; }
+};
+template <>
+struct Best<true> {
+    h2 acc[kAcc];
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int k = 0; k < kAcc; ++k) acc[k] = h2{0, 0};
+    }
+    __device__ __forceinline__ void pin() {
+        static_assert(kAcc == 23, "pin list");
+        asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]),
+                     "+v"(acc[6]), "+v"(acc[7]));
+        asm volatile("" : "+v"(acc[8]), "+v"(acc[9]), "+v"(acc[10]), "+v"(acc[11]), "+v"(acc[12]), "+v"(acc[13]),
+                     "+v"(acc[14]), "+v"(acc[15]));
+        asm volatile("" : "+v"(acc[16]), "+v"(acc[17]), "+v"(acc[18]), "+v"(acc[19]), "+v"(acc[20]),
+                     "+v"(acc[21]), "+v"(acc[22]));
+    }
+    __device__ __forceinline__ h2 value(const InterArgs& a) const {
+        h2 b = acc[0];
+#pragma unroll
+        for (int k = 1; k < kAcc; ++k)
+            b = __builtin_elementwise_maximum(b, acc[k] - __builtin_bit_cast(h2, a.f16_step[k]));
+        return b;
+    }
+};
+
 // Score and guard of one block (lane = subject).
 // Guarded mode: H grows by at most max S per cell, so a lane whose values
 // could have left the exact range has its running maximum in the guard
@@ -458,8 +521,8 @@ __device__ __forceinline__ void ring_load(uint32_t (&v)[SG], const int4* ring, i
 // out_ring, and every sub-group ends with one workgroup barrier (a tick).
 template <int R, int SG, bool AFFINE, bool F16, bool PAIR, int CR = 16>
 __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32_t ncols, uint64_t base, int lane,
-                                         int s0, typename PkCell<F16>::V& best, int4* ring, bool in_ring,
-                                         bool out_ring, int* tick) {
+                                         int s0, Best<F16>& best, int4* ring, bool in_ring, bool out_ring,
+                                         int* tick) {
     // SG: sub-group width = the lag (columns) between the two strips
     // CR: profile rows per LDS chunk (16: 2 x 4 ds_read_b128 in flight; 8
     // halves the chunk registers)
@@ -472,41 +535,43 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     const u2 go2 = {static_cast<unsigned short>(a.gap_open), static_cast<unsigned short>(a.gap_open)};
     const u2 ge2 = {static_cast<unsigned short>(a.gap_extend), static_cast<unsigned short>(a.gap_extend)};
     uint32_t* bnd = reinterpret_cast<uint32_t*>(a.bnd_h);
-    // fp16 column-biased cell constants (exact integers, host-built, SGPRs)
-    h2 ge_h = {}, gog_h = {}, reb_h = {};
+    // fp16 biased cell constants (exact integers, host-built, SGPRs)
+    static_assert(!F16 || (R % kRowGroup == 0 && SG <= 8), "fp16 row groups");
+    h2 gog_h = {}, reb_h = {}, grp_h = {};
     if constexpr (F16) {
-        ge_h = __builtin_bit_cast(h2, a.f16_step[1]);
         gog_h = __builtin_bit_cast(h2, a.f16_gog);
         reb_h = __builtin_bit_cast(h2, a.f16_step[SG]);
+        grp_h = __builtin_bit_cast(h2, a.f16_step[kRowGroup]);
     }
     const bool first = (s0 == 0);
     const bool last = (s0 + 2 * R >= a.qpad);
-    stage_x2s<R, F16>(L, prof16, a.prof_stride, s0, lane, F16 ? a.gap_extend : 0);
+    // fp16: the images hold S + 2 ge (the diagonal comes from bias r - 1 + jj - 1)
+    stage_x2s<R, F16>(L, prof16, a.prof_stride, s0, lane, F16 ? 2 * a.gap_extend : 0);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 
-    // fp16: every value of column jj of a sub-group carries the bias jj * ge
-    // (see the cell below); "zero" of column jj is f16_step[jj], the zero
-    // boundary row is (H, F') = (jj ge, (jj + 1) ge), and the state of column
-    // -1 is (SG - 1) ge (rebased to -ge before column 0)
-    const uint32_t zcol = F16 ? a.f16_step[SG - 1] : 0u;
+    // fp16: cell (r, jj) carries the bias (r % 16 + jj) ge (see the cell
+    // below).  Before the first sub-group's rebase the state is that of
+    // column SG - 1 of a sub-group: H of column -1 (= 0) is (r % 16 + SG - 1)
+    // ge, row -1's H (dtop) (SG - 2) ge; rows come in from the boundary with
+    // the last row group's bias, (15 + jj) ge for H and (16 + jj) ge for F.
     V H[R];
     V E[AFFINE ? R : 1];
 #pragma unroll
-    for (int r = 0; r < R; ++r) H[r] = P::from(zcol);
+    for (int r = 0; r < R; ++r) H[r] = P::from(F16 ? a.f16_step[r % kRowGroup + SG - 1] : 0u);
 #pragma unroll
     for (int r = 0; r < (AFFINE ? R : 1); ++r) E[r] = P::from(0u);
-    uint32_t dtop = zcol;              // packed H of row -1 at the previous step
+    uint32_t dtop = F16 ? a.f16_step[SG - 2] : 0u;  // packed H of row -1 at the previous step
     uint32_t dl_h[SG], dl_f[SG];       // low strip's bottom row, SG steps back
     uint32_t bin[SG], bin_n[SG];       // HBM boundary in (H | F << 16), this / next sub-group
     uint32_t bz[SG];                   // the zero boundary row
     uint32_t rc[SG / 4], rp[SG / 4], rn[SG / 4];  // codes: current (low), previous (high), next
 #pragma unroll
     for (int q = 0; q < SG; ++q) {
-        bz[q] = F16 ? lo_lo(a.f16_step[q], a.f16_step[q + 1]) : 0u;
-        dl_h[q] = F16 ? a.f16_step[q] : 0u;
-        dl_f[q] = F16 ? a.f16_step[q + 1] : 0u;
+        bz[q] = F16 ? lo_lo(a.f16_step[kRowGroup - 1 + q], a.f16_step[kRowGroup + q]) : 0u;
+        dl_h[q] = F16 ? a.f16_step[kRowGroup - 1 + q] : 0u;
+        dl_f[q] = F16 ? a.f16_step[kRowGroup + q] : 0u;
         bin[q] = bz[q];
         bin_n[q] = 0;
     }
@@ -518,7 +583,11 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
         else load_pairs<SG>(bin, reinterpret_cast<const int32_t*>(bnd) + base);
     }
     int4 PL[2][CQ], PH[2][CQ];
-    read_x2<R, CQ>(PL[0], PH[0], L, code_of(rc, 0), code_of(rp, 0), 0, 0);
+    constexpr uint32_t RB = x2_row_dwords(R) * 4;
+    const uint32_t blo = lds_addr(L.lo), bhi = lds_addr(L.hi);
+    // LDS addresses of the code rows of the column being prefetched
+    uint32_t aa = blo + code_of(rc, 0) * RB, ab = bhi + code_of(rp, 0) * RB;
+    read_x2a<CQ>(PL[0], PH[0], aa, ab, 0, 0);
 
     // sub-groups 0 .. ncols/SG: the last one runs the high strip only
     for (uint32_t col0 = 0; col0 <= ncols; col0 += SG) {
@@ -543,72 +612,73 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
             }
             dtop = P::bits(P::from(dtop) - reb_h);
         }
-        // One cell pair of column jj.  `up`, `diag`, `f` and `cb` roll down
-        // the column; `bst` is the running maximum of the int16 cells.
-        // (A two-stream schedule — rows [0, 16) of column m beside rows
-        // [16, 32) of column m - 1, 8-row chunks — removes the s_nop gfx950
-        // puts between back-to-back dependent packed ops, 525 -> 50 per
-        // sub-group, but measured 1 % slower affine and 3 % slower linear:
-        // the second wave on the SIMD already hides the nops.)
-        // slo = (S_low strip, 1), shi = (1, S_high strip): slo * shi + diag is
-        // the pair's H_diag + S in one packed op (no v_or_b32 to assemble it).
-        auto cell = [&](V& Hr, V& Er, V& up, V& diag, V& f, V& cb, V& bst, const V slo, const V shi,
-                        const bool top, const int jj) {
+        // One cell pair: row r of column jj.  `up`, `diag` and `f` roll down
+        // the column; slo = (S_low strip, 1), shi = (1, S_high strip), so
+        // slo * shi + diag is the pair's H_diag + S in one packed op.
+        auto cell = [&](const int r, const int jj, V& up, V& diag, V& f, const V slo, const V shi) {
             if constexpr (F16) {
-                // Column-biased Farrar cell.  Column jj of a sub-group holds
-                // H~ = H + jj ge, E' = E + jj ge and F' = F + (jj + 1) ge, so
-                // E's gap extension is the drift of the bias (E' = max(E', m),
-                // no subtraction) and the profile holds S + ge (the diagonal
-                // comes from column jj - 1).  F carries the 0 floor (so
-                // H >= 0): F' = max3(F' - ge, H~ - go + ge, (jj + 1) ge).
-                // 6 packed ops per cell pair instead of 7 (+ 2 per row per
-                // sub-group for the rebase above).
-                const h2 g = f - ge_h;
-                const h2 h = max3h(Er, g, __builtin_elementwise_fma(slo, shi, diag));
+                // Biased Farrar cell.  Cell (r, jj) holds H~ = H + b, E' = E + b,
+                // F~ = F + b with b = (r % 16 + jj) ge, so both gap extensions
+                // are the drift of the bias: E' = max(E', m) along the row and
+                // F~ = max3(F~, m, floor) down the column with m = H~ - go + ge,
+                // no subtraction.  F carries the 0 floor (H >= 0), b of the
+                // next row.  5 packed ops per cell pair (+ about half a max3
+                // for the maximum, 2 per row per sub-group for the column
+                // rebase, 4 per column for the row-group resets).
+                const int rg = r % kRowGroup;
+                if (rg == 0 && r > 0) {  // next row group: its bias restarts at 0
+                    f = f - grp_h;
+                    diag = diag - grp_h;
+                }
+                const h2 h = max3h(E[r], f, __builtin_elementwise_fma(slo, shi, diag));
                 const h2 m = h - gog_h;
-                Er = __builtin_elementwise_maximum(Er, m);
-                f = max3h(g, m, __builtin_bit_cast(h2, a.f16_step[jj + 1]));
-                diag = Hr;
-                Hr = h;
+                E[r] = __builtin_elementwise_maximum(E[r], m);
+                f = max3h(f, m, __builtin_bit_cast(h2, a.f16_step[rg + jj + 1]));
+                h2& acc = best.acc[rg + jj];
+                if (jj & 1) {
+                    if (rg + 1 < kRowGroup) acc = max3h(acc, h, H[r + 1]);  // H[r + 1]: cell (r + 1, jj - 1)
+                    else acc = __builtin_elementwise_maximum(acc, h);
+                } else if (rg == 0) {  // the even columns' other rows are partners above
+                    acc = __builtin_elementwise_maximum(acc, h);
+                }
+                diag = H[r];
+                H[r] = h;
                 up = h;
-                cb = top ? h : __builtin_elementwise_maximum(cb, h);
             } else if constexpr (!AFFINE) {
-                const s2 h = usub2(max2(max2(Hr, up), slo * shi + diag), go2);
-                diag = Hr;
-                Hr = h;
+                const s2 h = usub2(max2(max2(H[r], up), slo * shi + diag), go2);
+                diag = H[r];
+                H[r] = h;
                 up = h;
-                bst = max2(bst, h);
+                best.v = max2(best.v, h);
             } else {
-                const s2 h = max2(max2(Er, f), slo * shi + diag);
+                const s2 h = max2(max2(E[r], f), slo * shi + diag);
                 const s2 n = usub2(h, go2);
-                Er = max2(usub2(Er, ge2), n);
+                E[r] = max2(usub2(E[r], ge2), n);
                 f = max2(usub2(f, ge2), n);
-                diag = Hr;
-                Hr = h;
+                diag = H[r];
+                H[r] = h;
                 up = h;
-                bst = max2(bst, h);
+                best.v = max2(best.v, h);
             }
         };
         // end of column jj: its bottom row feeds the high strip SG steps later
-        auto col_done = [&](const V up, const V f, V cb, const int jj) {
+        auto col_done = [&](const V up, const V f, const int jj) {
             dl_h[jj] = P::bits(up);
             if constexpr (AFFINE) dl_f[jj] = P::bits(f);
-            if constexpr (F16) {
-                // the column's maximum, unbiased
-                if (jj > 0) cb = cb - __builtin_bit_cast(h2, a.f16_step[jj]);
-                best = __builtin_elementwise_maximum(best, cb);
-            }
         };
         // row -1 inputs of column jj: low strip from HBM (previous pass),
-        // high strip from the low strip's bottom row SG steps back
+        // high strip from the low strip's bottom row SG steps back (fp16:
+        // both from the last row group's bias to row -1's / row 0's)
         auto col_start = [&](V& up, V& diag, V& f, const int jj) {
-            const uint32_t u = lo_lo(bin[jj], dl_h[jj]);
+            uint32_t u = lo_lo(bin[jj], dl_h[jj]);
+            if constexpr (F16) u = P::bits(P::from(u) - grp_h);
             up = P::from(u);
             diag = P::from(dtop);
             dtop = u;
             if constexpr (AFFINE) f = P::from(lo_lo(bin[jj] >> 16, dl_f[jj]));
+            if constexpr (F16) f = f - grp_h;
         };
-        V up = P::from(0u), diag = P::from(0u), f = P::from(0u), cb = P::from(0u);
+        V up = P::from(0u), diag = P::from(0u), f = P::from(0u);
 #pragma unroll
         for (int t = 0; t < STEPS; ++t) {
             const int jj = t / NCH;
@@ -616,21 +686,26 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
             const uint32_t dep = P::bits(k == 0 ? H[R - 1] : H[CR * k - 1]);
             if (t + 1 < STEPS) {
                 const int jn = (t + 1) / NCH, kn = (t + 1) % NCH;
-                read_x2<R, CQ>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(rc, jn), code_of(rp, jn), kn, dep);
+                if (kn == 0) {
+                    aa = blo + code_of(rc, jn) * RB;
+                    ab = bhi + code_of(rp, jn) * RB;
+                }
+                read_x2a<CQ>(PL[(t + 1) & 1], PH[(t + 1) & 1], aa, ab, kn, dep);
             } else if (has_next) {
-                read_x2<R, CQ>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(rn, 0), code_of(rc, 0), 0, dep);
+                aa = blo + code_of(rn, 0) * RB;
+                ab = bhi + code_of(rc, 0) * RB;
+                read_x2a<CQ>(PL[(t + 1) & 1], PH[(t + 1) & 1], aa, ab, 0, dep);
             }
             if (k == 0) col_start(up, diag, f, jj);
             const int4(&pl)[CQ] = PL[t & 1];
             const int4(&ph)[CQ] = PH[t & 1];
 #pragma unroll
-            for (int i = 0; i < CR; ++i) {
-                const int r = CR * k + i;
-                cell(H[r], E[AFFINE ? r : 0], up, diag, f, cb, best, P::from(word(pl, i)), P::from(word(ph, i)),
-                     i == 0 && k == 0, jj);
-            }
-            if (k == NCH - 1) col_done(up, f, cb, jj);
-            asm volatile("" : "+v"(best), "+v"(cb));
+            for (int i = 0; i < CR; ++i) cell(CR * k + i, jj, up, diag, f, P::from(word(pl, i)), P::from(word(ph, i)));
+            if (k == NCH - 1) col_done(up, f, jj);
+            // pin the running maxima at every step: left free, the compiler
+            // defers the max reductions and keeps every h alive (spills)
+            if constexpr (!F16) asm volatile("" : "+v"(best.v));
+            else best.pin();
             __builtin_amdgcn_sched_barrier(0);
         }
         // the high strip just finished columns [col0 - SG, col0)
@@ -665,14 +740,13 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
 
 template <int R, int SG, bool AFFINE, bool F16, int CR>
 __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>& L, int lane) {
-    using P = PkCell<F16>;
-    using V = typename P::V;
     const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
     const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
-    V best = P::from(0u);
+    Best<F16> best;
+    best.init();
     for (int s0 = 0; s0 < a.qpad && ncols > 0; s0 += 2 * R)
         x2s_pass<R, SG, AFFINE, F16, false, CR>(a, L, ncols, base, lane, s0, best, nullptr, false, false, nullptr);
-    x2s_finish<F16>(a, blk, lane, best);
+    x2s_finish<F16>(a, blk, lane, best.value(a));
 }
 
 // ---------------------------------------------------------------------------
@@ -736,7 +810,8 @@ __global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
         if (b < npair) tmax = max(tmax, pair_ticks(a.blk_groups[b] * kGroupCols, passes, SG));
     }
     const int blk = blockIdx.x * 2 + pr;
-    V best = P::from(0u);
+    Best<F16> best;
+    best.init();
     int tick = 0;
     if (blk < npair) {
         const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
@@ -756,13 +831,14 @@ __global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
         __syncthreads();
         ++tick;
     }
-    if (blk < npair && w == 1) part[pr][lane] = P::bits(best);
+    if (blk < npair && w == 1) part[pr][lane] = P::bits(best.value(a));
     __syncthreads();
     if (blk < npair && w == 0) {
         const V o = P::from(part[pr][lane]);
-        if constexpr (F16) best = __builtin_elementwise_maximum(best, o);
-        else best = max2(best, o);
-        x2s_finish<F16>(a, blk, lane, best);
+        V b = best.value(a);
+        if constexpr (F16) b = __builtin_elementwise_maximum(b, o);
+        else b = max2(b, o);
+        x2s_finish<F16>(a, blk, lane, b);
     }
 }
 
@@ -798,11 +874,9 @@ static hipError_t launch_x2s_shape(const InterArgs& a, bool affine, hipStream_t 
 hipError_t launch_inter_x2s(const InterArgs& a, int R, int SG, bool affine, bool f16, hipStream_t s) {
     if (a.nblocks - a.blk_first <= 0 || a.qpad <= 0) return hipSuccess;
     if (f16) {
-        if (!(affine && ((R == 32 && (SG == 8 || SG == 4)) || (R == 24 && SG == 4))))
-            return hipErrorInvalidValue;
+        if (!(affine && R == 32 && (SG == 8 || SG == 4))) return hipErrorInvalidValue;
         const dim3 grid((a.nblocks - a.blk_first + kWavesPerWG - 1) / kWavesPerWG), block(kWavesPerWG * kLanes);
         if (R == 32 && SG == 8) hipLaunchKernelGGL((sw_inter_x2s<32, 8, true, true, false>), grid, block, 0, s, a);
-        else if (R == 24) hipLaunchKernelGGL((sw_inter_x2s<24, 4, true, true, false, 8>), grid, block, 0, s, a);
         else if (R == 32) hipLaunchKernelGGL((sw_inter_x2s<32, 4, true, true, false, 8>), grid, block, 0, s, a);
         return hipGetLastError();
     }

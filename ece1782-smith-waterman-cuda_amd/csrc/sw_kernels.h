@@ -67,10 +67,10 @@ struct InterArgs {
     int32_t blk_first;
     // fp16 kernel: a lane whose running maximum reaches this flags its block
     int32_t sat_limit;
-    // fp16 kernel, column-biased cell (sw_inter_x2.hip): f16_step[j] = the
-    // packed fp16 pair (j * gap_extend, j * gap_extend), j = 0..8, and
-    // f16_gog = packed (gap_open - gap_extend); host-built so they stay in SGPRs
-    uint32_t f16_step[9];
+    // fp16 kernel, biased cell (sw_inter_x2.hip): f16_step[j] = the packed
+    // fp16 pair (j * gap_extend, j * gap_extend), j = 0..31, and f16_gog =
+    // packed (gap_open - gap_extend); host-built so they stay in SGPRs
+    uint32_t f16_step[32];
     uint32_t f16_gog;
 };
 

@@ -813,7 +813,7 @@ static InterShape inter_shape(bool affine, int x2_ok) {
             ((r == 64 && (g == 8 || g == 4)) || (r == 32 && g == 8) || (r == 48 && g == 8)))
             v = InterShape{r, g, true, false, false};
         else if (std::sscanf(e, "f%dx%d", &r, &g) == 2 && y_ok && affine &&
-                 ((r == 32 && (g == 8 || g == 4)) || (r == 24 && g == 4)))
+                 r == 32 && (g == 8 || g == 4))
             v = InterShape{2 * r, g, false, false, false, false, false, true, true};
         else if (std::sscanf(e, "y%dx%d", &r, &g) == 2 && y_ok &&
                  ((r == 32 && (g == 8 || g == 4)) || (r == 16 && g == 8) || (r == 48 && g == 4)))

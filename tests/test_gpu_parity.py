@@ -194,7 +194,7 @@ def test_device_topk(sw, handle, n, k):
 
 INTER_VARIANTS = ["32x8", "s32x8", "32x16", "s32x16", "48x8", "s48x8", "64x8", "s64x8", "16x16", "s16x16",
                   "x16x8", "x16x16", "x32x8", "x48x8", "y16x8", "y32x8", "y32x4",
-                  "y48x4", "f32x8", "f32x4", "f24x4"]
+                  "y48x4", "f32x8", "f32x4"]
 
 
 @pytest.mark.parametrize("variant", INTER_VARIANTS)
