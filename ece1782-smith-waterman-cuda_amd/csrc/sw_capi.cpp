@@ -727,7 +727,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // Affine 16-bit scans run the fp16 biased cell first; its values sit up
     // to 26 ge above the true ones, so absurd gap / matrix scales (far beyond
     // any published scheme) go straight to int32.
-    const bool f16_fits = !affine || 2 * max_s + 27 * ge + go < 1024;
+    const bool f16_fits = 2 * max_s + 27 * ge + go < 1024;
     const int x2_ok = !f16_fits                                                   ? 0
                       : (static_cast<int64_t>(qlen) + 2) * (max_s + go) < 32767 ? 2
                       : (max_s + go < 1000 && ge < 1000)                       ? 1
@@ -765,7 +765,8 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     const bool f16 = swk::inter_uses_f16(affine, x2_ok);
     const int32_t qpad_rescue = rescue ? static_cast<int32_t>(round_up(qlen, swk::rescue_rows(affine))) : 0;
     // fp16 chain stage 2 (the int16 two-strips 32x8 kernel): 64-row passes
-    const int32_t qpad_list = f16 ? static_cast<int32_t>(round_up(qlen, 64)) : 0;
+    // (the linear list kernel is the 48x4 shape: 96-row passes)
+    const int32_t qpad_list = f16 ? static_cast<int32_t>(round_up(qlen, affine ? 64 : 96)) : 0;
     // widest blocks first, one cooperative workgroup each (int32, int8-profile paths)
     // two-strips scans: the widest blocks by wave pairs (at least two passes)
     const int32_t npair =
@@ -788,7 +789,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         db->device_bytes += (db->nblocks + 1) * sizeof(int32_t);
     }
     const bool multi_inter = qpad_inter > R || qpad_rescue > swk::rescue_rows(affine) ||
-                             qpad_coop > swk::inter_coop_rows() || qpad_list > 64;
+                             qpad_coop > swk::inter_coop_rows() || qpad_list > (affine ? 64 : 96);
     const bool multi_intra = (ri && qpad_intra > swk::kLanes * ri) || (ri2 && qpad_intra2 > swk::kLanes * ri2);
     if ((multi_inter || multi_intra) && (rc = ensure_bnd(db, affine, intra_x2))) return rc;
     if (intra_x2 && !db->d_lrescue) {

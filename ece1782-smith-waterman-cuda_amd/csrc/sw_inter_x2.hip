@@ -415,7 +415,6 @@ __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>&
 template <int R, int SG, bool AFFINE, bool F16, bool LIST, int CR = 16>
 __global__ __launch_bounds__(256, 2) void sw_inter_x2s(InterArgs a) {
     static_assert(R % CR == 0 && SG % 4 == 0, "shape");
-    static_assert(AFFINE || !F16, "the fp16 cell is affine only");
     __shared__ __attribute__((aligned(16))) X2Lds<R> lds[kWavesPerWG];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -545,8 +544,9 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     }
     const bool first = (s0 == 0);
     const bool last = (s0 + 2 * R >= a.qpad);
-    // fp16: the images hold S + 2 ge (the diagonal comes from bias r - 1 + jj - 1)
-    stage_x2s<R, F16>(L, prof16, a.prof_stride, s0, lane, F16 ? 2 * a.gap_extend : 0);
+    // fp16: the images hold S + 2 ge (the diagonal comes from bias r - 1 + jj - 1;
+    // the linear profile already holds S + g)
+    stage_x2s<R, F16>(L, prof16, a.prof_stride, s0, lane, F16 ? (AFFINE ? 2 : 1) * a.gap_extend : 0);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -608,7 +608,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 H[r] = H[r] - reb_h;
-                E[r] = E[r] - reb_h;
+                if constexpr (AFFINE) E[r] = E[r] - reb_h;
             }
             dtop = P::bits(P::from(dtop) - reb_h);
         }
@@ -616,7 +616,29 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
         // the column; slo = (S_low strip, 1), shi = (1, S_high strip), so
         // slo * shi + diag is the pair's H_diag + S in one packed op.
         auto cell = [&](const int r, const int jj, V& up, V& diag, V& f, const V slo, const V shi) {
-            if constexpr (F16) {
+            if constexpr (F16 && !AFFINE) {
+                // Biased linear cell: H~ = H + (r % 16 + jj) g, so the left and
+                // up terms H - g are the stored neighbours themselves and
+                // H~ = max(max3(left, up, H_diag + S + 2 g), floor): 3 packed
+                // ops per cell pair + the anti-diagonal maxima.
+                const int rg = r % kRowGroup;
+                if (rg == 0 && r > 0) {  // next row group: its bias restarts at 0
+                    up = up - grp_h;
+                    diag = diag - grp_h;
+                }
+                const h2 t = max3h(H[r], up, __builtin_elementwise_fma(slo, shi, diag));
+                const h2 h = __builtin_elementwise_maximum(t, __builtin_bit_cast(h2, a.f16_step[rg + jj]));
+                h2& acc = best.acc[rg + jj];
+                if (jj & 1) {
+                    if (rg + 1 < kRowGroup) acc = max3h(acc, h, H[r + 1]);
+                    else acc = __builtin_elementwise_maximum(acc, h);
+                } else if (rg == 0) {
+                    acc = __builtin_elementwise_maximum(acc, h);
+                }
+                diag = H[r];
+                H[r] = h;
+                up = h;
+            } else if constexpr (F16) {
                 // Biased Farrar cell.  Cell (r, jj) holds H~ = H + b, E' = E + b,
                 // F~ = F + b with b = (r % 16 + jj) ge, so both gap extensions
                 // are the drift of the bias: E' = max(E', m) along the row and
@@ -787,7 +809,6 @@ __device__ __forceinline__ int pair_ticks(uint32_t ncols, int passes, int SG) {
 template <int R, int SG, bool AFFINE, bool F16, bool MERGED>
 __global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
     static_assert(R % 16 == 0 && SG % 4 == 0, "shape");
-    static_assert(AFFINE || !F16, "the fp16 cell is affine only");
     __shared__ __attribute__((aligned(16))) X2Lds<R> lds[kWavesPerWG];
     __shared__ int4 ring[kWavesPerWG / 2][kRingSlots * (SG / 4) * kLanes];
     __shared__ uint32_t part[kWavesPerWG / 2][kLanes];
@@ -852,7 +873,7 @@ static hipError_t launch_x2p(const InterArgs& a, bool affine, bool f16, hipStrea
     const int nwg = (np + 1) / 2 + (M ? (a.nblocks - np + kWavesPerWG - 1) / kWavesPerWG : 0);
     const dim3 grid(nwg), block(kWavesPerWG * kLanes);
     if (f16 && affine) hipLaunchKernelGGL((sw_inter_x2p<32, 8, true, true, M>), grid, block, 0, s, a);
-    else if (f16) return hipErrorInvalidValue;
+    else if (f16) hipLaunchKernelGGL((sw_inter_x2p<32, 8, false, true, M>), grid, block, 0, s, a);
     else if (affine) hipLaunchKernelGGL((sw_inter_x2p<32, 8, true, false, M>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((sw_inter_x2p<32, 8, false, false, M>), grid, block, 0, s, a);
     return hipGetLastError();
@@ -874,10 +895,11 @@ static hipError_t launch_x2s_shape(const InterArgs& a, bool affine, hipStream_t 
 hipError_t launch_inter_x2s(const InterArgs& a, int R, int SG, bool affine, bool f16, hipStream_t s) {
     if (a.nblocks - a.blk_first <= 0 || a.qpad <= 0) return hipSuccess;
     if (f16) {
-        if (!(affine && R == 32 && (SG == 8 || SG == 4))) return hipErrorInvalidValue;
+        if (!(R == 32 && (SG == 8 || (SG == 4 && affine)))) return hipErrorInvalidValue;
         const dim3 grid((a.nblocks - a.blk_first + kWavesPerWG - 1) / kWavesPerWG), block(kWavesPerWG * kLanes);
-        if (R == 32 && SG == 8) hipLaunchKernelGGL((sw_inter_x2s<32, 8, true, true, false>), grid, block, 0, s, a);
-        else if (R == 32) hipLaunchKernelGGL((sw_inter_x2s<32, 4, true, true, false, 8>), grid, block, 0, s, a);
+        if (!affine) hipLaunchKernelGGL((sw_inter_x2s<32, 8, false, true, false>), grid, block, 0, s, a);
+        else if (SG == 8) hipLaunchKernelGGL((sw_inter_x2s<32, 8, true, true, false>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((sw_inter_x2s<32, 4, true, true, false, 8>), grid, block, 0, s, a);
         return hipGetLastError();
     }
     if (R == 32 && SG == 8) return launch_x2s_shape<32, 8>(a, affine, s);

@@ -793,13 +793,13 @@ static InterShape inter_shape(bool affine, int x2_ok) {
     // x2_ok: 2 = int16 provably exact, 1 = guarded int16 allowed, 0 = int32 only
     const char* ge = std::getenv("SW_INT16_GUARD");
     const bool y_ok = x2_ok == 2 || (x2_ok == 1 && !(ge && ge[0] == '0'));
-    // Affine: the fp16 form of the two-strips kernel (v_pk_maximum3_f16;
-    // 7.1 TCUPS on C2 vs 6.25 int16, profiles/r01_fp16/), always guarded
-    // (rescue chain fp16 -> int16 -> int32).  Linear: int16 y32x8 (3 waves
-    // per SIMD; 10.3 TCUPS).
+    // Both gap models: the fp16 form of the two-strips kernel (biased cell,
+    // v_pk_maximum3_f16; C2 affine 9.4 TCUPS vs 6.25 int16), always guarded
+    // (rescue chain fp16 -> int16 -> int32).  SW_INTER_VARIANT=y32x8 forces
+    // the int16 form (linear: 3 waves per SIMD, 11.2 TCUPS).
     InterShape v = affine ? (y_ok ? InterShape{64, 8, false, false, false, false, false, true, true}
                                   : InterShape{32, 8, false, false, false})
-                          : (y_ok ? InterShape{64, 8, false, false, false, false, false, true}
+                          : (y_ok ? InterShape{64, 8, false, false, false, false, false, true, true}
                                   : InterShape{64, 8, false, false, false});
     if (const char* e = std::getenv("SW_INTER_VARIANT")) {
         int r = 0, g = 0;
@@ -812,8 +812,7 @@ static InterShape inter_shape(bool affine, int x2_ok) {
         else if (std::sscanf(e, "p%dx%d", &r, &g) == 2 && !affine &&
             ((r == 64 && (g == 8 || g == 4)) || (r == 32 && g == 8) || (r == 48 && g == 8)))
             v = InterShape{r, g, true, false, false};
-        else if (std::sscanf(e, "f%dx%d", &r, &g) == 2 && y_ok && affine &&
-                 r == 32 && (g == 8 || g == 4))
+        else if (std::sscanf(e, "f%dx%d", &r, &g) == 2 && y_ok && r == 32 && (g == 8 || (g == 4 && affine)))
             v = InterShape{2 * r, g, false, false, false, false, false, true, true};
         else if (std::sscanf(e, "y%dx%d", &r, &g) == 2 && y_ok &&
                  ((r == 32 && (g == 8 || g == 4)) || (r == 16 && g == 8) || (r == 48 && g == 4)))

@@ -255,7 +255,7 @@ def test_default_kernel_selection(sw, handle, monkeypatch):
     db.scan(q, sw.capi.builtin_matrix(1), 12, 1)
     assert family(handle) == "sw_inter_x2s<32,8,affine,fp16>"
     db.scan(q)
-    assert family(handle) == "sw_inter_x2s<32,8,linear>"
+    assert family(handle) == "sw_inter_x2s<32,8,linear,fp16>"
     # beyond the static int16 bound but inside the guard band: guarded packed
     db.scan(q, sw.capi.builtin_matrix(0), 100, 1)
     assert family(handle) == "sw_inter_x2s<32,8,affine,fp16>"
