@@ -306,11 +306,15 @@ def test_db_save_load_roundtrip(sw, oracle, handle, tmp_path):
         sw.Database.load(handle, str(tmp_path / "trunc.swdb"))
 
 
+@pytest.mark.parametrize("scoring", [(1, 12, 1), (0, 2, 2), (1, 14, 3), (0, 5, 5)])
 @pytest.mark.parametrize("qlen,selfhit", [(375, True), (900, True), (2400, False)])
-def test_fp16_guard_band(sw, oracle, handle, monkeypatch, qlen, selfhit):
-    """The fp16 kernel is exact below 2048 - 2 max S and flags its block
+def test_fp16_guard_band(sw, oracle, handle, monkeypatch, qlen, selfhit, scoring):
+    """The fp16 kernels (biased cells: stored values sit up to 26 ge above
+    the true ones) are exact below 2048 - 2 max S - 26 ge and flag their block
     otherwise: subjects scoring around and far above 2048 (planted near-copies
-    of the query) next to ordinary ones, BLOSUM62 11/1, against the oracle."""
+    of the query) next to ordinary ones, affine (BLOSUM62 11/1 and 13/3) and
+    linear (BLOSUM50, gap 2 and 5) against the oracle."""
+    mid, go, ge = scoring
     monkeypatch.setenv("SW_INTER_VARIANT", "f32x8")
     r, o = sw.synth.database(300, shard=qlen)
     q = sw.synth.query(qlen, shard=qlen + 5)
@@ -318,11 +322,11 @@ def test_fp16_guard_band(sw, oracle, handle, monkeypatch, qlen, selfhit):
     r2 = np.concatenate([r] + extra)
     o2 = np.concatenate([o, o[-1] + np.cumsum([len(x) for x in extra])])
     db = sw.Database(handle, r2, o2, long_threshold=4000)
-    m = sw.capi.builtin_matrix(1)
-    got = db.scan(q, m, 12, 1)
-    want = oracle.scan(q, r2, o2, mat=m, gap_open=12, gap_extend=1)
+    m = sw.capi.builtin_matrix(mid)
+    got = db.scan(q, m, go, ge)
+    want = oracle.scan(q, r2, o2, mat=m, gap_open=go, gap_extend=ge)
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
-    assert family(handle) == "sw_inter_x2s<32,8,affine,fp16>"
+    assert family(handle) == "sw_inter_x2s<32,8,%s,fp16>" % ("linear" if go == ge else "affine")
     assert want.max() > 1000
 
 
