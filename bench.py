@@ -81,12 +81,14 @@ VALU_MODEL = {
     # per 64 cells: 2.82 v_sub clamp, 1.83 v_max, 1.5 v_max3, 1 v_add_sdwa
     "sw_inter<32,8,affine>": (2.82 * 2.45 + 1.83 * 4.37 + 1.5 * 4.4 + 4.2) / 64,
 }
-# sw_intra_x2<RI> (two long subjects per wave, packed fp16): per lane-step,
-# RI rows x (4 v_pk_add_f16 + 3.5 v_pk_maximum3_f16 + 1 v_perm_b32) for
-# 2 x 64 cells, plus ~75 cycles of conveyor overhead (3 DPP moves, 5
-# readlanes, 7 moves, compares/selects; hipcc -S of sw_intra_x2.hip)
+# sw_intra_x2<RI> (two long subjects per wave, the biased fp16 cell): per
+# lane-step, RI rows x (1 v_perm_b32 + 1 v_pk_add_f16 for H_diag + S, 5
+# packed cell ops incl. E's max, 0.53 v_pk_maximum3_f16 for the anti-diagonal
+# maxima, 0.25 for the rebase every 8 steps) for 2 x 64 cells, plus ~80
+# cycles of conveyor work (3 DPP moves, 3 readlanes, 2 hand-off adjusts, the
+# lane-63 collection; hipcc -S of sw_intra_x2.hip)
 for _ri in (4, 8, 12, 16):
-    VALU_MODEL["sw_intra_x2<%d>" % _ri] = (_ri * (7.5 * 4.25 + 4.25) + 75.0) / (128 * _ri)
+    VALU_MODEL["sw_intra_x2<%d>" % _ri] = (_ri * (6.78 * 4.25) + 80.0) / (128 * _ri)
 MATRICES = {"blosum50": 0, "blosum62": 1}
 SEED = 1782
 C4_TOTAL = 50_000_000

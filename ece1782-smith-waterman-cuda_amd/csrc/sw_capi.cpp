@@ -821,7 +821,10 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             x.prof_stride = P.stride;
             x.bias = affine ? 0 : go;  // the linear profile holds S + gap
             x.qpad = qpad_intra2;
-            x.sat_limit = 2048 - 2 * std::max(max_s, 1);
+            // biased cell: stored values up to (RI + 10) ge above the true ones
+            x.sat_limit = 2048 - 2 * std::max(max_s, 1) - 26 * ge;
+            for (int j = 0; j < 32; ++j) x.f16_step[j] = f16_pair(j * ge);
+            x.f16_gog = f16_pair(go - ge);
             x.rescue_count = db->d_lrescue;
             x.rescue_list = db->d_lrescue + 1;
             HIPCHECK(hipMemsetAsync(db->d_lrescue, 0, sizeof(int32_t), h->side));

@@ -56,6 +56,8 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
     static_assert(RI % 4 == 0 && RI <= 16, "rows per lane");
     constexpr int CH = kLanes * RI;  // query rows per chunk
     constexpr int NQ = RI / 4;       // 4-row quarters per lane
+    constexpr int NB = 8;            // steps per bias period (one rebase each)
+    constexpr int NACC = RI + NB - 1;
     __shared__ int2 img[kCodes * NQ * kLanes];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -72,18 +74,29 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
     uint32_t* bnd_h = reinterpret_cast<uint32_t*>(a.bnd_h) + (LA >= LB ? offA : (hasB ? a.subj_off[sb] : 0));
     uint32_t* bnd_f = reinterpret_cast<uint32_t*>(a.bnd_f) + (LA >= LB ? offA : (hasB ? a.subj_off[sb] : 0));
     const int16_t* prof16 = reinterpret_cast<const int16_t*>(a.prof);
-    const h2 go = {static_cast<_Float16>(a.gap_open), static_cast<_Float16>(a.gap_open)};
-    const h2 ge = {static_cast<_Float16>(a.gap_extend), static_cast<_Float16>(a.gap_extend)};
-    const h2 zero = {static_cast<_Float16>(0), static_cast<_Float16>(0)};
-    h2 best = zero;
+    auto step = [&](int j) { return as_h2(a.f16_step[j]); };  // (j ge, j ge)
+    const h2 gog = as_h2(a.f16_gog);
+    // Biased cell (the two-strips kernel's, sw_inter_x2.hip): at step k,
+    // row i of a lane holds H~ = H + (i + k % NB) ge, E' and F~ likewise, so
+    // both gap extensions are the drift of the bias:
+    //   h = max3(E', F~, H_diag + S + 2 ge);  m = h - (go - ge)
+    //   E' = max(E', m);  F~ = max3(F~, m, (i + 1 + k % NB) ge)
+    // The bias is a function of the step, the same in every lane, so every
+    // NB steps all lanes rebase together (H, E' and the row -1 diagonal
+    // drop NB ge), and what crosses lanes (the bottom row's H and F, one step
+    // old) drops (RI - 1) ge (+ NB ge at a rebase step).  Maxima per
+    // anti-diagonal i + k % NB, two cells per v_pk_maximum3_f16.
+    h2 acc[NACC];
+#pragma unroll
+    for (int q = 0; q < NACC; ++q) acc[q] = as_h2(0u);
     constexpr uint32_t kPadPair = kPadCode | (kPadCode << 8);
 
     for (int c0 = 0; c0 < a.qpad; c0 += CH) {
         const bool first = (c0 == 0);
         const bool last = (c0 + CH >= a.qpad);
         __syncthreads();  // the previous chunk's LDS reads are done
-        // stage rows [c0, c0 + CH) of codes 0..25 as fp16 (raw S: the linear
-        // profile is biased by the gap, a.bias)
+        // stage rows [c0, c0 + CH) of codes 0..25 as fp16 S + 2 ge (the
+        // linear profile is biased by the gap, a.bias)
         for (int t = threadIdx.x; t < kCodes * NQ * kLanes; t += kWavesPerWG * kLanes) {
             const int code = t / (NQ * kLanes);
             const int u = t % (NQ * kLanes);
@@ -91,7 +104,7 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
             const int2 v = *reinterpret_cast<const int2*>(prof16 + static_cast<size_t>(code) * a.prof_stride + c0 +
                                                           ln * RI + 4 * qq);
             const uint32_t w0 = static_cast<uint32_t>(v.x), w1 = static_cast<uint32_t>(v.y);
-            const int b = a.bias;
+            const int b = a.bias - 2 * a.gap_extend;
             const uint32_t o0 = f16_bits(static_cast<int16_t>(w0 & 0xffffu) - b) |
                                 (f16_bits(static_cast<int16_t>(w0 >> 16) - b) << 16);
             const uint32_t o1 = f16_bits(static_cast<int16_t>(w1 & 0xffffu) - b) |
@@ -101,91 +114,127 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
         __syncthreads();
         if (!hasA && !hasB) continue;  // wave-uniform; the barriers above are shared
 
+        // state of step -1 (column -1 - lane: H = 0), before step 0's rebase
         h2 H[RI], E[RI];
 #pragma unroll
         for (int r = 0; r < RI; ++r) {
-            H[r] = zero;
-            E[r] = zero;
+            H[r] = step(r + NB - 1);
+            E[r] = as_h2(0u);
         }
-        uint32_t hl = 0, fl = 0;       // this lane's bottom row (H, F-next) at its last column
-        uint32_t up_prev = 0;          // H of the row above at column j-1 (diag of row 0)
+        // bottom row (H, F) of this lane one step back, and H of the row above
+        // at the previous column (row 0's diagonal): zeros of step -1
+        uint32_t hl = a.f16_step[RI + NB - 2], fl = a.f16_step[RI + NB - 1];
+        uint32_t up_prev = a.f16_step[NB - 2];
         uint32_t rc = kPadPair;        // codes (A | B << 8) of this lane's current column
         uint32_t in_res = kPadPair, in_bh = 0, in_bf = 0, out_h = 0, out_f = 0;
         const int nsteps = L + kLanes - 1;
         const int2* lrow = img + lane;
 
         for (int k0 = 0; k0 < nsteps; k0 += kLanes) {
-            // lane-0 conveyors for steps k0 .. k0+63 (column k = step)
+            // lane-0 conveyors for steps k0 .. k0+63 (column k = step); the
+            // first chunk's row -1 is H = 0, F = 0 at the bias lane 0 reads
+            // them with (see the hand-off below)
             {
                 const int col = k0 + lane;
                 const uint32_t ca = col < LA ? resA[col] : kPadCode;
                 const uint32_t cb = col < LB ? resB[col] : kPadCode;
                 in_res = ca | (cb << 8);
-                in_bh = (!first && col < L) ? bnd_h[col] : 0u;
-                in_bf = (!first && col < L) ? bnd_f[col] : 0u;
+                const int bz = RI - 2 + (col % NB) + ((col % NB) == 0 ? NB : 0);
+                const uint32_t zh = f16_bits(bz * a.gap_extend), zf = f16_bits((bz + 1) * a.gap_extend);
+                in_bh = (!first && col < L) ? bnd_h[col] : zh | (zh << 16);
+                in_bf = (!first && col < L) ? bnd_f[col] : zf | (zf << 16);
             }
+            // whole bias periods (steps past nsteps run pad columns: harmless)
             const int mend = min(kLanes, nsteps - k0);
-            for (int m = 0; m < mend; ++m) {
-                const uint32_t sres = __builtin_amdgcn_readlane(in_res, m);
-                const uint32_t sbh = __builtin_amdgcn_readlane(in_bh, m);
-                const uint32_t sbf = __builtin_amdgcn_readlane(in_bf, m);
-                rc = shr1u(sres, rc);
-                const uint32_t up0 = shr1u(sbh, hl);
-                h2 f = as_h2(shr1u(sbf, fl));
-                const int2* pa = lrow + (rc & 0xffu) * (NQ * kLanes);
-                const int2* pb = lrow + ((rc >> 8) & 0xffu) * (NQ * kLanes);
-                int2 wa[NQ], wb[NQ];
+            for (int m0 = 0; m0 < mend; m0 += NB) {
 #pragma unroll
-                for (int qq = 0; qq < NQ; ++qq) {
-                    wa[qq] = pa[qq * kLanes];
-                    wb[qq] = pb[qq * kLanes];
-                }
-                // H_diag + S for every row first (from the previous column's
-                // H), so H is then updated in place: no register rotation
-                h2 T[RI];
+                for (int b = 0; b < NB; ++b) {
+                    const int m = m0 + b;
+                    const uint32_t sres = __builtin_amdgcn_readlane(in_res, m);
+                    const uint32_t sbh = __builtin_amdgcn_readlane(in_bh, m);
+                    const uint32_t sbf = __builtin_amdgcn_readlane(in_bf, m);
+                    rc = shr1u(sres, rc);
+                    // hand-off: the row above's bottom (H, F) from one step back
+                    const h2 adj = step(RI - 1 + (b == 0 ? NB : 0));
+                    const uint32_t up0 = h2_bits(as_h2(shr1u(sbh, hl)) - adj);
+                    h2 f = as_h2(shr1u(sbf, fl)) - adj;
+                    if (b == 0) {  // rebase: the bias period restarts
+                        const h2 reb = step(NB);
 #pragma unroll
-                for (int r = 0; r < RI; ++r) {
-                    const int2 xa = wa[r >> 2], xb = wb[r >> 2];
-                    const uint32_t ua = static_cast<uint32_t>((r & 2) ? xa.y : xa.x);
-                    const uint32_t ub = static_cast<uint32_t>((r & 2) ? xb.y : xb.x);
-                    // low half: subject A's S for row r, high half: subject B's
-                    const h2 sc = as_h2(__builtin_amdgcn_perm(ub, ua, (r & 1) ? 0x07060302u : 0x05040100u));
-                    T[r] = (r == 0 ? as_h2(up_prev) : H[r - 1]) + sc;
-                }
-                up_prev = up0;
+                        for (int r = 0; r < RI; ++r) {
+                            H[r] = H[r] - reb;
+                            E[r] = E[r] - reb;
+                        }
+                        up_prev = h2_bits(as_h2(up_prev) - reb);
+                    }
+                    const int2* pa = lrow + (rc & 0xffu) * (NQ * kLanes);
+                    const int2* pb = lrow + ((rc >> 8) & 0xffu) * (NQ * kLanes);
+                    int2 wa[NQ], wb[NQ];
 #pragma unroll
-                for (int r = 0; r < RI; ++r) {
-                    const h2 h = hmax3(E[r], f, T[r]);
-                    const h2 n = h - go;
-                    E[r] = hmax3(E[r] - ge, n, zero);
-                    f = hmax3(f - ge, n, zero);
-                    H[r] = h;
-                    if (r & 1) best = hmax3(best, H[r - 1], h);
-                }
-                hl = h2_bits(H[RI - 1]);
-                fl = h2_bits(f);
-                if (!last) {
-                    // lane 63 finished column k - 63: collect it for the next pass
-                    const int oc = k0 + m - (kLanes - 1);
-                    if (oc >= 0) {
-                        const int slot = oc & (kLanes - 1);
-                        const uint32_t vh = __builtin_amdgcn_readlane(hl, kLanes - 1);
-                        const uint32_t vf = __builtin_amdgcn_readlane(fl, kLanes - 1);
-                        out_h = lane == slot ? vh : out_h;
-                        out_f = lane == slot ? vf : out_f;
-                        if (slot == kLanes - 1 || oc == L - 1) {
-                            const int col = (oc & ~(kLanes - 1)) + lane;
-                            if (col <= oc) {
-                                bnd_h[col] = out_h;
-                                bnd_f[col] = out_f;
+                    for (int qq = 0; qq < NQ; ++qq) {
+                        wa[qq] = pa[qq * kLanes];
+                        wb[qq] = pb[qq * kLanes];
+                    }
+                    // H_diag + S for every row first (from the previous
+                    // column's H), so H is then updated in place
+                    h2 T[RI];
+#pragma unroll
+                    for (int r = 0; r < RI; ++r) {
+                        const int2 xa = wa[r >> 2], xb = wb[r >> 2];
+                        const uint32_t ua = static_cast<uint32_t>((r & 2) ? xa.y : xa.x);
+                        const uint32_t ub = static_cast<uint32_t>((r & 2) ? xb.y : xb.x);
+                        // low half: subject A's S for row r, high half: subject B's
+                        const h2 sc = as_h2(__builtin_amdgcn_perm(ub, ua, (r & 1) ? 0x07060302u : 0x05040100u));
+                        T[r] = (r == 0 ? as_h2(up_prev) : H[r - 1]) + sc;
+                    }
+                    up_prev = up0;
+#pragma unroll
+                    for (int r = 0; r < RI; ++r) {
+                        const h2 h = hmax3(E[r], f, T[r]);
+                        const h2 mm = h - gog;
+                        E[r] = __builtin_elementwise_maximum(E[r], mm);
+                        f = hmax3(f, mm, step(r + 1 + b));
+                        h2& ac = acc[r + b];
+                        if (b & 1) {
+                            if (r + 1 < RI) ac = hmax3(ac, h, H[r + 1]);  // H[r + 1]: cell (r + 1, step - 1)
+                            else ac = __builtin_elementwise_maximum(ac, h);
+                        } else if (r == 0) {  // the even steps' other rows are partners above
+                            ac = __builtin_elementwise_maximum(ac, h);
+                        }
+                        H[r] = h;
+                    }
+                    hl = h2_bits(H[RI - 1]);
+                    fl = h2_bits(f);
+                    if (!last) {
+                        // lane 63 finished column k - 63: collect it for the next pass
+                        const int oc = k0 + m - (kLanes - 1);
+                        if (oc >= 0 && oc < L) {
+                            const int slot = oc & (kLanes - 1);
+                            const uint32_t vh = __builtin_amdgcn_readlane(hl, kLanes - 1);
+                            const uint32_t vf = __builtin_amdgcn_readlane(fl, kLanes - 1);
+                            out_h = lane == slot ? vh : out_h;
+                            out_f = lane == slot ? vf : out_f;
+                            if (slot == kLanes - 1 || oc == L - 1) {
+                                const int col = (oc & ~(kLanes - 1)) + lane;
+                                if (col <= oc) {
+                                    bnd_h[col] = out_h;
+                                    bnd_f[col] = out_f;
+                                }
                             }
                         }
                     }
+                    // pin the maxima at every step (left free, the compiler
+                    // defers the reductions and keeps every h alive)
+#pragma unroll
+                    for (int q = 0; q < NACC; ++q) asm volatile("" : "+v"(acc[q]));
                 }
             }
         }
     }
-    // wave max-reduction of the packed maxima
+    // the lane's maximum (unbiased), then the wave's
+    h2 best = acc[0];
+#pragma unroll
+    for (int q = 1; q < NACC; ++q) best = __builtin_elementwise_maximum(best, acc[q] - step(q));
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(h2_bits(best)), off));

@@ -94,6 +94,8 @@ struct IntraArgs {
     int32_t prof_stride = 0;
     int32_t bias = 0;
     int32_t sat_limit = 0;       // flag subjects whose maximum reaches this
+    uint32_t f16_step[32] = {};  // as InterArgs: packed fp16 (j ge, j ge)
+    uint32_t f16_gog = 0;        // packed fp16 (go - ge, go - ge)
     int32_t* rescue_list = nullptr;
     int32_t* rescue_count = nullptr;
     // sw_intra in list mode: only subjects subj_list[0 .. *list_count)
