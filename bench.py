@@ -437,7 +437,8 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if args.config == "c4" else "weak",
             "vs_baseline": None,
-            "dtype": "fp16" if "fp16" in kernel else "int16" if "_x2" in kernel else "int32",
+            "dtype": ("fp16" if ("fp16" in roof_kernel or "intra_x2" in roof_kernel)
+                      else "int16" if "_x2" in roof_kernel else "int32"),
             "dtype_note": "the DP cells compute in packed 16-bit pairs (fp16 holds every integer up to 2048 "
                           "exactly; a lane whose maximum nears that bound is re-scored in int16, then int32); "
                           "scores are bit-exact int32",
