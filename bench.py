@@ -59,16 +59,16 @@ VALU_MODEL = {
     # the blocks of one 8-column sub-group = 256 cell pairs): the biased fp16
     # cell (5 packed ops + ~0.53 v_pk_maximum3_f16 for the anti-diagonal
     # maxima + column rebase + row-group resets) = 5.91 packed, 0.38 other
-    "sw_inter_x2s<32,8,affine,fp16>": (5.91 * 4.25 + 0.38 * 2.7) / 128,
+    "sw_inter_x2s<32,8,affine,fp16>": (5.91 * 4.25 + 0.305 * 2.7) / 128,
     # linear int16: 2.81 v_pk_max_i16, 0.94 v_pk_sub_u16, 0.94 v_pk_mad_u16
     # in the hot block, 5.0 packed + 0.29 other over the whole loop
     "sw_inter_x2s<32,8,linear>": (5.0 * 4.25 + 0.29 * 2.7) / 128,
     # the biased linear fp16 cell: fma, max3, floor max + ~0.53 maxima = 3.73
     # packed, 0.32 other
-    "sw_inter_x2s<32,8,linear,fp16>": (3.73 * 4.25 + 0.32 * 2.7) / 128,
-    "sw_inter_x2p<32,8,linear,fp16>": (3.73 * 4.25 + 0.32 * 2.7) / 128,
+    "sw_inter_x2s<32,8,linear,fp16>": (3.86 * 4.25 + 0.305 * 2.7) / 128,
+    "sw_inter_x2p<32,8,linear,fp16>": (3.86 * 4.25 + 0.305 * 2.7) / 128,
     # the same cells with the widest blocks run by wave pairs in the same launch
-    "sw_inter_x2p<32,8,affine,fp16>": (5.91 * 4.25 + 0.38 * 2.7) / 128,
+    "sw_inter_x2p<32,8,affine,fp16>": (5.91 * 4.25 + 0.305 * 2.7) / 128,
     "sw_inter_x2p<32,8,linear>": (5.0 * 4.25 + 0.29 * 2.7) / 128,
     # per 2 x 64 cells: 4.53 v_pk_max_i16, 2.65 v_pk_sub_u16, 0.94 v_pk_mad_u16
     "sw_inter_x2p<32,8,affine>": (8.117 * 4.25) / 128,

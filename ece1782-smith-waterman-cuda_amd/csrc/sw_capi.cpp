@@ -230,6 +230,7 @@ struct sw_db {
     // stage's (list B)
     int32_t* d_rescue = nullptr;
     int32_t* d_lrescue = nullptr;        // [count, subjects...] flagged by sw_intra_x2
+    uint64_t* h_trace = nullptr;         // SW_TRACE_FILE: host-mapped block timeline
     std::vector<uint32_t> h_blk_groups;  // block widths (16-column groups), widest first
     std::vector<int64_t> h_blk_res;      // unpadded residues per block
     int32_t last_ncoop = 0;              // blocks the last scan gave the coop kernel
@@ -669,9 +670,10 @@ int32_t coop_blocks(const sw_db* db, int divisor) {
 
 // Leading (widest) blocks of a two-strips scan handled by wave pairs
 // (sw_inter_x2p): blocks at least `width` columns wide, width =
-// residues / kPairDivisor (512 on C2: best of 16..1536, profiles/r01_pair*/,
-// r01_ix2/; SW_PAIR_WIDTH overrides; 0 disables).
-constexpr int64_t kPairDivisor = 400000;
+// residues / kPairDivisor (1024 on C2: with the biased cell 1,024 beat 256,
+// 512 and none by 2-4 %, profiles/r01_tail2/; SW_PAIR_WIDTH overrides; 0
+// disables).
+constexpr int64_t kPairDivisor = 200000;
 
 int32_t pair_blocks(const sw_db* db) {
     int64_t wmin = std::max<int64_t>(256, db->residues / kPairDivisor);
@@ -856,6 +858,12 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         a.bnd_h = db->d_bnd_h;
         a.bnd_f = db->d_bnd_f;
         a.scores = scores_dev;
+        if (std::getenv("SW_TRACE_FILE")) {
+            if (!db->h_trace)
+                HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&db->h_trace), 32 * db->nblocks,
+                                       hipHostMallocMapped));
+            HIPCHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.trace), db->h_trace, 0));
+        }
         int32_t* listA = db->d_rescue;                    // [count, ids...]
         int32_t* listB = db->d_rescue ? db->d_rescue + db->nblocks + 1 : nullptr;
         if (rescue) {
@@ -1272,6 +1280,14 @@ int sw_db_free(sw_db* db) {
     (void)hipSetDevice(db->h->device);
     (void)hipStreamSynchronize(db->h->stream);
     (void)hipStreamSynchronize(db->h->side);
+    if (db->h_trace) {  // the last scan's block timeline (tail analysis builds)
+        if (const char* path = std::getenv("SW_TRACE_FILE"))
+            if (FILE* f = std::fopen(path, "wb")) {
+                std::fwrite(db->h_trace, 32, static_cast<size_t>(db->nblocks), f);
+                std::fclose(f);
+            }
+        (void)hipHostFree(db->h_trace);
+    }
     free_dev(db);
     delete db;
     return SW_OK;

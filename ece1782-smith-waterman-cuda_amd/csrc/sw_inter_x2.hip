@@ -350,7 +350,10 @@ __device__ __forceinline__ void stage_x2s(X2Lds<R>& L, const int16_t* __restrict
     }
 }
 
-__device__ __forceinline__ uint32_t lo_lo(uint32_t a, uint32_t b) { return (a & 0xffffu) | (b << 16); }
+// half-word shuffles as one v_perm_b32 each (byte i of the result = byte
+// sel[i] of {src0 : src1}, src1 the low dword)
+__device__ __forceinline__ uint32_t lo_lo(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040100u); }
+__device__ __forceinline__ uint32_t hi_lo(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040302u); }
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const v4i lds_int4;
@@ -376,7 +379,7 @@ __device__ __forceinline__ void read_x2a(int4 (&pl)[N], int4 (&ph)[N], uint32_t&
         ph[q] = __builtin_bit_cast(int4, b[q]);
     }
 }
-__device__ __forceinline__ uint32_t hi_hi(uint32_t a, uint32_t b) { return (a >> 16) | (b & 0xffff0000u); }
+__device__ __forceinline__ uint32_t hi_hi(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
@@ -467,6 +470,31 @@ struct Best<true> {
         return b;
     }
 };
+
+// Block timeline for tail analysis (-DSW_TRACE_BLOCKS builds only).
+__device__ __forceinline__ uint64_t trace_now() {
+#ifdef SW_TRACE_BLOCKS
+    return __builtin_amdgcn_s_memrealtime();
+#else
+    return 0;
+#endif
+}
+__device__ __forceinline__ void trace_block(const InterArgs& a, int blk, uint64_t t0, int lane, uint32_t kind) {
+#ifdef SW_TRACE_BLOCKS
+    if (a.trace && lane == 0) {
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));  // HW_REG_XCC_ID
+        uint64_t* t = a.trace + 4 * static_cast<size_t>(blk);
+        t[0] = t0;
+        t[1] = t1;
+        t[2] = hw;
+        t[3] = xcc | (static_cast<uint64_t>(kind) << 32);
+    }
+#else
+    (void)a; (void)blk; (void)t0; (void)lane; (void)kind;
+#endif
+}
 
 // Score and guard of one block (lane = subject).
 // Guarded mode: H grows by at most max S per cell, so a lane whose values
@@ -697,7 +725,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
             up = P::from(u);
             diag = P::from(dtop);
             dtop = u;
-            if constexpr (AFFINE) f = P::from(lo_lo(bin[jj] >> 16, dl_f[jj]));
+            if constexpr (AFFINE) f = P::from(hi_lo(bin[jj], dl_f[jj]));
             if constexpr (F16) f = f - grp_h;
         };
         V up = P::from(0u), diag = P::from(0u), f = P::from(0u);
@@ -766,9 +794,11 @@ __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>&
     const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
     Best<F16> best;
     best.init();
+    const uint64_t t0 = trace_now();
     for (int s0 = 0; s0 < a.qpad && ncols > 0; s0 += 2 * R)
         x2s_pass<R, SG, AFFINE, F16, false, CR>(a, L, ncols, base, lane, s0, best, nullptr, false, false, nullptr);
     x2s_finish<F16>(a, blk, lane, best.value(a));
+    trace_block(a, blk, t0, lane, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -834,6 +864,7 @@ __global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
     Best<F16> best;
     best.init();
     int tick = 0;
+    const uint64_t t0 = trace_now();
     if (blk < npair) {
         const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
         const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
@@ -860,6 +891,7 @@ __global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
         if constexpr (F16) b = __builtin_elementwise_maximum(b, o);
         else b = max2(b, o);
         x2s_finish<F16>(a, blk, lane, b);
+        trace_block(a, blk, t0, lane, 1);
     }
 }
 

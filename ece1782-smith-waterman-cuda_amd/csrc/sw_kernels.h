@@ -72,6 +72,10 @@ struct InterArgs {
     // packed (gap_open - gap_extend); host-built so they stay in SGPRs
     uint32_t f16_step[32];
     uint32_t f16_gog;
+    // per-block timeline (builds with -DSW_TRACE_BLOCKS only; env
+    // SW_TRACE_FILE): [block][start, end, HW_ID, XCC_ID | kind << 32],
+    // s_memrealtime (100 MHz) stamps, host-mapped memory
+    uint64_t* trace;
 };
 
 // Long subjects: one wave per subject, query rows spread over the 64 lanes,
