@@ -16,3 +16,4 @@ from .solver import smith_waterman_cuda, smith_waterman_cuda_char  # noqa: F401
 MATRIX_BLOSUM50_REF = capi.MATRIX_BLOSUM50_REF
 MATRIX_BLOSUM62 = capi.MATRIX_BLOSUM62
 MATRIX_IDENTITY3 = capi.MATRIX_IDENTITY3
+MATRIX_BLOSUM50_CHAR = capi.MATRIX_BLOSUM50_CHAR

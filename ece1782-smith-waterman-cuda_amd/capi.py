@@ -19,6 +19,7 @@ SW_ALPHABET = 25
 MATRIX_BLOSUM50_REF = 0
 MATRIX_BLOSUM62 = 1
 MATRIX_IDENTITY3 = 2
+MATRIX_BLOSUM50_CHAR = 3  # the _char path's table as its lookup reads it ('*' = -5)
 
 # Every symbol include/sw_amd.h declares (checked by tests/test_abi.py).
 EXPORTED = (

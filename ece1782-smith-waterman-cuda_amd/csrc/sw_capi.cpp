@@ -1013,6 +1013,12 @@ int sw_builtin_matrix(int32_t id, int8_t* out625) {
     } else if (id == SW_MATRIX_IDENTITY3) {
         for (int a = 0; a < 25; ++a)
             for (int b = 0; b < 25; ++b) out625[a * 25 + b] = static_cast<int8_t>(a == b ? 3 : -3);
+    } else if (id == SW_MATRIX_BLOSUM50_CHAR) {
+        // the letters score as BLOSUM50_REF; '*' (and
+        // everything convertStringToChar maps to it) -5, '*' vs '*' +1
+        std::memcpy(out625, kBlosum50Ref, 625);
+        for (int k = 0; k < 25; ++k) out625[SW_CODE_STAR * 25 + k] = out625[k * 25 + SW_CODE_STAR] = -5;
+        out625[SW_CODE_STAR * 25 + SW_CODE_STAR] = 1;
     } else {
         return fail(SW_E_INVALID, "unknown matrix id");
     }

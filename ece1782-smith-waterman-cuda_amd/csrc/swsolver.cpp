@@ -60,9 +60,11 @@ Flat flatten(FASTADatabase& db) {
 
 // Scores of the flattened subjects (index k), reference scoring:
 // BLOSUM50 of SWSolver.cu:54-81 with linear gap 2 (SWSolver.cu:7).
-std::vector<int32_t> score_all(FASTAQuery& query, const Flat& f) {
+// char_compat: the _char path's scoring (SW_MATRIX_BLOSUM50_CHAR, no query
+// padding: SWSolver_char.cu:195-198 copies the query as is).
+std::vector<int32_t> score_all(FASTAQuery& query, const Flat& f, bool char_compat = false) {
     std::string q = query.get_buffer();
-    while (q.size() % TILE_SIZE != 0) q += "/";  // SWSolver.cu:267-269
+    while (!char_compat && q.size() % TILE_SIZE != 0) q += "/";  // SWSolver.cu:267-269
     std::vector<uint8_t> qc(q.size());
     check(sw_encode(q.data(), static_cast<int64_t>(q.size()), qc.data()), "sw_encode");
     const int64_t n = static_cast<int64_t>(f.record_ids.size());
@@ -71,7 +73,9 @@ std::vector<int32_t> score_all(FASTAQuery& query, const Flat& f) {
     sw_handle* h = handle();
     sw_db* db = nullptr;
     check(sw_db_create(h, f.residues.data(), f.offsets.data(), n, nullptr, &db), "sw_db_create");
-    const sw_scoring sc = {nullptr, 2, 2};
+    int8_t mat[625];
+    if (char_compat) check(sw_builtin_matrix(SW_MATRIX_BLOSUM50_CHAR, mat), "sw_builtin_matrix");
+    const sw_scoring sc = {char_compat ? mat : nullptr, 2, 2};
     const int rc = sw_scan(h, db, qc.data(), static_cast<int32_t>(qc.size()), &sc, scores.data());
     sw_db_free(db);
     check(rc, "sw_scan");
@@ -103,10 +107,14 @@ void sw_save_fasta_db(FASTADatabase& fdb, const std::string& path) {
     check(rc, "sw_db_save");
 }
 
+// Scores equal smith_waterman_cuda's (golden-pinned), returned in file order;
+// SW_CHAR_COMPAT=1 scores with the _char path's own table instead
+// (SW_MATRIX_BLOSUM50_CHAR).
 std::vector<seqid_score> smith_waterman_cuda_char(FASTAQuery& query, FASTADatabase& db) {
     std::lock_guard<std::mutex> lock(g_mu);
     const Flat f = flatten(db);
-    const std::vector<int32_t> scores = score_all(query, f);
+    const char* cc = std::getenv("SW_CHAR_COMPAT");
+    const std::vector<int32_t> scores = score_all(query, f, cc && cc[0] == '1');
     std::vector<seqid_score> out(scores.size());
     for (size_t k = 0; k < scores.size(); ++k) out[k] = std::make_pair(f.record_ids[k], scores[k]);
     std::stable_sort(out.begin(), out.end(),

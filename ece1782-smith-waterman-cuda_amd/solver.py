@@ -12,13 +12,17 @@ Same argument meaning and result semantics as the reference:
 * `result` receives (id, score) pairs APPENDED (SWSolver.cu:387) in descending
   padded-length order, file order within a length (SWSolver.cu:309,384-390).
 The char variant (which does not compile in the reference)
-returns the same scores as a fresh list in file order.
+returns the same scores as a fresh list in file order; in compat mode
+(SW_CHAR_COMPAT=1) it scores as the char path's own table
+would: '*' (and what its encoder maps to '*': the parser's '/' padding, U, O,
+lowercase) -5 against a letter, +1 against '*', the query unpadded.
 
 Differences, on purpose: scores are exact int32 (the reference stores int16
 and would overflow); there is no 1024-residue query cap
 (SWSolver.cu:85, F6); HIP errors raise instead of being ignored
 (SWSolver.cu:276).
 """
+import os
 import numpy as np
 
 from . import capi
@@ -41,12 +45,13 @@ def _padded_query(query):
     return q
 
 
-def _scores_by_record(query, db, handle=None, **scoring):
+def _scores_by_record(query, db, handle=None, pad=True, **scoring):
     h = handle or default_handle()
     residues, offsets, ids = db.flat(capi.encode)
     # Record ids may repeat only for the degenerate -1 case; key by position.
     gdb = capi.Database(h, residues, offsets)
-    scores = gdb.scan(capi.encode(_padded_query(query)), **scoring)
+    q = _padded_query(query) if pad else query.get_buffer()
+    scores = gdb.scan(capi.encode(q), **scoring)
     gdb.close()
     return ids, scores
 
@@ -67,7 +72,16 @@ def smith_waterman_cuda(query, db, result, handle=None):
     return None
 
 
-def smith_waterman_cuda_char(query, db, handle=None):
-    """Same scores, returned as a new list in file order."""
-    ids, scores = _scores_by_record(query, db, handle)
+def smith_waterman_cuda_char(query, db, handle=None, compat=None):
+    """Same scores, returned as a new list in file order.  compat (default:
+    env SW_CHAR_COMPAT == "1", as the C++ shim): score with the _char path's
+    own table instead — BLOSUM50 with '*' = -5 (SWSolver_char.cu:22-49 read
+    through its lookup :106-179) — and the query unpadded."""
+    if compat is None:
+        compat = os.environ.get("SW_CHAR_COMPAT") == "1"
+    if compat:
+        ids, scores = _scores_by_record(query, db, handle, pad=False,
+                                        matrix=capi.builtin_matrix(capi.MATRIX_BLOSUM50_CHAR), gap_open=2)
+    else:
+        ids, scores = _scores_by_record(query, db, handle)
     return [(int(i), int(s)) for i, s in zip(ids, scores)]

@@ -60,6 +60,10 @@ extern "C" {
 #define SW_MATRIX_BLOSUM50_REF 0  /* SWSolver.cu:54-81 exactly ('*' = 0) */
 #define SW_MATRIX_BLOSUM62 1      /* NCBI BLOSUM62 (option, not in the reference) */
 #define SW_MATRIX_IDENTITY3 2     /* +3/-3, the cpu.cpp:6-8 scheme */
+#define SW_MATRIX_BLOSUM50_CHAR 3 /* the _char path's table (SWSolver_char.cu:22-49) as
+                                     its lookup (:106-179) reads it: BLOSUM50_REF with
+                                     '*' = -5 and '*'/'*' = 1 (its L->W typo at :35 is
+                                     never read: the lookup orders the pair by range) */
 
 typedef struct sw_scoring {
     const int8_t* matrix;  /* 625 int8 (row = query code, col = subject code);

@@ -67,7 +67,84 @@ def _u8(a):
     return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
 
 
+MATRIX_BLOSUM50_CHAR = 3  # SWSolver_char.cu:22-49 through its lookup :106-179
+
+CODE_ORDER = "ARNDCQEGHILKMFPSTWYVBJZX*"   # SWSolver.cu:17-41
+CHAR_ORDER = "ABCDEFGHIJKLMNPQRSTVWXYZ*"   # SWSolver_char.cu:23 (alphabetical, no O/U)
+
+
+def char_table():
+    """The char path's 25x25 table in its alphabetical order
+    (SWSolver_char.cu:22-49).  Its letter entries are the reference BLOSUM50's
+    (SWSolver.cu:54-81; checked entry by entry against the source), except the
+    typo L->W = +2 (:35, W->L is -2 at :44); '*' rows/columns are -5 and
+    '*'/'*' is +1 (:48)."""
+    ref = matrix(MATRIX_BLOSUM50_REF)
+    t = np.zeros((25, 25), dtype=np.int64)
+    for i, a in enumerate(CHAR_ORDER):
+        for j, b in enumerate(CHAR_ORDER):
+            if a == "*" or b == "*":
+                t[i, j] = 1 if a == b else -5
+            else:
+                t[i, j] = ref[CODE_ORDER.index(a), CODE_ORDER.index(b)]
+    t[CHAR_ORDER.index("L"), CHAR_ORDER.index("W")] = 2
+    return t
+
+
+def char_lookup(query, subject, t):
+    """f_scoreSequence's substitution lookup on ASCII values
+    (SWSolver_char.cu:106-179), restated branch by branch: the pair is ordered
+    by alphabet range (A-N < P-T < V-Z,'*'), the query first within a range,
+    and the flat 625-entry table indexed with the range's ASCII offset
+    (65 / 66 / 67: the alphabet without O and U)."""
+    q, s = query, subject
+    flat = t.reshape(625)
+
+    def vstar(c):
+        return c > 85 or c == 42
+
+    if vstar(q) and vstar(s):
+        if q == 42 and s == 42:
+            return 1
+        if q == 42 or s == 42:
+            return -5
+        return int(flat[(q - 67) * 25 + s - 67])
+    if vstar(q) and s > 79:
+        return -5 if q == 42 else int(flat[(q - 67) * 25 + s - 66])
+    if q > 79 and vstar(s):
+        q, s = s, q
+        return -5 if q == 42 else int(flat[(q - 67) * 25 + s - 66])
+    if vstar(q):
+        return -5 if q == 42 else int(flat[(q - 67) * 25 + s - 65])
+    if vstar(s):
+        q, s = s, q
+        return -5 if q == 42 else int(flat[(q - 67) * 25 + s - 65])
+    if q > 79 and s > 79:
+        return int(flat[(q - 66) * 25 + s - 66])
+    if q > 79:
+        return int(flat[(q - 66) * 25 + s - 65])
+    if s > 79:
+        q, s = s, q
+        return int(flat[(q - 66) * 25 + s - 65])
+    return int(flat[(q - 65) * 25 + s - 65])
+
+
+def char_compat_matrix():
+    """The char path's effective scores in code order: M[qc][sc] =
+    char_lookup(letter(qc), letter(sc)); code 24 is '*', which
+    convertStringToChar (SWSolver_char.cu:56-85) also makes of U, O,
+    lowercase and the parser's '/' padding."""
+    t = char_table()
+    m = np.zeros((25, 25), dtype=np.int8)
+    for i, a in enumerate(CODE_ORDER):
+        for j, b in enumerate(CODE_ORDER):
+            m[i, j] = char_lookup(ord(a), ord(b), t)
+    return m
+
+
 def matrix(mid=MATRIX_BLOSUM50_REF):
+    if mid == MATRIX_BLOSUM50_CHAR:
+        return char_compat_matrix()
     p = lib().swo_matrix(mid)
     return np.ctypeslib.as_array(p, shape=(625,)).copy().reshape(25, 25)
 

@@ -48,7 +48,7 @@ def test_encode_matches_oracle(sw, oracle):
 
 
 def test_builtin_matrices_match_oracle(sw, oracle):
-    for mid in (0, 1, 2):
+    for mid in (0, 1, 2, 3):
         assert np.array_equal(sw.builtin_matrix(mid), oracle.matrix(mid))
     with pytest.raises(sw.SWError):
         sw.builtin_matrix(7)

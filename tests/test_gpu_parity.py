@@ -125,6 +125,30 @@ def test_batch_and_solver_api(sw, oracle, handle, tmp_path):
     assert order == sorted(order, reverse=True)
     chars = sw.smith_waterman_cuda_char(query, fdb)
     assert [s for _, s in chars] == golden
+    # the char path's own scoring ('*' / '/' padding = -5,
+    # query unpadded) against the oracle over the same flattened records
+    compat = sw.smith_waterman_cuda_char(query, fdb, compat=True)
+    flat_res, flat_offs, _ = fdb.flat(sw.encode)
+    want = oracle.scan(sw.encode(query.get_buffer()), flat_res, flat_offs,
+                       mat=oracle.matrix(oracle.MATRIX_BLOSUM50_CHAR), gap_open=2, gap_extend=2)
+    assert [s for _, s in compat] == [int(x) for x in want]
+
+
+def test_char_compat_star_residues(sw, oracle, handle):
+    """The compat table on sequences full of '*' (U, O, lowercase, '/' all
+    encode to it): +1 per '*'/'*' cell, -5 against letters, vs the oracle."""
+    rng = np.random.default_rng(4)
+    alphabet = "ARNDCQEGHILKMFPSTWYVBJZX*UO/acg"
+    seqs = ["".join(rng.choice(list(alphabet), size=int(rng.integers(1, 300)))) for _ in range(400)]
+    res = np.concatenate([sw.encode(x) for x in seqs])
+    offs = np.zeros(len(seqs) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(x) for x in seqs])
+    q = sw.encode("".join(rng.choice(list(alphabet), size=260)))
+    m = sw.builtin_matrix(sw.MATRIX_BLOSUM50_CHAR)
+    db = sw.Database(handle, res, offs, long_threshold=200)
+    got = db.scan(q, m, 2, 2)
+    want = oracle.scan(q, res, offs, mat=oracle.matrix(oracle.MATRIX_BLOSUM50_CHAR), gap_open=2, gap_extend=2)
+    assert np.array_equal(got, want)
 
 
 def test_long_query_self_hit_int32(sw, oracle, handle):

@@ -101,6 +101,28 @@ def test_matrices(oracle):
     assert (b62 == b62.T).all() and b62[17, 17] == 11
 
 
+def test_char_compat_matrix(oracle):
+    """the _char path's table read through its range-ordered
+    lookup (SWSolver_char.cu:22-49, :106-179): BLOSUM50 letters, '*' = -5
+    against a letter and +1 against itself; the table's L->W typo (+2) is never
+    read (L-W and W-L both come out -2)."""
+    t = oracle.char_table()
+    L, W = oracle.CHAR_ORDER.index("L"), oracle.CHAR_ORDER.index("W")
+    assert t[L, W] == 2 and t[W, L] == -2
+    m = oracle.matrix(oracle.MATRIX_BLOSUM50_CHAR)
+    b50 = oracle.matrix(0)
+    cl, cw = oracle.CODE_ORDER.index("L"), oracle.CODE_ORDER.index("W")
+    assert m[cl, cw] == m[cw, cl] == -2
+    assert (m == m.T).all()
+    assert (m[:24, :24] == b50[:24, :24]).all()
+    assert (m[24, :24] == -5).all() and (m[:24, 24] == -5).all() and m[24, 24] == 1
+    # a few lookups straight on ASCII (query, subject), both orders
+    for a, b in [("A", "A"), ("A", "W"), ("P", "Z"), ("Y", "*"), ("*", "*"), ("N", "T"), ("V", "I")]:
+        x = oracle.char_lookup(ord(a), ord(b), t)
+        y = oracle.char_lookup(ord(b), ord(a), t)
+        assert x == y == m[oracle.CODE_ORDER.index(a), oracle.CODE_ORDER.index(b)]
+
+
 def test_encoding(oracle):
     codes = oracle.encode("ARNDCQEGHILKMFPSTWYVBJZX")
     assert codes.tolist() == list(range(24))
