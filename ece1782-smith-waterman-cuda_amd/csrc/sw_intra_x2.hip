@@ -24,6 +24,9 @@
 // per cell, so a subject whose running maximum reaches a.sat_limit =
 // 2048 − 2·max S (computed exactly) is appended to a.rescue_list and re-scored
 // by the int32 sw_intra in list mode (sw_capi.cpp).
+#include <cstdlib>
+#include <type_traits>
+
 #include "sw_kernels.h"
 
 namespace swk {
@@ -49,16 +52,49 @@ __device__ __forceinline__ uint32_t shr1u(uint32_t old, uint32_t src) {
 
 constexpr int kCodes = kPadCode + 1;  // residue codes 0..24 and the pad code
 
+// fp16 pair of two int16 profile entries minus `b`
+__device__ __forceinline__ uint32_t f16x2_of(uint32_t w, int b) {
+    return f16_bits(static_cast<int16_t>(w & 0xffffu) - b) | (f16_bits(static_cast<int16_t>(w >> 16) - b) << 16);
+}
+
+// A lane's rows of one code in the LDS image, 4 rows (int2) per element when
+// RI is a multiple of 4 (one ds_read_b64), 2 rows (one dword, ds_read_b32)
+// otherwise; either way lane l's element sits at l·size in a 64-element row,
+// so the reads are conflict-free whatever code each lane reads.
+template <int RI>
+struct IntraImg {
+    static constexpr int kRows = RI % 4 == 0 ? 4 : 2;
+    using Elem = typename std::conditional<kRows == 4, int2, uint32_t>::type;
+    using LElem = __attribute__((address_space(3))) const Elem;
+    static constexpr int kPer = RI / kRows;  // elements per lane and code
+    static __device__ __forceinline__ uint32_t word(const Elem (&w)[kPer], int r) {
+        if constexpr (kRows == 4) return static_cast<uint32_t>((r & 2) ? w[r >> 2].y : w[r >> 2].x);
+        else return w[r >> 1];
+    }
+    // staging: the element of rows [4q, 4q + 4) or [2q, 2q + 2) of a lane
+    static __device__ __forceinline__ Elem load(const int16_t* p, int b) {
+        if constexpr (kRows == 4) {
+            const int2 v = *reinterpret_cast<const int2*>(p);
+            return make_int2(static_cast<int>(f16x2_of(static_cast<uint32_t>(v.x), b)),
+                             static_cast<int>(f16x2_of(static_cast<uint32_t>(v.y), b)));
+        } else {
+            return f16x2_of(*reinterpret_cast<const uint32_t*>(p), b);
+        }
+    }
+};
+
 }  // namespace
 
 template <int RI>
 __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
-    static_assert(RI % 4 == 0 && RI <= 16, "rows per lane");
+    static_assert(RI % 2 == 0 && RI <= 16, "rows per lane");
     constexpr int CH = kLanes * RI;  // query rows per chunk
-    constexpr int NQ = RI / 4;       // 4-row quarters per lane
+    using Img = IntraImg<RI>;
+    using Elem = typename Img::Elem;
+    constexpr int NQ = Img::kPer;    // image elements per lane and code
     constexpr int NB = 8;            // steps per bias period (one rebase each)
     constexpr int NACC = RI + NB - 1;
-    __shared__ int2 img[kCodes * NQ * kLanes];
+    __shared__ Elem img[kCodes * NQ * kLanes];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int p = blockIdx.x * kWavesPerWG + wave;  // subject pair
@@ -101,15 +137,8 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
             const int code = t / (NQ * kLanes);
             const int u = t % (NQ * kLanes);
             const int qq = u / kLanes, ln = u % kLanes;
-            const int2 v = *reinterpret_cast<const int2*>(prof16 + static_cast<size_t>(code) * a.prof_stride + c0 +
-                                                          ln * RI + 4 * qq);
-            const uint32_t w0 = static_cast<uint32_t>(v.x), w1 = static_cast<uint32_t>(v.y);
-            const int b = a.bias - 2 * a.gap_extend;
-            const uint32_t o0 = f16_bits(static_cast<int16_t>(w0 & 0xffffu) - b) |
-                                (f16_bits(static_cast<int16_t>(w0 >> 16) - b) << 16);
-            const uint32_t o1 = f16_bits(static_cast<int16_t>(w1 & 0xffffu) - b) |
-                                (f16_bits(static_cast<int16_t>(w1 >> 16) - b) << 16);
-            img[t] = make_int2(static_cast<int>(o0), static_cast<int>(o1));
+            img[t] = Img::load(prof16 + static_cast<size_t>(code) * a.prof_stride + c0 + ln * RI + Img::kRows * qq,
+                               a.bias - 2 * a.gap_extend);
         }
         __syncthreads();
         if (!hasA && !hasB) continue;  // wave-uniform; the barriers above are shared
@@ -128,7 +157,8 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
         uint32_t rc = kPadPair;        // codes (A | B << 8) of this lane's current column
         uint32_t in_res = kPadPair, in_bh = 0, in_bf = 0, out_h = 0, out_f = 0;
         const int nsteps = L + kLanes - 1;
-        const int2* lrow = img + lane;
+        // LDS byte address of this lane's element of code 0
+        const uint32_t lrow = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(img + lane));
 
         for (int k0 = 0; k0 < nsteps; k0 += kLanes) {
             // lane-0 conveyors for steps k0 .. k0+63 (column k = step); the
@@ -167,22 +197,23 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
                         }
                         up_prev = h2_bits(as_h2(up_prev) - reb);
                     }
-                    const int2* pa = lrow + (rc & 0xffu) * (NQ * kLanes);
-                    const int2* pb = lrow + ((rc >> 8) & 0xffu) * (NQ * kLanes);
-                    int2 wa[NQ], wb[NQ];
+                    constexpr uint32_t kCodeBytes = NQ * kLanes * sizeof(Elem);
+                    typename Img::LElem* pa = reinterpret_cast<typename Img::LElem*>(
+                        static_cast<uintptr_t>(lrow + (rc & 0xffu) * kCodeBytes));
+                    typename Img::LElem* pb = reinterpret_cast<typename Img::LElem*>(
+                        static_cast<uintptr_t>(lrow + ((rc >> 8) & 0xffu) * kCodeBytes));
+                    Elem wa[NQ], wb[NQ];
 #pragma unroll
                     for (int qq = 0; qq < NQ; ++qq) {
-                        wa[qq] = pa[qq * kLanes];
-                        wb[qq] = pb[qq * kLanes];
+                        wa[qq] = __builtin_bit_cast(Elem, pa[qq * kLanes]);
+                        wb[qq] = __builtin_bit_cast(Elem, pb[qq * kLanes]);
                     }
                     // H_diag + S for every row first (from the previous
                     // column's H), so H is then updated in place
                     h2 T[RI];
 #pragma unroll
                     for (int r = 0; r < RI; ++r) {
-                        const int2 xa = wa[r >> 2], xb = wb[r >> 2];
-                        const uint32_t ua = static_cast<uint32_t>((r & 2) ? xa.y : xa.x);
-                        const uint32_t ub = static_cast<uint32_t>((r & 2) ? xb.y : xb.x);
+                        const uint32_t ua = Img::word(wa, r), ub = Img::word(wb, r);
                         // low half: subject A's S for row r, high half: subject B's
                         const h2 sc = as_h2(__builtin_amdgcn_perm(ub, ua, (r & 1) ? 0x07060302u : 0x05040100u));
                         T[r] = (r == 0 ? as_h2(up_prev) : H[r - 1]) + sc;
@@ -256,12 +287,17 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
 
 int intra_x2_rows_for(int qlen, int longest) {
     // chunks x steps x (cell pairs per lane-step + conveyor/hand-off overhead)
+    if (const char* e = std::getenv("SW_INTRA_X2_RI")) {  // tests: force a shape
+        const int ri = std::atoi(e);
+        if (ri == 4 || ri == 6 || ri == 8 || ri == 10 || ri == 12 || ri == 16) return ri;
+    }
     int best_ri = 16;
     double best_cost = 1e300;
-    for (int ri = 4; ri <= 16; ri += 4) {
+    for (int ri : {4, 6, 8, 10, 12, 16}) {
         const int chunk = kLanes * ri;
         const int nch = (qlen + chunk - 1) / chunk;
-        const double cost = static_cast<double>(nch) * (longest + kLanes - 1) * (ri * 4.5 + 18.0);
+        // SIMD cycles per lane-step: ri rows x 6.8 ops x 4.25 + ~80 of conveyor
+        const double cost = static_cast<double>(nch) * (longest + kLanes - 1) * (ri * 28.8 + 80.0);
         if (cost < best_cost) {
             best_cost = cost;
             best_ri = ri;
@@ -276,7 +312,9 @@ hipError_t launch_intra_x2(const IntraArgs& a, int ri, hipStream_t s) {
     const dim3 grid((npairs + kWavesPerWG - 1) / kWavesPerWG), block(kWavesPerWG * kLanes);
     switch (ri) {
         case 4: hipLaunchKernelGGL((sw_intra_x2<4>), grid, block, 0, s, a); break;
+        case 6: hipLaunchKernelGGL((sw_intra_x2<6>), grid, block, 0, s, a); break;
         case 8: hipLaunchKernelGGL((sw_intra_x2<8>), grid, block, 0, s, a); break;
+        case 10: hipLaunchKernelGGL((sw_intra_x2<10>), grid, block, 0, s, a); break;
         case 12: hipLaunchKernelGGL((sw_intra_x2<12>), grid, block, 0, s, a); break;
         case 16: hipLaunchKernelGGL((sw_intra_x2<16>), grid, block, 0, s, a); break;
         default: return hipErrorInvalidValue;

@@ -2,7 +2,7 @@
 # packed kernels, C2 bench (affine + reference scoring), C3 subset.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/v22
+O=gpurun_out/v24
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 120 --timeout-method thread > $O/parity.log 2>&1 && \
 timeout -k 10 300 python3 bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err

@@ -388,14 +388,17 @@ def test_wave_pair_kernel(sw, oracle, handle, monkeypatch, variant, width):
             assert want.max() > 2048  # the fp16 guard band is crossed
 
 
-@pytest.mark.parametrize("packed", ["1", "0"])
-def test_intra_two_subjects_per_wave(sw, oracle, handle, monkeypatch, packed):
+@pytest.mark.parametrize("packed,ri", [("1", ""), ("1", "6"), ("1", "10"), ("0", "")])
+def test_intra_two_subjects_per_wave(sw, oracle, handle, monkeypatch, packed, ri):
     """sw_intra_x2 (two long subjects per wave, packed fp16; SW_INTRA_X2=0:
-    int32 sw_intra only): rows per lane 4..16 (query lengths 40..2100, one to
-    several chunk passes), an odd number of long subjects, pairs of unequal
-    length, linear and affine scoring, and planted near-copies of the query
-    whose fp16 maxima cross 2048 (re-scored by sw_intra in list mode)."""
+    int32 sw_intra only): rows per lane 4..16 by the cost model (query lengths
+    40..2100, one to several chunk passes) or forced to the 2-row-element
+    shapes 6 and 10, an odd number of long subjects, pairs of unequal length,
+    linear and affine scoring, and planted near-copies of the query whose fp16
+    maxima cross 2048 (re-scored by sw_intra in list mode)."""
     monkeypatch.setenv("SW_INTRA_X2", packed)
+    if ri:
+        monkeypatch.setenv("SW_INTRA_X2_RI", ri)
     rng = np.random.default_rng(7)
     q0 = sw.synth.query(2100, shard=8)
     lens = rng.integers(70, 900, size=40)
@@ -405,8 +408,8 @@ def test_intra_two_subjects_per_wave(sw, oracle, handle, monkeypatch, packed):
     o = np.concatenate([[0], np.cumsum([len(x) for x in subs])]).astype(np.int64)
     db = sw.Database(handle, r, o, long_threshold=64)
     assert db.stats()["n_long"] == len(subs)
-    for qlen, mid, go, ge in [(40, 1, 12, 1), (375, 1, 12, 1), (700, 1, 11, 2), (1500, 0, 2, 2),
-                              (2100, 1, 12, 1), (260, 0, 8, 8)]:
+    for qlen, mid, go, ge in [(40, 1, 12, 1), (375, 1, 12, 1), (600, 1, 12, 1), (700, 1, 11, 2), (1100, 0, 2, 2),
+                              (1500, 0, 2, 2), (2100, 1, 12, 1), (260, 0, 8, 8)]:
         q = q0[:qlen]
         m = sw.capi.builtin_matrix(mid)
         got = db.scan(q, m, go, ge)
