@@ -794,9 +794,9 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                              qpad_coop > swk::inter_coop_rows() || qpad_list > (affine ? 64 : 96);
     const bool multi_intra = (ri && qpad_intra > swk::kLanes * ri) || (ri2 && qpad_intra2 > swk::kLanes * ri2);
     if ((multi_inter || multi_intra) && (rc = ensure_bnd(db, affine, intra_x2))) return rc;
-    if (intra_x2 && !db->d_lrescue) {
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lrescue), (db->nlong + 1) * sizeof(int32_t)));
-        db->device_bytes += (db->nlong + 1) * sizeof(int32_t);
+    if (intra_x2 && !db->d_lrescue) {  // two lists: [count, subjects...] x 2
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lrescue), 2 * (db->nlong + 1) * sizeof(int32_t)));
+        db->device_bytes += 2 * (db->nlong + 1) * sizeof(int32_t);
     }
 
     // fork: the side stream starts when the main stream reaches ev[0]
@@ -827,14 +827,26 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             x.sat_limit = 2048 - 2 * std::max(max_s, 1) - 26 * ge;
             for (int j = 0; j < 32; ++j) x.f16_step[j] = f16_pair(j * ge);
             x.f16_gog = f16_pair(go - ge);
-            x.rescue_count = db->d_lrescue;
-            x.rescue_list = db->d_lrescue + 1;
-            HIPCHECK(hipMemsetAsync(db->d_lrescue, 0, sizeof(int32_t), h->side));
+            int32_t* list1 = db->d_lrescue;                  // flagged by the fp16 pass
+            int32_t* list2 = db->d_lrescue + db->nlong + 1;  // ... and again by the int16 pass
+            x.rescue_count = list1;
+            x.rescue_list = list1 + 1;
+            HIPCHECK(hipMemsetAsync(list1, 0, sizeof(int32_t), h->side));
+            HIPCHECK(hipMemsetAsync(list2, 0, sizeof(int32_t), h->side));
             HIPCHECK(swk::launch_intra_x2(x, ri2, h->side));
-            // int32 re-scoring of the flagged subjects (device-side list)
-            ia.list_count = db->d_lrescue;
-            ia.subj_list = db->d_lrescue + 1;
-            h->launches += 2;
+            // the int16 form re-scores the fp16 pass's list (scores near
+            // 2048: high-scoring pairs, or linear scoring with cheap gaps,
+            // whose scores grow with the lengths) and flags near-32767 ones
+            swk::IntraArgs y = x;
+            y.list_count = list1;
+            y.subj_list = list1 + 1;
+            y.rescue_count = list2;
+            y.rescue_list = list2 + 1;
+            HIPCHECK(swk::launch_intra_x2_list16(y, ri2, h->side));
+            // int32 re-scoring of what is left (device-side list)
+            ia.list_count = list2;
+            ia.subj_list = list2 + 1;
+            h->launches += 3;
         }
         HIPCHECK(swk::launch_intra(ia, ri, affine, h->side));
         ++h->launches;

@@ -57,11 +57,54 @@ __device__ __forceinline__ uint32_t f16x2_of(uint32_t w, int b) {
     return f16_bits(static_cast<int16_t>(w & 0xffffu) - b) | (f16_bits(static_cast<int16_t>(w >> 16) - b) << 16);
 }
 
+typedef short s2 __attribute__((ext_vector_type(2)));
+
+// The cell's number format.  F16: exact integers up to 2048 (the default);
+// int16: up to 32767 (the rescue stage for subjects whose fp16 maximum nears
+// 2048, e.g. linear scoring with cheap gaps), wrapping add, no 3-input max.
+template <bool F16>
+struct IntraCell {
+    using V = h2;
+    static __device__ __forceinline__ V from(uint32_t x) { return __builtin_bit_cast(h2, x); }
+    static __device__ __forceinline__ uint32_t bits(V x) { return __builtin_bit_cast(uint32_t, x); }
+    static __device__ __forceinline__ V max2(V a, V b) { return __builtin_elementwise_maximum(a, b); }
+    static __device__ __forceinline__ V max3(V a, V b, V c) { return hmax3(a, b, c); }
+    static __device__ __forceinline__ uint32_t step(const IntraArgs& a, int j) { return a.f16_step[j]; }
+    static __device__ __forceinline__ uint32_t pair_of(int v) { const uint32_t b = f16_bits(v); return b | (b << 16); }
+    static __device__ __forceinline__ uint32_t convert(uint32_t w, int b) { return f16x2_of(w, b); }
+    static __device__ __forceinline__ int lo(V x) { return static_cast<int>(static_cast<float>(x.x)); }
+    static __device__ __forceinline__ int hi(V x) { return static_cast<int>(static_cast<float>(x.y)); }
+    static __device__ __forceinline__ bool flag(const IntraArgs& a, int b) { return b >= a.sat_limit; }
+};
+template <>
+struct IntraCell<false> {
+    using V = s2;
+    static __device__ __forceinline__ V from(uint32_t x) { return __builtin_bit_cast(s2, x); }
+    static __device__ __forceinline__ uint32_t bits(V x) { return __builtin_bit_cast(uint32_t, x); }
+    static __device__ __forceinline__ V max2(V a, V b) { return __builtin_elementwise_max(a, b); }
+    static __device__ __forceinline__ V max3(V a, V b, V c) { return max2(max2(a, b), c); }
+    static __device__ __forceinline__ uint32_t step(const IntraArgs& a, int j) { return pair_of(j * a.gap_extend); }
+    static __device__ __forceinline__ uint32_t pair_of(int v) {
+        const uint32_t b = static_cast<uint16_t>(v);
+        return b | (b << 16);
+    }
+    static __device__ __forceinline__ uint32_t convert(uint32_t w, int b) {
+        return static_cast<uint16_t>(static_cast<int16_t>(w & 0xffffu) - b) |
+               (static_cast<uint32_t>(static_cast<uint16_t>(static_cast<int16_t>(w >> 16) - b)) << 16);
+    }
+    static __device__ __forceinline__ int lo(V x) { return x.x; }
+    static __device__ __forceinline__ int hi(V x) { return x.y; }
+    // the int16 guard band (the biased values sit up to 26 ge above the true)
+    static __device__ __forceinline__ bool flag(const IntraArgs& a, int b) {
+        return b >= kSat16 - 26 * a.gap_extend || b < 0;
+    }
+};
+
 // A lane's rows of one code in the LDS image, 4 rows (int2) per element when
 // RI is a multiple of 4 (one ds_read_b64), 2 rows (one dword, ds_read_b32)
 // otherwise; either way lane l's element sits at l·size in a 64-element row,
 // so the reads are conflict-free whatever code each lane reads.
-template <int RI>
+template <int RI, bool F16>
 struct IntraImg {
     static constexpr int kRows = RI % 4 == 0 ? 4 : 2;
     using Elem = typename std::conditional<kRows == 4, int2, uint32_t>::type;
@@ -73,23 +116,29 @@ struct IntraImg {
     }
     // staging: the element of rows [4q, 4q + 4) or [2q, 2q + 2) of a lane
     static __device__ __forceinline__ Elem load(const int16_t* p, int b) {
+        using C = IntraCell<F16>;
         if constexpr (kRows == 4) {
             const int2 v = *reinterpret_cast<const int2*>(p);
-            return make_int2(static_cast<int>(f16x2_of(static_cast<uint32_t>(v.x), b)),
-                             static_cast<int>(f16x2_of(static_cast<uint32_t>(v.y), b)));
+            return make_int2(static_cast<int>(C::convert(static_cast<uint32_t>(v.x), b)),
+                             static_cast<int>(C::convert(static_cast<uint32_t>(v.y), b)));
         } else {
-            return f16x2_of(*reinterpret_cast<const uint32_t*>(p), b);
+            return C::convert(*reinterpret_cast<const uint32_t*>(p), b);
         }
     }
 };
 
 }  // namespace
 
-template <int RI>
+// LIST: the rescue stage — subject pairs come from the device-side list of
+// the subjects the fp16 pass flagged (a.subj_list / a.list_count); the grid
+// covers the longest possible list and surplus workgroups return at once.
+template <int RI, bool F16, bool LIST>
 __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
     static_assert(RI % 2 == 0 && RI <= 16, "rows per lane");
     constexpr int CH = kLanes * RI;  // query rows per chunk
-    using Img = IntraImg<RI>;
+    using C = IntraCell<F16>;
+    using V = typename C::V;
+    using Img = IntraImg<RI, F16>;
     using Elem = typename Img::Elem;
     constexpr int NQ = Img::kPer;    // image elements per lane and code
     constexpr int NB = 8;            // steps per bias period (one rebase each)
@@ -98,8 +147,16 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int p = blockIdx.x * kWavesPerWG + wave;  // subject pair
-    const int sa = 2 * p, sb = 2 * p + 1;
-    const bool hasA = sa < a.nsubj, hasB = sb < a.nsubj;
+    int sa = 2 * p, sb = 2 * p + 1;
+    bool hasA = sa < a.nsubj, hasB = sb < a.nsubj;
+    if constexpr (LIST) {
+        const int n = __builtin_amdgcn_readfirstlane(*a.list_count);
+        if (static_cast<int>(blockIdx.x) * 2 * kWavesPerWG >= n) return;  // workgroup-uniform
+        hasA = sa < n;
+        hasB = sb < n;
+        sa = hasA ? a.subj_list[sa] : 0;
+        sb = hasB ? a.subj_list[sb] : 0;
+    }
     const int LA = hasA ? a.subj_len[sa] : 0;
     const int LB = hasB ? a.subj_len[sb] : 0;
     const int L = max(LA, LB);  // = LA (length-sorted), kept general
@@ -110,8 +167,8 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
     uint32_t* bnd_h = reinterpret_cast<uint32_t*>(a.bnd_h) + (LA >= LB ? offA : (hasB ? a.subj_off[sb] : 0));
     uint32_t* bnd_f = reinterpret_cast<uint32_t*>(a.bnd_f) + (LA >= LB ? offA : (hasB ? a.subj_off[sb] : 0));
     const int16_t* prof16 = reinterpret_cast<const int16_t*>(a.prof);
-    auto step = [&](int j) { return as_h2(a.f16_step[j]); };  // (j ge, j ge)
-    const h2 gog = as_h2(a.f16_gog);
+    auto step = [&](int j) { return C::from(C::step(a, j)); };  // (j ge, j ge)
+    const V gog = C::from(C::pair_of(a.gap_open - a.gap_extend));
     // Biased cell (the two-strips kernel's, sw_inter_x2.hip): at step k,
     // row i of a lane holds H~ = H + (i + k % NB) ge, E' and F~ likewise, so
     // both gap extensions are the drift of the bias:
@@ -122,9 +179,9 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
     // drop NB ge), and what crosses lanes (the bottom row's H and F, one step
     // old) drops (RI - 1) ge (+ NB ge at a rebase step).  Maxima per
     // anti-diagonal i + k % NB, two cells per v_pk_maximum3_f16.
-    h2 acc[NACC];
+    V acc[NACC];
 #pragma unroll
-    for (int q = 0; q < NACC; ++q) acc[q] = as_h2(0u);
+    for (int q = 0; q < NACC; ++q) acc[q] = C::from(0u);
     constexpr uint32_t kPadPair = kPadCode | (kPadCode << 8);
 
     for (int c0 = 0; c0 < a.qpad; c0 += CH) {
@@ -144,16 +201,16 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
         if (!hasA && !hasB) continue;  // wave-uniform; the barriers above are shared
 
         // state of step -1 (column -1 - lane: H = 0), before step 0's rebase
-        h2 H[RI], E[RI];
+        V H[RI], E[RI];
 #pragma unroll
         for (int r = 0; r < RI; ++r) {
             H[r] = step(r + NB - 1);
-            E[r] = as_h2(0u);
+            E[r] = C::from(0u);
         }
         // bottom row (H, F) of this lane one step back, and H of the row above
         // at the previous column (row 0's diagonal): zeros of step -1
-        uint32_t hl = a.f16_step[RI + NB - 2], fl = a.f16_step[RI + NB - 1];
-        uint32_t up_prev = a.f16_step[NB - 2];
+        uint32_t hl = C::step(a, RI + NB - 2), fl = C::step(a, RI + NB - 1);
+        uint32_t up_prev = C::step(a, NB - 2);
         uint32_t rc = kPadPair;        // codes (A | B << 8) of this lane's current column
         uint32_t in_res = kPadPair, in_bh = 0, in_bf = 0, out_h = 0, out_f = 0;
         const int nsteps = L + kLanes - 1;
@@ -170,9 +227,8 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
                 const uint32_t cb = col < LB ? resB[col] : kPadCode;
                 in_res = ca | (cb << 8);
                 const int bz = RI - 2 + (col % NB) + ((col % NB) == 0 ? NB : 0);
-                const uint32_t zh = f16_bits(bz * a.gap_extend), zf = f16_bits((bz + 1) * a.gap_extend);
-                in_bh = (!first && col < L) ? bnd_h[col] : zh | (zh << 16);
-                in_bf = (!first && col < L) ? bnd_f[col] : zf | (zf << 16);
+                in_bh = (!first && col < L) ? bnd_h[col] : C::pair_of(bz * a.gap_extend);
+                in_bf = (!first && col < L) ? bnd_f[col] : C::pair_of((bz + 1) * a.gap_extend);
             }
             // whole bias periods (steps past nsteps run pad columns: harmless)
             const int mend = min(kLanes, nsteps - k0);
@@ -185,17 +241,17 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
                     const uint32_t sbf = __builtin_amdgcn_readlane(in_bf, m);
                     rc = shr1u(sres, rc);
                     // hand-off: the row above's bottom (H, F) from one step back
-                    const h2 adj = step(RI - 1 + (b == 0 ? NB : 0));
-                    const uint32_t up0 = h2_bits(as_h2(shr1u(sbh, hl)) - adj);
-                    h2 f = as_h2(shr1u(sbf, fl)) - adj;
+                    const V adj = step(RI - 1 + (b == 0 ? NB : 0));
+                    const uint32_t up0 = C::bits(C::from(shr1u(sbh, hl)) - adj);
+                    V f = C::from(shr1u(sbf, fl)) - adj;
                     if (b == 0) {  // rebase: the bias period restarts
-                        const h2 reb = step(NB);
+                        const V reb = step(NB);
 #pragma unroll
                         for (int r = 0; r < RI; ++r) {
                             H[r] = H[r] - reb;
                             E[r] = E[r] - reb;
                         }
-                        up_prev = h2_bits(as_h2(up_prev) - reb);
+                        up_prev = C::bits(C::from(up_prev) - reb);
                     }
                     constexpr uint32_t kCodeBytes = NQ * kLanes * sizeof(Elem);
                     typename Img::LElem* pa = reinterpret_cast<typename Img::LElem*>(
@@ -210,32 +266,32 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
                     }
                     // H_diag + S for every row first (from the previous
                     // column's H), so H is then updated in place
-                    h2 T[RI];
+                    V T[RI];
 #pragma unroll
                     for (int r = 0; r < RI; ++r) {
                         const uint32_t ua = Img::word(wa, r), ub = Img::word(wb, r);
                         // low half: subject A's S for row r, high half: subject B's
-                        const h2 sc = as_h2(__builtin_amdgcn_perm(ub, ua, (r & 1) ? 0x07060302u : 0x05040100u));
-                        T[r] = (r == 0 ? as_h2(up_prev) : H[r - 1]) + sc;
+                        const V sc = C::from(__builtin_amdgcn_perm(ub, ua, (r & 1) ? 0x07060302u : 0x05040100u));
+                        T[r] = (r == 0 ? C::from(up_prev) : H[r - 1]) + sc;
                     }
                     up_prev = up0;
 #pragma unroll
                     for (int r = 0; r < RI; ++r) {
-                        const h2 h = hmax3(E[r], f, T[r]);
-                        const h2 mm = h - gog;
-                        E[r] = __builtin_elementwise_maximum(E[r], mm);
-                        f = hmax3(f, mm, step(r + 1 + b));
-                        h2& ac = acc[r + b];
+                        const V h = C::max3(E[r], f, T[r]);
+                        const V mm = h - gog;
+                        E[r] = C::max2(E[r], mm);
+                        f = C::max3(f, mm, step(r + 1 + b));
+                        V& ac = acc[r + b];
                         if (b & 1) {
-                            if (r + 1 < RI) ac = hmax3(ac, h, H[r + 1]);  // H[r + 1]: cell (r + 1, step - 1)
-                            else ac = __builtin_elementwise_maximum(ac, h);
+                            if (r + 1 < RI) ac = C::max3(ac, h, H[r + 1]);  // H[r + 1]: cell (r + 1, step - 1)
+                            else ac = C::max2(ac, h);
                         } else if (r == 0) {  // the even steps' other rows are partners above
-                            ac = __builtin_elementwise_maximum(ac, h);
+                            ac = C::max2(ac, h);
                         }
                         H[r] = h;
                     }
-                    hl = h2_bits(H[RI - 1]);
-                    fl = h2_bits(f);
+                    hl = C::bits(H[RI - 1]);
+                    fl = C::bits(f);
                     if (!last) {
                         // lane 63 finished column k - 63: collect it for the next pass
                         const int oc = k0 + m - (kLanes - 1);
@@ -263,24 +319,24 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
         }
     }
     // the lane's maximum (unbiased), then the wave's
-    h2 best = acc[0];
+    V best = acc[0];
 #pragma unroll
-    for (int q = 1; q < NACC; ++q) best = __builtin_elementwise_maximum(best, acc[q] - step(q));
+    for (int q = 1; q < NACC; ++q) best = C::max2(best, acc[q] - step(q));
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-        const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(h2_bits(best)), off));
-        best = __builtin_elementwise_maximum(best, as_h2(o));
+        const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(C::bits(best)), off));
+        best = C::max2(best, C::from(o));
     }
     if (lane == 0) {
-        const int ba = static_cast<int>(static_cast<float>(best.x));
-        const int bb = static_cast<int>(static_cast<float>(best.y));
+        const int ba = C::lo(best);
+        const int bb = C::hi(best);
         if (hasA) {
             a.scores[a.subj_id[sa]] = ba;
-            if (a.rescue_list && ba >= a.sat_limit) a.rescue_list[atomicAdd(a.rescue_count, 1)] = sa;
+            if (a.rescue_list && C::flag(a, ba)) a.rescue_list[atomicAdd(a.rescue_count, 1)] = sa;
         }
         if (hasB) {
             a.scores[a.subj_id[sb]] = bb;
-            if (a.rescue_list && bb >= a.sat_limit) a.rescue_list[atomicAdd(a.rescue_count, 1)] = sb;
+            if (a.rescue_list && C::flag(a, bb)) a.rescue_list[atomicAdd(a.rescue_count, 1)] = sb;
         }
     }
 }
@@ -306,20 +362,33 @@ int intra_x2_rows_for(int qlen, int longest) {
     return best_ri;
 }
 
-hipError_t launch_intra_x2(const IntraArgs& a, int ri, hipStream_t s) {
-    if (a.nsubj <= 0 || a.qpad <= 0) return hipSuccess;
+template <bool F16, bool LIST>
+static hipError_t launch_intra_x2_t(const IntraArgs& a, int ri, hipStream_t s) {
     const int npairs = (a.nsubj + 1) / 2;
     const dim3 grid((npairs + kWavesPerWG - 1) / kWavesPerWG), block(kWavesPerWG * kLanes);
     switch (ri) {
-        case 4: hipLaunchKernelGGL((sw_intra_x2<4>), grid, block, 0, s, a); break;
-        case 6: hipLaunchKernelGGL((sw_intra_x2<6>), grid, block, 0, s, a); break;
-        case 8: hipLaunchKernelGGL((sw_intra_x2<8>), grid, block, 0, s, a); break;
-        case 10: hipLaunchKernelGGL((sw_intra_x2<10>), grid, block, 0, s, a); break;
-        case 12: hipLaunchKernelGGL((sw_intra_x2<12>), grid, block, 0, s, a); break;
-        case 16: hipLaunchKernelGGL((sw_intra_x2<16>), grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((sw_intra_x2<4, F16, LIST>), grid, block, 0, s, a); break;
+        case 6: hipLaunchKernelGGL((sw_intra_x2<6, F16, LIST>), grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((sw_intra_x2<8, F16, LIST>), grid, block, 0, s, a); break;
+        case 10: hipLaunchKernelGGL((sw_intra_x2<10, F16, LIST>), grid, block, 0, s, a); break;
+        case 12: hipLaunchKernelGGL((sw_intra_x2<12, F16, LIST>), grid, block, 0, s, a); break;
+        case 16: hipLaunchKernelGGL((sw_intra_x2<16, F16, LIST>), grid, block, 0, s, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+hipError_t launch_intra_x2(const IntraArgs& a, int ri, hipStream_t s) {
+    if (a.nsubj <= 0 || a.qpad <= 0) return hipSuccess;
+    return launch_intra_x2_t<true, false>(a, ri, s);
+}
+
+// The int16 form over the device-side list of subjects the fp16 pass flagged
+// (a.subj_list / a.list_count); it flags its own near-32767 subjects into
+// a.rescue_list for the int32 sw_intra.
+hipError_t launch_intra_x2_list16(const IntraArgs& a, int ri, hipStream_t s) {
+    if (a.nsubj <= 0 || a.qpad <= 0) return hipSuccess;
+    return launch_intra_x2_t<false, true>(a, ri, s);
 }
 
 }  // namespace swk

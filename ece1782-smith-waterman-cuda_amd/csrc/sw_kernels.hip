@@ -643,7 +643,7 @@ template <int RI, bool AFFINE>
 __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kProfileRows * intra_stride(RI)];
     if (a.list_count) {
-        // list mode: a fixed grid re-scores the subjects a packed kernel flagged
+        // list mode: re-scores the subjects a packed kernel flagged
         const int n = __builtin_amdgcn_readfirstlane(*a.list_count);
         for (int i = blockIdx.x; i < n; i += gridDim.x) intra_subject<RI, AFFINE>(a, a.subj_list[i], lds);
         return;
@@ -948,8 +948,9 @@ hipError_t launch_inter(const InterArgs& a, bool affine, int x2_ok, hipStream_t 
 
 template <int RI>
 static void launch_intra_ri(const IntraArgs& a, bool affine, hipStream_t s) {
-    // list mode: 256 workgroups walk the device-side list (usually empty)
-    const dim3 grid(a.list_count ? std::min(a.nsubj, 256) : a.nsubj);
+    // list mode: one workgroup per possible entry (surplus ones return at
+    // once), so a long list runs as wide as a full scan
+    const dim3 grid(a.nsubj);
     if (affine)
         hipLaunchKernelGGL((sw_intra<RI, true>), grid, dim3(kLanes), 0, s, a);
     else

@@ -417,3 +417,28 @@ def test_intra_two_subjects_per_wave(sw, oracle, handle, monkeypatch, packed, ri
         assert np.array_equal(got, want), (qlen, mid, go, ge, np.nonzero(got != want)[0][:10])
         if qlen >= 1500:
             assert want.max() > 2048
+
+
+def test_intra_rescue_chain_fp16_int16_int32(sw, oracle, handle):
+    """The intra rescue chain end to end: sw_intra_x2 (fp16) flags subjects
+    near 2048 into list 1, its int16 form re-scores list 1 and flags those
+    near 32767 into list 2, and int32 sw_intra re-scores list 2.  Cheap linear
+    gaps (the reference scoring, BLOSUM50, 2 per gap) make random 5k-aa pairs score
+    in the thousands; a planted copy of the 6,500-aa query scores above 32767;
+    ordinary subjects sit next to both in the same pairs."""
+    rng = np.random.default_rng(11)
+    q = sw.synth.query(6500, shard=21)
+    lens = rng.integers(1500, 5500, size=17)
+    subs = [sw.synth.query(int(n), shard=300 + k) for k, n in enumerate(lens)]
+    subs.insert(5, q.copy())
+    subs.insert(9, q[:3000].copy())
+    r = np.concatenate(subs).astype(np.uint8)
+    o = np.concatenate([[0], np.cumsum([len(x) for x in subs])]).astype(np.int64)
+    db = sw.Database(handle, r, o, long_threshold=64)
+    m = sw.capi.builtin_matrix(0)
+    for go, ge in [(2, 2), (12, 1)]:
+        got = db.scan(q, m, go, ge)
+        want = oracle.scan(q, r, o, mat=m, gap_open=go, gap_extend=ge)
+        assert np.array_equal(got, want), (go, ge, np.nonzero(got != want)[0][:10])
+        assert want.max() > 32767
+        assert ((want > 2048) & (want < 32000)).sum() >= (2 if ge == 2 else 1)
