@@ -229,7 +229,16 @@ struct sw_db {
     // 16-bit kernels' flagged blocks (list A), and the fp16 chain's second
     // stage's (list B)
     int32_t* d_rescue = nullptr;
-    int32_t* d_lrescue = nullptr;        // [count, subjects...] flagged by sw_intra_x2
+    int32_t* d_lrescue = nullptr;        // [count, subjects...] x 2: the intra rescue chain's lists
+    // the intra chain's order (scan_impl): the fp16 pass's flagged count read
+    // back after the scan (pinned, event-gated), and per scoring the shortest
+    // query seen to flag over half of the long subjects
+    int32_t* h_lcount = nullptr;
+    hipEvent_t lcount_ev = nullptr;
+    bool lcount_pending = false;
+    uint64_t lcount_key = 0;
+    int32_t lcount_qlen = 0;
+    std::vector<std::pair<uint64_t, int32_t>> i16_first;
     uint64_t* h_trace = nullptr;         // SW_TRACE_FILE: host-mapped block timeline
     std::vector<uint32_t> h_blk_groups;  // block widths (16-column groups), widest first
     std::vector<int64_t> h_blk_res;      // unpadded residues per block
@@ -297,6 +306,8 @@ void free_dev(sw_db* db) {
     db->d_bnd_h = nullptr; db->d_bnd_f = nullptr; db->d_rescue = nullptr; db->d_lres = nullptr; db->d_loff = nullptr;
     db->d_llen = nullptr; db->d_lid = nullptr; db->d_lbnd_h = nullptr; db->d_lbnd_f = nullptr;
     db->d_lrescue = nullptr;
+    db->lcount_pending = false;
+    db->i16_first.clear();  // the long partition may change
     db->device_bytes = 0;
     db->built = false;
 }
@@ -744,6 +755,37 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     const char* ix = std::getenv("SW_INTRA_X2");
     const bool intra_x2 = db->nlong && x2_ok >= 1 && !(ix && ix[0] == '0');
     const int ri2 = intra_x2 ? swk::intra_x2_rows_for(qlen, db->long_max) : 0;
+    // The intra chain's order.  Linear scoring with cheap gaps makes random
+    // pairs' scores grow with their lengths, so on long subjects the fp16
+    // pass can flag nearly everything (C5 with the reference's BLOSUM50 / 2:
+    // all of it) and its time is wasted.  Once a scan with the same scoring
+    // has flagged over half of the long subjects at a query no longer than
+    // this one, the int16 form runs first, over all of them.
+    // SW_INTRA_I16_FIRST=0 / 1: never / always.
+    uint64_t skey = 1469598103934665603ull;  // FNV-1a of the scoring
+    for (int k = 0; k < 625; ++k) skey = (skey ^ static_cast<uint8_t>(mat[k])) * 1099511628211ull;
+    skey = ((skey ^ static_cast<uint32_t>(go)) * 1099511628211ull ^ static_cast<uint32_t>(ge)) * 1099511628211ull;
+    if (db->lcount_pending && hipEventQuery(db->lcount_ev) == hipSuccess) {
+        db->lcount_pending = false;
+        if (2 * static_cast<int64_t>(*db->h_lcount) > db->nlong) {
+            bool seen = false;
+            for (auto& e : db->i16_first)
+                if (e.first == db->lcount_key) {
+                    e.second = std::min(e.second, db->lcount_qlen);
+                    seen = true;
+                }
+            if (!seen) db->i16_first.emplace_back(db->lcount_key, db->lcount_qlen);
+        }
+    }
+    const char* i16f = std::getenv("SW_INTRA_I16_FIRST");
+    bool intra_i16_first = false;
+    if (i16f && (i16f[0] == '0' || i16f[0] == '1')) {
+        intra_i16_first = i16f[0] == '1';
+    } else {
+        for (const auto& e : db->i16_first)
+            if (e.first == skey && e.second <= qlen) intra_i16_first = true;
+    }
+    intra_i16_first = intra_i16_first && intra_x2;
     const int32_t qpad_intra2 = ri2 ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri2)) : 0;
     // Empty query: every score is 0 (the reference's kernel leaves maxScore 0).
     if (qlen == 0) {
@@ -829,28 +871,49 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             x.f16_gog = f16_pair(go - ge);
             int32_t* list1 = db->d_lrescue;                  // flagged by the fp16 pass
             int32_t* list2 = db->d_lrescue + db->nlong + 1;  // ... and again by the int16 pass
-            x.rescue_count = list1;
-            x.rescue_list = list1 + 1;
             HIPCHECK(hipMemsetAsync(list1, 0, sizeof(int32_t), h->side));
             HIPCHECK(hipMemsetAsync(list2, 0, sizeof(int32_t), h->side));
-            HIPCHECK(swk::launch_intra_x2(x, ri2, h->side));
-            // the int16 form re-scores the fp16 pass's list (scores near
-            // 2048: high-scoring pairs, or linear scoring with cheap gaps,
-            // whose scores grow with the lengths) and flags near-32767 ones
-            swk::IntraArgs y = x;
-            y.list_count = list1;
-            y.subj_list = list1 + 1;
-            y.rescue_count = list2;
-            y.rescue_list = list2 + 1;
-            HIPCHECK(swk::launch_intra_x2_list16(y, ri2, h->side));
+            if (intra_i16_first) {
+                // the int16 form over every long subject, flagging near-32767 ones
+                x.rescue_count = list2;
+                x.rescue_list = list2 + 1;
+                HIPCHECK(swk::launch_intra_x2_int16(x, ri2, h->side));
+                h->launches += 1;
+            } else {
+                x.rescue_count = list1;
+                x.rescue_list = list1 + 1;
+                HIPCHECK(swk::launch_intra_x2(x, ri2, h->side));
+                // the fp16 pass's flagged count, read by a later scan
+                if (!db->h_lcount) {
+                    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&db->h_lcount), sizeof(int32_t),
+                                           hipHostMallocDefault));
+                    HIPCHECK(hipEventCreateWithFlags(&db->lcount_ev, hipEventDisableTiming));
+                }
+                if (!db->lcount_pending) {
+                    HIPCHECK(hipMemcpyAsync(db->h_lcount, list1, sizeof(int32_t), hipMemcpyDeviceToHost, h->side));
+                    HIPCHECK(hipEventRecord(db->lcount_ev, h->side));
+                    db->lcount_pending = true;
+                    db->lcount_key = skey;
+                    db->lcount_qlen = qlen;
+                }
+                // the int16 form re-scores the fp16 pass's list (scores near
+                // 2048: high-scoring pairs, or linear scoring with cheap gaps)
+                // and flags near-32767 ones
+                swk::IntraArgs y = x;
+                y.list_count = list1;
+                y.subj_list = list1 + 1;
+                y.rescue_count = list2;
+                y.rescue_list = list2 + 1;
+                HIPCHECK(swk::launch_intra_x2_list16(y, ri2, h->side));
+                h->launches += 2;
+            }
             // int32 re-scoring of what is left (device-side list)
             ia.list_count = list2;
             ia.subj_list = list2 + 1;
-            h->launches += 3;
         }
         HIPCHECK(swk::launch_intra(ia, ri, affine, h->side));
         ++h->launches;
-        h->last_intra = intra_x2 ? "sw_intra_x2<" + std::to_string(ri2) + ">"
+        h->last_intra = intra_x2 ? "sw_intra_x2<" + std::to_string(ri2) + (intra_i16_first ? ",int16>" : ">")
                                  : "sw_intra<" + std::to_string(ri) + (affine ? ",affine>" : ",linear>");
         h->had_intra = true;
     }
@@ -1306,6 +1369,8 @@ int sw_db_free(sw_db* db) {
             }
         (void)hipHostFree(db->h_trace);
     }
+    if (db->h_lcount) (void)hipHostFree(db->h_lcount);
+    if (db->lcount_ev) (void)hipEventDestroy(db->lcount_ev);
     free_dev(db);
     delete db;
     return SW_OK;

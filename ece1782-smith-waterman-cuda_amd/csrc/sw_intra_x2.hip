@@ -35,8 +35,6 @@ namespace {
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ h2 as_h2(uint32_t x) { return __builtin_bit_cast(h2, x); }
-__device__ __forceinline__ uint32_t h2_bits(h2 x) { return __builtin_bit_cast(uint32_t, x); }
 __device__ __forceinline__ h2 hmax3(h2 a, h2 b, h2 c) {
     return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
@@ -389,6 +387,11 @@ hipError_t launch_intra_x2(const IntraArgs& a, int ri, hipStream_t s) {
 hipError_t launch_intra_x2_list16(const IntraArgs& a, int ri, hipStream_t s) {
     if (a.nsubj <= 0 || a.qpad <= 0) return hipSuccess;
     return launch_intra_x2_t<false, true>(a, ri, s);
+}
+
+hipError_t launch_intra_x2_int16(const IntraArgs& a, int ri, hipStream_t s) {
+    if (a.nsubj <= 0 || a.qpad <= 0) return hipSuccess;
+    return launch_intra_x2_t<false, false>(a, ri, s);
 }
 
 }  // namespace swk

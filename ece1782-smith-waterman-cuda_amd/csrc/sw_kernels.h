@@ -173,6 +173,8 @@ hipError_t launch_intra(const IntraArgs& a, int ri, bool affine, hipStream_t s);
 hipError_t launch_intra_x2(const IntraArgs& a, int ri, hipStream_t s);
 // its int16 form over the device-side list a.subj_list / a.list_count
 hipError_t launch_intra_x2_list16(const IntraArgs& a, int ri, hipStream_t s);
+// ... and over every subject (the chain's first stage when fp16 would flag most)
+hipError_t launch_intra_x2_int16(const IntraArgs& a, int ri, hipStream_t s);
 int intra_x2_rows_for(int qlen, int longest);
 
 // Traceback of chosen hits (sw_align.hip), linear gap, cpu.cpp's tie rules.

@@ -1,8 +1,7 @@
-# v25: int16 list stage in the intra rescue chain (fp16 -> int16 -> int32):
-# full GPU suite, C5 and C2 bench lines.
+# Full GPU suite, C5 and C2 bench lines into gpurun_out/$RUN (default v25).
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/v25
+O=gpurun_out/${RUN:-v25}
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > $O/parity.log 2>&1 && \
 timeout -k 10 300 python3 bench.py --config c5 --no-cpu-baseline > $O/c5.json 2> $O/c5.err && \

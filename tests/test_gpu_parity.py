@@ -419,13 +419,19 @@ def test_intra_two_subjects_per_wave(sw, oracle, handle, monkeypatch, packed, ri
             assert want.max() > 2048
 
 
-def test_intra_rescue_chain_fp16_int16_int32(sw, oracle, handle):
+@pytest.mark.parametrize("order", ["", "0", "1"])
+def test_intra_rescue_chain_fp16_int16_int32(sw, oracle, handle, monkeypatch, order):
     """The intra rescue chain end to end: sw_intra_x2 (fp16) flags subjects
     near 2048 into list 1, its int16 form re-scores list 1 and flags those
     near 32767 into list 2, and int32 sw_intra re-scores list 2.  Cheap linear
     gaps (the reference scoring, BLOSUM50, 2 per gap) make random 5k-aa pairs score
     in the thousands; a planted copy of the 6,500-aa query scores above 32767;
-    ordinary subjects sit next to both in the same pairs."""
+    ordinary subjects sit next to both in the same pairs.  The chain's order
+    (SW_INTRA_I16_FIRST): adaptive (int16 first once a scan with the same
+    scoring flagged over half of the long subjects at a query no longer than
+    this one), never, always."""
+    if order:
+        monkeypatch.setenv("SW_INTRA_I16_FIRST", order)
     rng = np.random.default_rng(11)
     q = sw.synth.query(6500, shard=21)
     lens = rng.integers(1500, 5500, size=17)
@@ -436,9 +442,17 @@ def test_intra_rescue_chain_fp16_int16_int32(sw, oracle, handle):
     o = np.concatenate([[0], np.cumsum([len(x) for x in subs])]).astype(np.int64)
     db = sw.Database(handle, r, o, long_threshold=64)
     m = sw.capi.builtin_matrix(0)
-    for go, ge in [(2, 2), (12, 1)]:
-        got = db.scan(q, m, go, ge)
+    for rnd, (go, ge) in enumerate([(2, 2), (12, 1), (2, 2), (12, 1)]):
         want = oracle.scan(q, r, o, mat=m, gap_open=go, gap_extend=ge)
-        assert np.array_equal(got, want), (go, ge, np.nonzero(got != want)[0][:10])
+        for qq in (q, q[:5000]):
+            w = want if len(qq) == len(q) else oracle.scan(qq, r, o, mat=m, gap_open=go, gap_extend=ge)
+            got = db.scan(qq, m, go, ge)
+            assert np.array_equal(got, w), (order, go, ge, len(qq), np.nonzero(got != w)[0][:10])
+            # adaptive: BLOSUM50 / 2 flags nearly all of them, so its second
+            # round runs int16 first; 12 / 1 flags only the planted copies
+            i16 = handle.last_intra_kernel().endswith(",int16>")
+            assert i16 == (order == "1" or (order == "" and rnd == 2)), (order, rnd, len(qq))
+            if len(qq) == 5000:
+                assert (w >= 1966).sum() * 2 > len(subs) or ge == 1
         assert want.max() > 32767
         assert ((want > 2048) & (want < 32000)).sum() >= (2 if ge == 2 else 1)
