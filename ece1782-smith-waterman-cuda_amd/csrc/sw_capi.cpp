@@ -844,8 +844,13 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // fork: the side stream starts when the main stream reaches ev[0]
     HIPCHECK(hipEventRecord(h->ev[0], h->stream));
     h->last_intra = "none";
+    // the long subjects' stream: a side stream, concurrent with the inter
+    // kernels (SW_INTRA_SERIAL=1: the main stream, before them — to measure
+    // what the concurrency costs the inter kernel)
+    const char* iser = std::getenv("SW_INTRA_SERIAL");
+    hipStream_t is = (iser && iser[0] == '1') ? h->stream : h->side;
     if (db->nlong) {
-        HIPCHECK(hipStreamWaitEvent(h->side, h->ev[0], 0));
+        HIPCHECK(hipStreamWaitEvent(is, h->ev[0], 0));
         swk::IntraArgs ia{};
         ia.residues = db->d_lres;
         ia.subj_off = db->d_loff;
@@ -871,18 +876,18 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             x.f16_gog = f16_pair(go - ge);
             int32_t* list1 = db->d_lrescue;                  // flagged by the fp16 pass
             int32_t* list2 = db->d_lrescue + db->nlong + 1;  // ... and again by the int16 pass
-            HIPCHECK(hipMemsetAsync(list1, 0, sizeof(int32_t), h->side));
-            HIPCHECK(hipMemsetAsync(list2, 0, sizeof(int32_t), h->side));
+            HIPCHECK(hipMemsetAsync(list1, 0, sizeof(int32_t), is));
+            HIPCHECK(hipMemsetAsync(list2, 0, sizeof(int32_t), is));
             if (intra_i16_first) {
                 // the int16 form over every long subject, flagging near-32767 ones
                 x.rescue_count = list2;
                 x.rescue_list = list2 + 1;
-                HIPCHECK(swk::launch_intra_x2_int16(x, ri2, h->side));
+                HIPCHECK(swk::launch_intra_x2_int16(x, ri2, is));
                 h->launches += 1;
             } else {
                 x.rescue_count = list1;
                 x.rescue_list = list1 + 1;
-                HIPCHECK(swk::launch_intra_x2(x, ri2, h->side));
+                HIPCHECK(swk::launch_intra_x2(x, ri2, is));
                 // the fp16 pass's flagged count, read by a later scan
                 if (!db->h_lcount) {
                     HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&db->h_lcount), sizeof(int32_t),
@@ -890,8 +895,8 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                     HIPCHECK(hipEventCreateWithFlags(&db->lcount_ev, hipEventDisableTiming));
                 }
                 if (!db->lcount_pending) {
-                    HIPCHECK(hipMemcpyAsync(db->h_lcount, list1, sizeof(int32_t), hipMemcpyDeviceToHost, h->side));
-                    HIPCHECK(hipEventRecord(db->lcount_ev, h->side));
+                    HIPCHECK(hipMemcpyAsync(db->h_lcount, list1, sizeof(int32_t), hipMemcpyDeviceToHost, is));
+                    HIPCHECK(hipEventRecord(db->lcount_ev, is));
                     db->lcount_pending = true;
                     db->lcount_key = skey;
                     db->lcount_qlen = qlen;
@@ -904,20 +909,20 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                 y.subj_list = list1 + 1;
                 y.rescue_count = list2;
                 y.rescue_list = list2 + 1;
-                HIPCHECK(swk::launch_intra_x2_list16(y, ri2, h->side));
+                HIPCHECK(swk::launch_intra_x2_list16(y, ri2, is));
                 h->launches += 2;
             }
             // int32 re-scoring of what is left (device-side list)
             ia.list_count = list2;
             ia.subj_list = list2 + 1;
         }
-        HIPCHECK(swk::launch_intra(ia, ri, affine, h->side));
+        HIPCHECK(swk::launch_intra(ia, ri, affine, is));
         ++h->launches;
         h->last_intra = intra_x2 ? "sw_intra_x2<" + std::to_string(ri2) + (intra_i16_first ? ",int16>" : ">")
                                  : "sw_intra<" + std::to_string(ri) + (affine ? ",affine>" : ",linear>");
         h->had_intra = true;
     }
-    HIPCHECK(hipEventRecord(h->ev[1], db->nlong ? h->side : h->stream));
+    HIPCHECK(hipEventRecord(h->ev[1], db->nlong ? is : h->stream));
     if (db->nblocks) {
         swk::InterArgs a{};
         a.residues = db->d_res;

@@ -3,66 +3,193 @@
 //
 // Hits are ordered by score descending, then global id ascending; both fold
 // into one int64 key (score << 32 | (2^31 - 1 - id)) sorted descending.
-// Each workgroup sorts a chunk of CH keys in LDS (bitonic) and keeps its
-// best K; the stage repeats on the survivors until a single chunk remains.
-// No host synchronisation: every stage's size is known from n and K.
-// CH = 2048 (256 threads) when K <= 1024: ~n/2048 workgroups fill the chip
-// and the network is 66 passes deep; 8192-key chunks (91 passes, 70
-// workgroups for 570k scores) took 2 x 92 us per step on C2.
+// Radix select: a workgroup holds a chunk of 16,384 keys in registers (1,024
+// threads x 16), finds its k-th largest key with 8-bit digit histograms in
+// LDS — starting at the highest bit where the chunk's keys differ, stopping
+// as soon as the keys left at the chosen digit are exactly the ones still
+// needed — and writes the k keys at or above it (equal keys, i.e. padding,
+// by ticket).  The stage repeats on the survivors (chunks x k keys) until one
+// chunk remains, whose workgroup also sorts its k keys (bitonic in LDS).  No
+// host synchronisation: every stage's size is known from n and k.  For C2
+// (570k scores, k = 100) that is 2 launches of ~4 passes each, where the
+// previous bitonic sort of 2,048-key chunks took 3 launches x 39 us.
 #include "sw_kernels.h"
 
 namespace swk {
 
-constexpr int kTopkChunk = 8192;   // largest chunk: keys per workgroup (64 KiB of LDS)
+constexpr int kTopkThreads = 1024;
+constexpr int kTopkPer = 16;                             // keys per thread
+constexpr int kTopkChunk = kTopkThreads * kTopkPer;      // keys per workgroup
+constexpr int kTopkMaxK = 4096;
 constexpr int64_t kKeyPad = INT64_MIN;
 
 __device__ __forceinline__ int64_t make_key(int32_t score, int64_t id) {
     return (static_cast<int64_t>(score) << 32) | ((int64_t{1} << 31) - 1 - id);
 }
+// order-preserving map of the signed keys onto uint64 (pad -> 0)
+__device__ __forceinline__ uint64_t key_ord(int64_t k) { return static_cast<uint64_t>(k) ^ (uint64_t{1} << 63); }
+__device__ __forceinline__ int64_t key_of(uint64_t u) { return static_cast<int64_t>(u ^ (uint64_t{1} << 63)); }
 
-// in_scores != nullptr: stage 0 builds keys from scores (ids = id_base + i);
-// otherwise keys come from in_keys.
-template <int CH, int NT>
-__global__ __launch_bounds__(NT) void sw_topk_stage(const int32_t* __restrict__ in_scores,
-                                                   const int64_t* __restrict__ in_keys, int64_t n, int64_t id_base,
-                                                   int k, int64_t* __restrict__ out) {
-    __shared__ int64_t key[CH];
-    const int64_t start = static_cast<int64_t>(blockIdx.x) * CH;
-    for (int i = threadIdx.x; i < CH; i += NT) {
-        const int64_t g = start + i;
-        int64_t v = kKeyPad;
-        if (g < n) v = in_scores ? make_key(in_scores[g], id_base + g) : in_keys[g];
-        key[i] = v;
-    }
-    __syncthreads();
-    // bitonic sort, descending
-    for (int size = 2; size <= CH; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = threadIdx.x; i < CH / 2; i += NT) {
-                const int lo = 2 * i - (i & (stride - 1));
-                const int hi = lo + stride;
-                const bool desc = ((lo & size) == 0);
-                const int64_t a = key[lo], b = key[hi];
-                if ((a < b) == desc) {
-                    key[lo] = b;
-                    key[hi] = a;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    for (int i = threadIdx.x; i < k; i += NT) out[static_cast<int64_t>(blockIdx.x) * k + i] = key[i];
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+    const int lo = __shfl_xor(static_cast<int>(v & 0xffffffffu), m);
+    const int hi = __shfl_xor(static_cast<int>(v >> 32), m);
+    return (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo);
 }
 
-static int chunk_for(int k) { return k <= 1024 ? 2048 : kTopkChunk; }
+// in_scores != nullptr: keys are built from scores (ids = id_base + i);
+// otherwise they come from in_keys.  FINAL: one workgroup, sorted output.
+template <bool FINAL>
+__global__ __launch_bounds__(kTopkThreads) void sw_topk_select(const int32_t* __restrict__ in_scores,
+                                                              const int64_t* __restrict__ in_keys, int64_t n,
+                                                              int64_t id_base, int k, int64_t* __restrict__ out) {
+    __shared__ uint32_t hist[256];
+    __shared__ uint64_t red[2][kTopkThreads / 64];
+    __shared__ int ctl[5];  // digit, keys above it, keys at it, output slot, tie ticket
+    __shared__ int64_t sorted[FINAL ? kTopkMaxK : 1];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t start = static_cast<int64_t>(blockIdx.x) * kTopkChunk;
+    const int m = static_cast<int>(min(static_cast<int64_t>(kTopkChunk), n - start));  // keys in this chunk
+    uint64_t u[kTopkPer];
+    uint64_t all_and = ~uint64_t{0}, all_or = 0;
+#pragma unroll
+    for (int j = 0; j < kTopkPer; ++j) {
+        const int i = j * kTopkThreads + t;
+        u[j] = 0;
+        if (i < m) {
+            const int64_t g = start + i;
+            u[j] = key_ord(in_scores ? make_key(in_scores[g], id_base + g) : in_keys[g]);
+            all_and &= u[j];
+            all_or |= u[j];
+        }
+    }
+    if (t == 0) {
+        ctl[3] = 0;
+        ctl[4] = 0;
+    }
+    auto emit = [&](uint64_t v) {
+        const int pos = atomicAdd(&ctl[3], 1);
+        if (FINAL) sorted[pos] = key_of(v);
+        else out[static_cast<int64_t>(blockIdx.x) * k + pos] = key_of(v);
+    };
+    if (m <= k) {  // workgroup-uniform: every key survives
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kTopkPer; ++j)
+            if (j * kTopkThreads + t < m) emit(u[j]);
+    } else {
+        // bits above the highest one where the chunk's keys differ are common
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            all_and &= shfl_xor64(all_and, off);
+            all_or |= shfl_xor64(all_or, off);
+        }
+        if (lane == 0) {
+            red[0][wave] = all_and;
+            red[1][wave] = all_or;
+        }
+        __syncthreads();
+        all_and = red[0][0];
+        all_or = red[1][0];
+        for (int w = 1; w < kTopkThreads / 64; ++w) {
+            all_and &= red[0][w];
+            all_or |= red[1][w];
+        }
+        const uint64_t diff = all_and ^ all_or;
+        int remaining = k;  // keys still to take among those matching prefix
+        uint64_t mask = ~uint64_t{0}, prefix = all_and;
+        if (diff) {
+            const int top = 63 - __clzll(static_cast<long long>(diff));
+            mask = top == 63 ? 0 : ~((uint64_t{1} << (top + 1)) - 1);
+            prefix = all_and & mask;
+            for (int s = top - 7;; s -= 8) {
+                const int sh = max(s, 0);
+                const uint32_t dmask = (1u << (s >= 0 ? 8 : 8 + s)) - 1;
+                if (t < 256) hist[t] = 0;
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < kTopkPer; ++j)
+                    if (j * kTopkThreads + t < m && (u[j] & mask) == prefix)
+                        atomicAdd(&hist[static_cast<uint32_t>(u[j] >> sh) & dmask], 1u);
+                __syncthreads();
+                if (wave == 0) {
+                    // the digit d where the count of keys at digits >= d
+                    // first reaches `remaining` (lane l holds bins 4l..4l+3)
+                    const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2],
+                                   h3 = hist[4 * lane + 3];
+                    const int sum = static_cast<int>(h0 + h1 + h2 + h3);
+                    int suf = sum;
+#pragma unroll
+                    for (int off = 1; off < 64; off <<= 1) {
+                        const int v = __shfl_down(suf, off);
+                        if (lane + off < 64) suf += v;
+                    }
+                    int run = suf - sum;  // keys at lanes above this one
+                    const int hb[4] = {static_cast<int>(h0), static_cast<int>(h1), static_cast<int>(h2),
+                                       static_cast<int>(h3)};
+#pragma unroll
+                    for (int b = 3; b >= 0; --b) {
+                        if (run < remaining && run + hb[b] >= remaining) {
+                            ctl[0] = 4 * lane + b;
+                            ctl[1] = run;
+                            ctl[2] = hb[b];
+                        }
+                        run += hb[b];
+                    }
+                }
+                __syncthreads();
+                const int d = ctl[0];
+                remaining -= ctl[1];
+                prefix |= static_cast<uint64_t>(d) << sh;
+                mask |= static_cast<uint64_t>(dmask) << sh;
+                if (ctl[2] == remaining || sh == 0) break;  // workgroup-uniform
+                __syncthreads();  // ctl and hist are rewritten by the next pass
+            }
+        }
+        // keys above the prefix all survive; of those at it, `remaining`
+        // (all of them unless they are equal keys, i.e. padding)
+#pragma unroll
+        for (int j = 0; j < kTopkPer; ++j) {
+            if (j * kTopkThreads + t >= m) continue;
+            const uint64_t mu = u[j] & mask;
+            if (mu > prefix) emit(u[j]);
+            else if (mu == prefix && atomicAdd(&ctl[4], 1) < remaining) emit(u[j]);
+        }
+    }
+    if constexpr (!FINAL) {
+        __syncthreads();
+        for (int i = min(m, k) + t; i < k; i += kTopkThreads) out[static_cast<int64_t>(blockIdx.x) * k + i] = kKeyPad;
+    } else {
+        int P = 1;
+        while (P < k) P <<= 1;
+        __syncthreads();
+        for (int i = min(m, k) + t; i < P; i += kTopkThreads) sorted[i] = kKeyPad;
+        __syncthreads();
+        // bitonic sort of P keys, descending
+        for (int size = 2; size <= P; size <<= 1) {
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                for (int i = t; i < P / 2; i += kTopkThreads) {
+                    const int lo = 2 * i - (i & (stride - 1));
+                    const int hi = lo + stride;
+                    const bool desc = ((lo & size) == 0);
+                    const int64_t a = sorted[lo], b = sorted[hi];
+                    if ((a < b) == desc) {
+                        sorted[lo] = b;
+                        sorted[hi] = a;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (int i = t; i < k; i += kTopkThreads) out[i] = sorted[i];
+    }
+}
 
 // Workspace bytes sw_topk_device needs for n inputs and k outputs.
 size_t topk_workspace_bytes(int64_t n, int k) {
-    const int CH = chunk_for(k);
     size_t total = 0;
     int64_t cur = n;
-    while (cur > CH) {
-        const int64_t chunks = (cur + CH - 1) / CH;
+    while (cur > kTopkChunk) {
+        const int64_t chunks = (cur + kTopkChunk - 1) / kTopkChunk;
         cur = chunks * k;
         total += static_cast<size_t>(cur) * sizeof(int64_t);
     }
@@ -71,30 +198,23 @@ size_t topk_workspace_bytes(int64_t n, int k) {
 
 hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, int k,
                        int64_t* out, int64_t* work, hipStream_t s) {
-    if (k <= 0 || k > kTopkChunk / 2) return hipErrorInvalidValue;
-    const int CH = chunk_for(k);
-    auto stage = [&](unsigned grid, const int32_t* sc, const int64_t* kin, int64_t cnt, int64_t* dst) {
-        if (CH == 2048)
-            hipLaunchKernelGGL((sw_topk_stage<2048, 256>), dim3(grid), dim3(256), 0, s, sc, kin, cnt, id_base, k, dst);
-        else
-            hipLaunchKernelGGL((sw_topk_stage<kTopkChunk, 512>), dim3(grid), dim3(512), 0, s, sc, kin, cnt, id_base,
-                               k, dst);
-    };
+    if (k <= 0 || k > kTopkMaxK) return hipErrorInvalidValue;
     const int32_t* sc = scores;
     const int64_t* kin = keys;
     int64_t cur = n;
     int64_t* w = work;
-    while (cur > CH) {
-        const int64_t chunks = (cur + CH - 1) / CH;
-        stage(static_cast<unsigned>(chunks), sc, kin, cur, w);
-        hipError_t e = hipGetLastError();
+    while (cur > kTopkChunk) {  // each stage keeps k of every 16,384 keys (k <= 4,096)
+        const int64_t chunks = (cur + kTopkChunk - 1) / kTopkChunk;
+        hipLaunchKernelGGL((sw_topk_select<false>), dim3(static_cast<unsigned>(chunks)), dim3(kTopkThreads), 0, s,
+                           sc, kin, cur, id_base, k, w);
+        const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         sc = nullptr;
         kin = w;
         cur = chunks * k;
         w += cur;
     }
-    stage(1, sc, kin, cur, out);
+    hipLaunchKernelGGL((sw_topk_select<true>), dim3(1), dim3(kTopkThreads), 0, s, sc, kin, cur, id_base, k, out);
     return hipGetLastError();
 }
 

@@ -216,6 +216,34 @@ def test_device_topk(sw, handle, n, k):
     assert sc2[:m].tolist() == s[order[:m]].tolist()
 
 
+@pytest.mark.parametrize("n,k,dist", [(2_000_000, 4096, "ties"), (200_000, 300, "wide"), (50_000, 100, "equal"),
+                                      (16_384, 100, "ties"), (16_385, 4096, "wide"), (1, 1, "ties")])
+def test_device_topk_radix_select(sw, handle, n, k, dist):
+    """The radix select's corners: scores over the whole int32 range
+    ("wide"), one score for every subject ("equal": the order is the ids
+    alone), many ties; chunk-size boundaries (16,384 keys per workgroup), the
+    largest k, three stages (2M scores)."""
+    import torch
+    rng = np.random.default_rng(n ^ k)
+    if dist == "wide":
+        s = rng.integers(0, 2**31 - 1, size=n, dtype=np.int64).astype(np.int32)
+    elif dist == "equal":
+        s = np.full(n, 7, dtype=np.int32)
+    else:
+        s = rng.integers(0, 90, size=n).astype(np.int32)
+    m = min(n, k)
+    order = np.lexsort((np.arange(n), -s))[:m]
+    d = torch.from_numpy(s).cuda()
+    out = torch.empty(k, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    handle.topk_device(d.data_ptr(), n, k, out.data_ptr(), id_base=5)
+    torch.cuda.synchronize()
+    ids, sc = sw.capi.decode_keys(out.cpu().numpy())
+    assert ids[:m].tolist() == (order + 5).tolist()
+    assert sc[:m].tolist() == s[order].tolist()
+    assert (ids[m:] == -1).all()
+
+
 INTER_VARIANTS = ["32x8", "s32x8", "32x16", "s32x16", "48x8", "s48x8", "64x8", "s64x8", "16x16", "s16x16",
                   "x16x8", "x16x16", "x32x8", "x48x8", "y16x8", "y32x8", "y32x4",
                   "y48x4", "f32x8", "f32x4"]
