@@ -239,7 +239,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r01_pmc_traffic.json"))
+    # the latest rocprofv3 --pmc measurement of the C2 launch (FETCH_SIZE x2 +
+    # WRITE_SIZE, scripts/pmc_traffic.py); kept at the root because profiles/
+    # does not travel to the GPU box
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "pmc_traffic.json"))
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = rehearse the multi-rank path on one GPU (CPU collectives)")
     ap.add_argument("--device", type=int, default=None, help="override the GPU index (rehearsal)")
