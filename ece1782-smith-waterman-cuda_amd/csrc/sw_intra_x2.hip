@@ -130,6 +130,14 @@ struct IntraImg {
 // LIST: the rescue stage — subject pairs come from the device-side list of
 // the subjects the fp16 pass flagged (a.subj_list / a.list_count); the grid
 // covers the longest possible list and surplus workgroups return at once.
+// SW_IX2_PREFETCH: read the next step's profile words from LDS during this
+// step (its codes are known one step ahead), so the LDS latency is hidden
+// even when the SIMD's waves run in lockstep
+#ifndef SW_IX2_PREFETCH
+#define SW_IX2_PREFETCH 1
+#endif
+constexpr bool kPrefetch = SW_IX2_PREFETCH != 0;
+
 template <int RI, bool F16, bool LIST>
 __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
     static_assert(RI % 2 == 0 && RI <= 16, "rows per lane");
@@ -215,18 +223,43 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
         // LDS byte address of this lane's element of code 0
         const uint32_t lrow = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(img + lane));
 
+        constexpr uint32_t kCodeBytes = NQ * kLanes * sizeof(Elem);
+        // the profile words of code pair rcx (A | B << 8) for this lane
+        auto read_words = [&](uint32_t rcx, Elem (&wa)[NQ], Elem (&wb)[NQ]) {
+            typename Img::LElem* pa = reinterpret_cast<typename Img::LElem*>(
+                static_cast<uintptr_t>(lrow + (rcx & 0xffu) * kCodeBytes));
+            typename Img::LElem* pb = reinterpret_cast<typename Img::LElem*>(
+                static_cast<uintptr_t>(lrow + ((rcx >> 8) & 0xffu) * kCodeBytes));
+#pragma unroll
+            for (int qq = 0; qq < NQ; ++qq) {
+                wa[qq] = __builtin_bit_cast(Elem, pa[qq * kLanes]);
+                wb[qq] = __builtin_bit_cast(Elem, pb[qq * kLanes]);
+            }
+        };
+        auto codes_at = [&](int col) {
+            const uint32_t ca = col < LA ? resA[col] : kPadCode;
+            const uint32_t cb = col < LB ? resB[col] : kPadCode;
+            return ca | (cb << 8);
+        };
+        uint32_t in_res_nb = codes_at(lane);  // codes of the next block of 64 steps
+        Elem wa_n[NQ], wb_n[NQ];               // prefetched words of the next step
+        uint32_t rc_n = 0;
+
         for (int k0 = 0; k0 < nsteps; k0 += kLanes) {
             // lane-0 conveyors for steps k0 .. k0+63 (column k = step); the
             // first chunk's row -1 is H = 0, F = 0 at the bias lane 0 reads
             // them with (see the hand-off below)
             {
                 const int col = k0 + lane;
-                const uint32_t ca = col < LA ? resA[col] : kPadCode;
-                const uint32_t cb = col < LB ? resB[col] : kPadCode;
-                in_res = ca | (cb << 8);
+                in_res = in_res_nb;
+                in_res_nb = codes_at(col + kLanes);
                 const int bz = RI - 2 + (col % NB) + ((col % NB) == 0 ? NB : 0);
                 in_bh = (!first && col < L) ? bnd_h[col] : C::pair_of(bz * a.gap_extend);
                 in_bf = (!first && col < L) ? bnd_f[col] : C::pair_of((bz + 1) * a.gap_extend);
+            }
+            if (kPrefetch && k0 == 0) {
+                rc_n = shr1u(__builtin_amdgcn_readlane(in_res, 0), rc);
+                read_words(rc_n, wa_n, wb_n);
             }
             // whole bias periods (steps past nsteps run pad columns: harmless)
             const int mend = min(kLanes, nsteps - k0);
@@ -234,10 +267,27 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
 #pragma unroll
                 for (int b = 0; b < NB; ++b) {
                     const int m = m0 + b;
-                    const uint32_t sres = __builtin_amdgcn_readlane(in_res, m);
                     const uint32_t sbh = __builtin_amdgcn_readlane(in_bh, m);
                     const uint32_t sbf = __builtin_amdgcn_readlane(in_bf, m);
-                    rc = shr1u(sres, rc);
+                    Elem wa[NQ], wb[NQ];
+                    if constexpr (kPrefetch) {
+                        rc = rc_n;
+#pragma unroll
+                        for (int qq = 0; qq < NQ; ++qq) {
+                            wa[qq] = wa_n[qq];
+                            wb[qq] = wb_n[qq];
+                        }
+                        // the next step's codes: lane 0 takes the next column
+                        // (the next block's first at the block's last step)
+                        const bool wrap = (b == NB - 1) && (m0 + NB == kLanes);
+                        const uint32_t sres_n = wrap ? __builtin_amdgcn_readlane(in_res_nb, 0)
+                                                     : __builtin_amdgcn_readlane(in_res, (m + 1) & (kLanes - 1));
+                        rc_n = shr1u(sres_n, rc);
+                        read_words(rc_n, wa_n, wb_n);
+                    } else {
+                        rc = shr1u(__builtin_amdgcn_readlane(in_res, m), rc);
+                        read_words(rc, wa, wb);
+                    }
                     // hand-off: the row above's bottom (H, F) from one step back
                     const V adj = step(RI - 1 + (b == 0 ? NB : 0));
                     const uint32_t up0 = C::bits(C::from(shr1u(sbh, hl)) - adj);
@@ -250,17 +300,6 @@ __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
                             E[r] = E[r] - reb;
                         }
                         up_prev = C::bits(C::from(up_prev) - reb);
-                    }
-                    constexpr uint32_t kCodeBytes = NQ * kLanes * sizeof(Elem);
-                    typename Img::LElem* pa = reinterpret_cast<typename Img::LElem*>(
-                        static_cast<uintptr_t>(lrow + (rc & 0xffu) * kCodeBytes));
-                    typename Img::LElem* pb = reinterpret_cast<typename Img::LElem*>(
-                        static_cast<uintptr_t>(lrow + ((rc >> 8) & 0xffu) * kCodeBytes));
-                    Elem wa[NQ], wb[NQ];
-#pragma unroll
-                    for (int qq = 0; qq < NQ; ++qq) {
-                        wa[qq] = __builtin_bit_cast(Elem, pa[qq * kLanes]);
-                        wb[qq] = __builtin_bit_cast(Elem, pb[qq * kLanes]);
                     }
                     // H_diag + S for every row first (from the previous
                     // column's H), so H is then updated in place
