@@ -114,7 +114,7 @@ def valu_roofline(kernel, cells_rank, scan_ms, kernel_gcups):
     """The binding roofline: VALU instruction issue.  peak = the modeled
     issue-bound rate of the per-wave inter kernel (VALU_MODEL), achieved =
     the whole scan's rate (all kernels of the scan, concurrent)."""
-    cpc = VALU_MODEL.get(kernel)
+    cpc = VALU_MODEL.get(kernel.split("+")[0])  # "+int16[0,n)": the widest blocks in int16 beside it
     if cpc is None or scan_ms <= 0:
         return None
     peak = SIMDS * CLOCK_HZ / cpc / 1e9

@@ -239,6 +239,22 @@ struct sw_db {
     uint64_t lcount_key = 0;
     int32_t lcount_qlen = 0;
     std::vector<std::pair<uint64_t, int32_t>> i16_first;
+    // the inter scan's counterpart: the fp16 pass's flagged count and largest
+    // flagged block (pinned pair, event-gated) and per (scoring, query
+    // length) the span of widest blocks the int16 kernel then takes first
+    int32_t* h_icount = nullptr;
+    hipEvent_t icount_ev = nullptr;
+    bool icount_pending = false;
+    uint64_t icount_key = 0;
+    int32_t icount_qlen = 0;
+    int32_t icount_nr = 0;
+    struct SpanObs {
+        uint64_t key;
+        int32_t qlen;
+        int32_t span;
+    };
+    std::vector<SpanObs> i16_span;
+    int32_t last_i16_span = 0;
     uint64_t* h_trace = nullptr;         // SW_TRACE_FILE: host-mapped block timeline
     std::vector<uint32_t> h_blk_groups;  // block widths (16-column groups), widest first
     std::vector<int64_t> h_blk_res;      // unpadded residues per block
@@ -308,6 +324,8 @@ void free_dev(sw_db* db) {
     db->d_lrescue = nullptr;
     db->lcount_pending = false;
     db->i16_first.clear();  // the long partition may change
+    db->icount_pending = false;
+    db->i16_span.clear();   // ... and the block layout
     db->device_bytes = 0;
     db->built = false;
 }
@@ -786,6 +804,35 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             if (e.first == skey && e.second <= qlen) intra_i16_first = true;
     }
     intra_i16_first = intra_i16_first && intra_x2;
+    // The same for the inter scan, per block: long queries under cheap linear
+    // gaps put the WIDEST blocks (length-sorted, ids 0, 1, ...) in the fp16
+    // guard band, and their re-scoring by the list kernel (one wave per block,
+    // every pass in turn) takes longer than the whole scan.  A scan with the
+    // same scoring whose fp16 pass flagged most of blocks [0, span) makes
+    // later queries at least as long run those blocks in int16, by wave pairs
+    // beside the fp16 launch.  SW_INTER_I16_SPAN=n forces n blocks (0: off).
+    if (db->icount_pending && hipEventQuery(db->icount_ev) == hipSuccess) {
+        db->icount_pending = false;
+        const int32_t cnt = db->h_icount[0], span = db->h_icount[1] + 1;
+        // most of [nr, span) flagged: not a few high-scoring hits far out
+        if (cnt > 0 && span > db->icount_nr && 2 * static_cast<int64_t>(cnt) >= span - db->icount_nr) {
+            bool seen = false;
+            for (auto& e : db->i16_span)
+                if (e.key == db->icount_key && e.qlen == db->icount_qlen) {
+                    e.span = std::max(e.span, span);
+                    seen = true;
+                }
+            if (!seen) db->i16_span.push_back({db->icount_key, db->icount_qlen, span});
+        }
+    }
+    int32_t i16_span = 0;
+    if (const char* e = std::getenv("SW_INTER_I16_SPAN")) {
+        i16_span = std::atoi(e);
+    } else {
+        for (const auto& o : db->i16_span)
+            if (o.key == skey && o.qlen <= qlen) i16_span = std::max(i16_span, o.span);
+    }
+    i16_span = static_cast<int32_t>(std::min<int64_t>(std::max(i16_span, 0), db->nblocks));
     const int32_t qpad_intra2 = ri2 ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri2)) : 0;
     // Empty query: every score is 0 (the reference's kernel leaves maxScore 0).
     if (qlen == 0) {
@@ -829,7 +876,8 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                              p32, ri, qpad_intra, &P)))
         return rc;
     if (rescue && db->nblocks && !db->d_rescue) {
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rescue), 2 * (db->nblocks + 1) * sizeof(int32_t)));
+        // lists A and B, then the fp16 pass's largest flagged block
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rescue), (2 * (db->nblocks + 1) + 2) * sizeof(int32_t)));
         db->device_bytes += (db->nblocks + 1) * sizeof(int32_t);
     }
     const bool multi_inter = qpad_inter > R || qpad_rescue > swk::rescue_rows(affine) ||
@@ -946,11 +994,19 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         }
         int32_t* listA = db->d_rescue;                    // [count, ids...]
         int32_t* listB = db->d_rescue ? db->d_rescue + db->nblocks + 1 : nullptr;
+        int32_t* maxA = db->d_rescue ? db->d_rescue + 2 * (db->nblocks + 1) : nullptr;
+        // the widest blocks the int16 kernel takes first (see i16_span)
+        const int32_t nr = (f16 && rescue && npair && pair_merged && !ncoop) ? i16_span : 0;
+        db->last_i16_span = nr;
         if (rescue) {
             a.rescue_count = listA;
             a.rescue_list = listA + 1;
             HIPCHECK(hipMemsetAsync(listA, 0, sizeof(int32_t), h->stream));
-            if (f16) HIPCHECK(hipMemsetAsync(listB, 0, sizeof(int32_t), h->stream));
+            if (f16) {
+                HIPCHECK(hipMemsetAsync(listB, 0, sizeof(int32_t), h->stream));
+                HIPCHECK(hipMemsetAsync(maxA, 0xff, sizeof(int32_t), h->stream));  // -1
+                a.rescue_max = maxA;
+            }
             // fp16 exact range: every integer up to 2048; H grows by <= max S
             // per cell and the biased cell stores values up to 26 ge above
             // the true ones (bias (15 + 7 + 2) ge, + 2 ge in the profile)
@@ -983,23 +1039,57 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             HIPCHECK(hipEventRecord(h->coop_done, h->side2));
             ++h->launches;
             a.blk_first = npair;
+        } else if (nr) {
+            // blocks [0, nr) in int16 by wave pairs beside the fp16 launch;
+            // their near-32767 ones go to list B (the int32 stage)
+            swk::InterArgs c = a;
+            c.nblocks = nr;
+            c.blk_base = 0;
+            c.rescue_list = listB + 1;
+            c.rescue_count = listB;
+            c.rescue_max = nullptr;
+            HIPCHECK(hipEventRecord(h->fork2, h->stream));
+            HIPCHECK(hipStreamWaitEvent(h->side2, h->fork2, 0));
+            HIPCHECK(hipEventRecord(h->ev[4], h->side2));
+            HIPCHECK(swk::launch_inter_x2p(c, affine, false, false, h->side2));
+            HIPCHECK(hipEventRecord(h->ev[5], h->side2));
+            HIPCHECK(hipEventRecord(h->coop_done, h->side2));
+            ++h->launches;
         } else {
             HIPCHECK(hipEventRecord(h->ev[4], h->stream));
             HIPCHECK(hipEventRecord(h->ev[5], h->stream));
         }
         HIPCHECK(hipEventRecord(h->ev[6], h->stream));
         if (npair && pair_merged) {
-            // one launch: pairs for blocks [0, npair), one wave per block after
-            a.blk_first = npair;
+            // one launch: pairs for blocks [nr, npair), one wave per block after
+            a.blk_base = nr;
+            a.blk_first = std::max(npair, nr);
             HIPCHECK(swk::launch_inter_x2p(a, affine, f16, true, h->stream));
         } else {
             HIPCHECK(swk::launch_inter(a, affine, x2_ok, h->stream));
         }
         h->last_kernel = swk::inter_kernel_name(affine, x2_ok);
         if (npair) h->last_kernel.replace(0, std::strlen("sw_inter_x2s"), "sw_inter_x2p");  // + wave pairs
+        if (nr) h->last_kernel += "+int16[0," + std::to_string(nr) + ")";
         HIPCHECK(hipEventRecord(h->ev[7], h->stream));
         ++h->launches;
-        if (ncoop || (npair && !pair_merged)) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
+        if (f16 && rescue && !db->icount_pending) {
+            // the fp16 pass's flagged count and largest flagged block, read
+            // by a later scan (no synchronisation here)
+            if (!db->h_icount) {
+                HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&db->h_icount), 2 * sizeof(int32_t),
+                                       hipHostMallocDefault));
+                HIPCHECK(hipEventCreateWithFlags(&db->icount_ev, hipEventDisableTiming));
+            }
+            HIPCHECK(hipMemcpyAsync(db->h_icount, listA, sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
+            HIPCHECK(hipMemcpyAsync(db->h_icount + 1, maxA, sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
+            HIPCHECK(hipEventRecord(db->icount_ev, h->stream));
+            db->icount_pending = true;
+            db->icount_key = skey;
+            db->icount_qlen = qlen;
+            db->icount_nr = nr;
+        }
+        if (ncoop || (npair && !pair_merged) || nr) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
         if (f16) {
             // fp16 chain, stage 2: the int16 packed kernel re-scores the
             // blocks the fp16 kernel flagged (scores near 2048) and flags
@@ -1010,6 +1100,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             r.blk_count = listA;
             r.rescue_list = listB + 1;
             r.rescue_count = listB;
+            r.rescue_max = nullptr;
             HIPCHECK(swk::launch_inter_x2s_list(r, affine, h->stream));
             ++h->launches;
         }
@@ -1035,6 +1126,36 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     HIPCHECK(hipEventRecord(h->ev[3], h->stream));
     h->evpool[h->nscans - 1].launches = h->launches;
     h->timed = true;
+    if (std::getenv("SW_RESCUE_STATS")) {  // diagnostics: what the guard bands flagged (synchronises)
+        HIPCHECK(hipStreamSynchronize(h->stream));
+        int32_t cA = 0, cB = 0, l1 = 0, l2 = 0;
+        std::vector<int32_t> ids;
+        if (db->d_rescue) {
+            HIPCHECK(hipMemcpy(&cA, db->d_rescue, 4, hipMemcpyDeviceToHost));
+            HIPCHECK(hipMemcpy(&cB, db->d_rescue + db->nblocks + 1, 4, hipMemcpyDeviceToHost));
+            ids.resize(static_cast<size_t>(cA));
+            if (cA) HIPCHECK(hipMemcpy(ids.data(), db->d_rescue + 1, 4 * ids.size(), hipMemcpyDeviceToHost));
+        }
+        if (db->d_lrescue) {
+            HIPCHECK(hipMemcpy(&l1, db->d_lrescue, 4, hipMemcpyDeviceToHost));
+            HIPCHECK(hipMemcpy(&l2, db->d_lrescue + db->nlong + 1, 4, hipMemcpyDeviceToHost));
+        }
+        int64_t res = 0;
+        int32_t wmin = 1 << 30, wmax = 0, bmin = 1 << 30, bmax = -1;
+        for (int32_t b : ids) {
+            res += db->h_blk_res[b];
+            wmin = std::min<int32_t>(wmin, db->h_blk_groups[b] * 16);
+            wmax = std::max<int32_t>(wmax, db->h_blk_groups[b] * 16);
+            bmin = std::min(bmin, b);
+            bmax = std::max(bmax, b);
+        }
+        std::fprintf(stderr,
+                     "rescue: qlen %d go %d ge %d: inter %d/%lld blocks flagged (ids %d..%d, widths %d..%d, "
+                     "%lld of %lld residues), %d again; pairs %d; intra %d/%lld flagged, %d again\n",
+                     qlen, go, ge, cA, static_cast<long long>(db->nblocks), bmin, bmax, wmin, wmax,
+                     static_cast<long long>(res), static_cast<long long>(db->residues), cB, npair, l1,
+                     static_cast<long long>(db->nlong), l2);
+    }
     return SW_OK;
 }
 
@@ -1376,6 +1497,8 @@ int sw_db_free(sw_db* db) {
     }
     if (db->h_lcount) (void)hipHostFree(db->h_lcount);
     if (db->lcount_ev) (void)hipEventDestroy(db->lcount_ev);
+    if (db->h_icount) (void)hipHostFree(db->h_icount);
+    if (db->icount_ev) (void)hipEventDestroy(db->icount_ev);
     free_dev(db);
     delete db;
     return SW_OK;

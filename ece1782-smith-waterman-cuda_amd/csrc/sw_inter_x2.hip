@@ -514,7 +514,10 @@ __device__ __forceinline__ void x2s_finish(const InterArgs& a, int blk, int lane
     if (a.rescue_list) {
         const bool sat = F16 ? (b >= a.sat_limit) : (b >= kSat16 || b < 0);
         const uint64_t m = __builtin_amdgcn_ballot_w64(sat);
-        if (m && lane == 0) a.rescue_list[atomicAdd(a.rescue_count, 1)] = blk;
+        if (m && lane == 0) {
+            a.rescue_list[atomicAdd(a.rescue_count, 1)] = blk;
+            if (a.rescue_max) atomicMax(a.rescue_max, blk);
+        }
     }
 }
 
@@ -846,9 +849,10 @@ __global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
     using V = typename P::V;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int npair = MERGED ? a.blk_first : a.nblocks;  // blocks [0, npair) by pairs
-    if (MERGED && static_cast<int>(blockIdx.x) >= (npair + 1) / 2) {
-        const int blk = npair + (blockIdx.x - (npair + 1) / 2) * kWavesPerWG + wave;
+    const int npair = MERGED ? a.blk_first : a.nblocks;  // blocks [blk_base, npair) by pairs
+    const int pwg = (npair - a.blk_base + 1) / 2;           // their workgroups
+    if (MERGED && static_cast<int>(blockIdx.x) >= pwg) {
+        const int blk = npair + (blockIdx.x - pwg) * kWavesPerWG + wave;
         if (blk < a.nblocks) x2s_block<R, SG, AFFINE, F16>(a, blk, lds[wave], lane);
         return;  // workgroup-uniform branch: no barrier below is skipped by part of it
     }
@@ -857,10 +861,10 @@ __global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
     // the workgroup's clock runs to the longer of its two blocks
     int tmax = 0;
     for (int q = 0; q < 2; ++q) {
-        const int b = blockIdx.x * 2 + q;
+        const int b = a.blk_base + blockIdx.x * 2 + q;
         if (b < npair) tmax = max(tmax, pair_ticks(a.blk_groups[b] * kGroupCols, passes, SG));
     }
-    const int blk = blockIdx.x * 2 + pr;
+    const int blk = a.blk_base + blockIdx.x * 2 + pr;
     Best<F16> best;
     best.init();
     int tick = 0;
@@ -895,14 +899,15 @@ __global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
     }
 }
 
-// merged = false: blocks [0, a.nblocks) by wave pairs (the caller passes the
-// pair count as nblocks).  merged = true: the whole scan in one launch, blocks
-// [0, a.blk_first) by pairs and [a.blk_first, a.nblocks) one per wave.  The
-// two-strips 32x8 shapes only.
+// merged = false: blocks [a.blk_base, a.nblocks) by wave pairs (the caller
+// passes the pair range's end as nblocks).  merged = true: the whole scan in
+// one launch, blocks [a.blk_base, a.blk_first) by pairs and [a.blk_first,
+// a.nblocks) one per wave.  The two-strips 32x8 shapes only.
 template <bool M>
 static hipError_t launch_x2p(const InterArgs& a, bool affine, bool f16, hipStream_t s) {
     const int np = M ? a.blk_first : a.nblocks;
-    const int nwg = (np + 1) / 2 + (M ? (a.nblocks - np + kWavesPerWG - 1) / kWavesPerWG : 0);
+    const int nwg = (np - a.blk_base + 1) / 2 + (M ? (a.nblocks - np + kWavesPerWG - 1) / kWavesPerWG : 0);
+    if (nwg <= 0) return hipSuccess;
     const dim3 grid(nwg), block(kWavesPerWG * kLanes);
     if (f16 && affine) hipLaunchKernelGGL((sw_inter_x2p<32, 8, true, true, M>), grid, block, 0, s, a);
     else if (f16) hipLaunchKernelGGL((sw_inter_x2p<32, 8, false, true, M>), grid, block, 0, s, a);

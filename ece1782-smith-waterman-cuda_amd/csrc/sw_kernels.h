@@ -72,6 +72,12 @@ struct InterArgs {
     // packed (gap_open - gap_extend); host-built so they stay in SGPRs
     uint32_t f16_step[32];
     uint32_t f16_gog;
+    // sw_inter_x2p: its pair blocks are [blk_base, blk_first) (merged) or
+    // [blk_base, nblocks); blocks below blk_base run elsewhere
+    int32_t blk_base;
+    // fp16 kernels: the largest flagged block id (atomicMax; nullable), read
+    // back by the host to route the widest blocks to int16 next time
+    int32_t* rescue_max;
     // per-block timeline (builds with -DSW_TRACE_BLOCKS only; env
     // SW_TRACE_FILE): [block][start, end, HW_ID, XCC_ID | kind << 32],
     // s_memrealtime (100 MHz) stamps, host-mapped memory

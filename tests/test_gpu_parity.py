@@ -484,3 +484,45 @@ def test_intra_rescue_chain_fp16_int16_int32(sw, oracle, handle, monkeypatch, or
                 assert (w >= 1966).sum() * 2 > len(subs) or ge == 1
         assert want.max() > 32767
         assert ((want > 2048) & (want < 32000)).sum() >= (2 if ge == 2 else 1)
+
+
+def test_inter_widest_blocks_int16_first(sw, oracle, handle, monkeypatch):
+    """Long queries under the reference scoring (BLOSUM50, linear 2) put the
+    widest blocks in the fp16 guard band; once a scan has flagged most of
+    blocks [0, span), later scans with queries at least as long run those
+    blocks in int16 by wave pairs beside the fp16 launch (SW_INTER_I16_SPAN
+    forces a span: one block, some, more than the pair blocks, all of them;
+    and under affine scoring).  Every scan bit-exact against the oracle."""
+    r1, o1 = sw.synth.fixed_length_database(1280, 1650, 200, shard=41)
+    r2, o2 = sw.synth.fixed_length_database(3000, 250, 80, shard=42)
+    r = np.concatenate([r1, r2])
+    o = np.concatenate([o1, o2[1:] + o1[-1]])
+    q = sw.synth.query(2600, shard=43)
+    m = sw.capi.builtin_matrix(0)
+    db = sw.Database(handle, r, o, long_threshold=4096)
+    assert db.stats()["n_long"] == 0
+    want = oracle.scan(q, r, o, mat=m, gap_open=2, gap_extend=2)
+    got = db.scan(q, m, 2, 2)
+    assert np.array_equal(got, want)
+    assert "+int16" not in handle.last_kernel()       # nothing observed yet
+    got = db.scan(q, m, 2, 2)
+    assert np.array_equal(got, want)
+    k = handle.last_kernel()
+    assert "+int16[0," in k, k                         # the widest ~19 blocks
+    assert 10 <= int(k.split("+int16[0,")[1].rstrip(")")) <= 30, k
+    q2 = q[:2000]
+    want2 = oracle.scan(q2, r, o, mat=m, gap_open=2, gap_extend=2)
+    assert np.array_equal(db.scan(q2, m, 2, 2), want2)
+    assert "+int16" not in handle.last_kernel()       # shorter than any observation
+    nblocks = db.stats()["n_blocks"]
+    monkeypatch.setenv("SW_PAIR_WIDTH", "2000")       # few pair blocks: spans beyond them
+    for span in (1, 7, 25, nblocks):
+        monkeypatch.setenv("SW_INTER_I16_SPAN", str(span))
+        got = db.scan(q, m, 2, 2)
+        assert np.array_equal(got, want), (span, np.nonzero(got != want)[0][:10])
+        assert handle.last_kernel().endswith("+int16[0,%d)" % span)
+    monkeypatch.setenv("SW_INTER_I16_SPAN", "5")
+    m62 = sw.capi.builtin_matrix(1)
+    want3 = oracle.scan(q2, r, o, mat=m62, gap_open=12, gap_extend=1)
+    assert np.array_equal(db.scan(q2, m62, 12, 1), want3)
+    assert handle.last_kernel().endswith("+int16[0,5)")
