@@ -889,6 +889,17 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         db->device_bytes += 2 * (db->nlong + 1) * sizeof(int32_t);
     }
 
+    // the rescue lists' counters (inter A, B, largest flagged block; intra
+    // 1, 2) in one launch instead of five memsets, before the fork so the
+    // side stream sees them
+    {
+        int32_t* cA = (rescue && db->nblocks) ? db->d_rescue : nullptr;
+        int32_t* cB = (cA && f16) ? db->d_rescue + db->nblocks + 1 : nullptr;
+        int32_t* mA = (cA && f16) ? db->d_rescue + 2 * (db->nblocks + 1) : nullptr;
+        int32_t* c1 = (db->nlong && intra_x2) ? db->d_lrescue : nullptr;
+        int32_t* c2 = c1 ? db->d_lrescue + db->nlong + 1 : nullptr;
+        if (cA || c1) HIPCHECK(swk::launch_reset_counters(cA, cB, mA, c1, c2, h->stream));
+    }
     // fork: the side stream starts when the main stream reaches ev[0]
     HIPCHECK(hipEventRecord(h->ev[0], h->stream));
     h->last_intra = "none";
@@ -924,8 +935,6 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             x.f16_gog = f16_pair(go - ge);
             int32_t* list1 = db->d_lrescue;                  // flagged by the fp16 pass
             int32_t* list2 = db->d_lrescue + db->nlong + 1;  // ... and again by the int16 pass
-            HIPCHECK(hipMemsetAsync(list1, 0, sizeof(int32_t), is));
-            HIPCHECK(hipMemsetAsync(list2, 0, sizeof(int32_t), is));
             if (intra_i16_first) {
                 // the int16 form over every long subject, flagging near-32767 ones
                 x.rescue_count = list2;
@@ -1001,12 +1010,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         if (rescue) {
             a.rescue_count = listA;
             a.rescue_list = listA + 1;
-            HIPCHECK(hipMemsetAsync(listA, 0, sizeof(int32_t), h->stream));
-            if (f16) {
-                HIPCHECK(hipMemsetAsync(listB, 0, sizeof(int32_t), h->stream));
-                HIPCHECK(hipMemsetAsync(maxA, 0xff, sizeof(int32_t), h->stream));  // -1
-                a.rescue_max = maxA;
-            }
+            if (f16) a.rescue_max = maxA;  // counters reset before the fork
             // fp16 exact range: every integer up to 2048; H grows by <= max S
             // per cell and the biased cell stores values up to 26 ge above
             // the true ones (bias (15 + 7 + 2) ge, + 2 ge in the profile)

@@ -223,6 +223,9 @@ uint64_t synth_hash(uint64_t seed, uint64_t id, uint64_t k);
 
 // Device top-K (sw_topk.hip): keys = score << 32 | (2^31 - 1 - id), best first.
 size_t topk_workspace_bytes(int64_t n, int k);
+// One thread zeroes the rescue lists' counters (c = -1: a largest-id slot);
+// null pointers are skipped.
+hipError_t launch_reset_counters(int32_t* a, int32_t* b, int32_t* c, int32_t* d, int32_t* e, hipStream_t s);
 hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, int k,
                        int64_t* out, int64_t* work, hipStream_t s);
 
