@@ -526,3 +526,34 @@ def test_inter_widest_blocks_int16_first(sw, oracle, handle, monkeypatch):
     want3 = oracle.scan(q2, r, o, mat=m62, gap_open=12, gap_extend=1)
     assert np.array_equal(db.scan(q2, m62, 12, 1), want3)
     assert handle.last_kernel().endswith("+int16[0,5)")
+
+
+@pytest.mark.parametrize("case", range(24))
+def test_random_scoring_and_shapes(sw, oracle, handle, case):
+    """Seeded random cases against the oracle: a random symmetric matrix
+    (entries -9..13, positive diagonal), gap pairs with open >= extend and a
+    few with open < extend, ragged databases with subjects of 1..4,000
+    residues, queries of 1..1,600, and the long threshold at the default, 64
+    or 500, so every kernel family and both rescue chains get random inputs.
+    Each database is scanned twice (the second scan may take the adaptive
+    int16 paths)."""
+    rng = np.random.default_rng(1000 + case)
+    m = rng.integers(-9, 14, size=(25, 25))
+    m = np.triu(m) + np.triu(m, 1).T
+    np.fill_diagonal(m, rng.integers(1, 14, size=25))
+    m = m.astype(np.int8).reshape(-1)
+    ge = int(rng.integers(1, 8))
+    go = int(ge + rng.integers(0, 15)) if case % 6 else int(rng.integers(1, ge + 1))
+    n = int(rng.integers(50, 400))
+    lens = np.clip(rng.lognormal(np.log(300), 0.9, size=n), 1, 4000).astype(np.int64)
+    subs = [rng.integers(0, 25, size=int(L)).astype(np.uint8) for L in lens]
+    r = np.concatenate(subs)
+    o = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    thr = [None, 64, 500][case % 3]
+    q = rng.integers(0, 25, size=int(rng.integers(1, 1600))).astype(np.uint8)
+    db = sw.Database(handle, r, o, long_threshold=thr)
+    want = oracle.scan(q, r, o, mat=m, gap_open=go, gap_extend=ge)
+    for _ in range(2):
+        got = db.scan(q, m, go, ge)
+        assert np.array_equal(got, want), (case, go, ge, len(q), handle.last_kernel(),
+                                           handle.last_intra_kernel(), np.nonzero(got != want)[0][:10])
