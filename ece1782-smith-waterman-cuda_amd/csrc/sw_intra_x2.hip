@@ -22,8 +22,11 @@
 //
 // Exactness: fp16 holds every integer up to 2048.  H grows by at most max S
 // per cell, so a subject whose running maximum reaches a.sat_limit =
-// 2048 − 2·max S (computed exactly) is appended to a.rescue_list and re-scored
-// by the int32 sw_intra in list mode (sw_capi.cpp).
+// 2048 − 2·max S − 26·ge (computed exactly) is appended to a.rescue_list.
+// The same kernel in int16 (IntraCell<false>, LIST) re-scores that list and
+// appends subjects near 32767 to a second list for the int32 sw_intra; when
+// the fp16 pass would flag most subjects (cheap linear gaps on long pairs)
+// the host runs the int16 form first over all of them (sw_capi.cpp).
 #include <cstdlib>
 #include <type_traits>
 
