@@ -350,6 +350,36 @@ __device__ __forceinline__ void stage_x2s(X2Lds<R>& L, const int16_t* __restrict
     }
 }
 
+// One of the two images (img 0: lo <- rows [s0, s0+R); img 1: hi <- rows
+// [s0+R, s0+2R)), for the chained passes of sw_inter_x2s.
+template <int R, bool F16 = false>
+__device__ __forceinline__ void stage_x2s_one(X2Lds<R>& L, const int16_t* __restrict__ prof, int stride, int s0,
+                                              int lane, int bias, int img) {
+    constexpr int RD = x2_row_dwords(R);
+    constexpr uint32_t one = F16 ? 0x3c00u : 1u;
+    for (int u = lane; u < kProfileRows * (R / 8); u += kLanes) {
+        const int c = u / (R / 8);
+        const int k = u % (R / 8);
+        const int4 v = *reinterpret_cast<const int4*>(prof + static_cast<size_t>(c) * stride + s0 + img * R + 8 * k);
+        const uint32_t w[4] = {static_cast<uint32_t>(v.x), static_cast<uint32_t>(v.y), static_cast<uint32_t>(v.z),
+                               static_cast<uint32_t>(v.w)};
+        uint32_t o[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            uint32_t a0 = w[e] & 0xffffu, a1 = w[e] >> 16;
+            if constexpr (F16) {
+                a0 = to_f16_bits(static_cast<uint32_t>(static_cast<int16_t>(a0) + bias));
+                a1 = to_f16_bits(static_cast<uint32_t>(static_cast<int16_t>(a1) + bias));
+            }
+            o[2 * e] = img ? (a0 << 16) | one : a0 | (one << 16);
+            o[2 * e + 1] = img ? (a1 << 16) | one : a1 | (one << 16);
+        }
+        int4* d = reinterpret_cast<int4*>((img ? L.hi : L.lo) + c * RD + 8 * k);
+        d[0] = make_int4(o[0], o[1], o[2], o[3]);
+        d[1] = make_int4(o[4], o[5], o[6], o[7]);
+    }
+}
+
 // half-word shuffles as one v_perm_b32 each (byte i of the result = byte
 // sel[i] of {src0 : src1}, src1 the low dword)
 __device__ __forceinline__ uint32_t lo_lo(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040100u); }
@@ -549,10 +579,21 @@ __device__ __forceinline__ void ring_load(uint32_t (&v)[SG], const int4* ring, i
 // is part of a wave pair's pipeline (sw_inter_x2p): the boundary comes from /
 // goes to the partner wave through an LDS ring instead of HBM when in_ring /
 // out_ring, and every sub-group ends with one workgroup barrier (a tick).
-template <int R, int SG, bool AFFINE, bool F16, bool PAIR, int CR = 16>
+//
+// CHAIN (single-wave blocks): all passes of the block in ONE sweep over
+// npass x ncols virtual columns.  The low strip enters pass k at virtual
+// column k ncols while the high strip still finishes pass k-1's last SG
+// columns, so the lag sub-group of each pass boundary does useful work in
+// both halves (2 % of C2's sub-groups otherwise half idle).  At that
+// transition the lo image is restaged and the low halves of H, E and dtop
+// restart; SG columns later the same for the hi image and the high halves.
+// The low strip's row -1 input of pass k's first columns was stored by pass
+// k-1's high strip at least one sub-group earlier (ncols >= 32).
+template <int R, int SG, bool AFFINE, bool F16, bool PAIR, int CR = 16, bool CHAIN = false>
 __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32_t ncols, uint64_t base, int lane,
                                          int s0, Best<F16>& best, int4* ring, bool in_ring, bool out_ring,
                                          int* tick) {
+    static_assert(!(CHAIN && PAIR), "chained passes: single-wave blocks only");
     // SG: sub-group width = the lag (columns) between the two strips
     // CR: profile rows per LDS chunk (16: 2 x 4 ds_read_b128 in flight; 8
     // halves the chunk registers)
@@ -575,6 +616,10 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     }
     const bool first = (s0 == 0);
     const bool last = (s0 + 2 * R >= a.qpad);
+    // CHAIN: passes in this sweep and its virtual width
+    const uint32_t npass = CHAIN ? static_cast<uint32_t>((a.qpad + 2 * R - 1) / (2 * R)) : 1u;
+    const uint32_t total = npass * ncols;
+    const int sbias = F16 ? (AFFINE ? 2 : 1) * a.gap_extend : 0;
     // fp16: the images hold S + 2 ge (the diagonal comes from bias r - 1 + jj - 1;
     // the linear profile already holds S + g)
     stage_x2s<R, F16>(L, prof16, a.prof_stride, s0, lane, F16 ? (AFFINE ? 2 : 1) * a.gap_extend : 0);
@@ -620,15 +665,64 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     uint32_t aa = blo + code_of(rc, 0) * RB, ab = bhi + code_of(rp, 0) * RB;
     read_x2a<CQ>(PL[0], PH[0], aa, ab, 0, 0);
 
-    // sub-groups 0 .. ncols/SG: the last one runs the high strip only
-    for (uint32_t col0 = 0; col0 <= ncols; col0 += SG) {
-        const bool has_next = col0 + SG <= ncols;          // another sub-group follows
-        const bool next_lo = col0 + SG < ncols;            // ... with real low-strip columns
+    // sub-groups 0 .. total/SG: the last one runs the high strip only.
+    // CHAIN: lo_p / lo_c = the low strip's pass and its first column in that
+    // pass (running counters: no divisions in the loop); t2 = the high strip
+    // enters a pass (the sub-group after the low strip's entry)
+    uint32_t lo_p = 0, lo_c = 0;
+    bool t2 = false;
+    for (uint32_t col0 = 0; col0 <= total; col0 += SG) {
+        const bool has_next = col0 + SG <= total;          // another sub-group follows
+        const bool next_lo = col0 + SG < total;            // ... with real low-strip columns
         const uint32_t ncol = col0 + SG;
-        const uint64_t noff = (ncol >> 4) * kGroupBytes + (ncol & 15);
+        const bool wrap = CHAIN && lo_c + SG == ncols;      // the next sub-group starts a pass
+        const uint32_t nreal = CHAIN ? (wrap ? 0u : lo_c + SG) : ncol;  // its column in the subject
+        const bool next_first = CHAIN ? (lo_p == 0 && !wrap) : first;
+        const uint64_t noff = (nreal >> 4) * kGroupBytes + (nreal & 15);
+        const bool t1 = CHAIN && lo_c == 0 && lo_p > 0 && lo_p < npass;  // low strip enters pass lo_p
+        // the next sub-group starts a pass in the low strip (T1) or the high
+        // strip (T2): its first profile words are read after the restaging
+        // instead of prefetched here
+        const bool next_t1 = CHAIN && wrap && next_lo;
+        const bool next_t2 = t1;
+        if (t1) {
+            stage_x2s_one<R, F16>(L, prof16, a.prof_stride, static_cast<int>(lo_p) * 2 * R, lane, sbias, 0);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                H[r] = P::from(__builtin_amdgcn_perm(P::bits(H[r]), F16 ? a.f16_step[r % kRowGroup + SG - 1] : 0u,
+                                                     0x07060100u));
+                if constexpr (AFFINE) E[r] = P::from(P::bits(E[r]) & 0xffff0000u);
+            }
+            dtop = __builtin_amdgcn_perm(dtop, F16 ? a.f16_step[SG - 2] : 0u, 0x07060100u);
+        }
+        if (t2) {
+            // the high strip enters pass lo_p (the low strip entered it one sub-group ago)
+            stage_x2s_one<R, F16>(L, prof16, a.prof_stride, static_cast<int>(lo_p) * 2 * R, lane, sbias, 1);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                H[r] = P::from(__builtin_amdgcn_perm(F16 ? a.f16_step[r % kRowGroup + SG - 1] : 0u, P::bits(H[r]),
+                                                     0x07060100u));
+                if constexpr (AFFINE) E[r] = P::from(P::bits(E[r]) & 0xffffu);
+            }
+            dtop = __builtin_amdgcn_perm(F16 ? a.f16_step[SG - 2] : 0u, dtop, 0x07060100u);
+        }
+        if (t1 || t2) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            aa = blo + code_of(rc, 0) * RB;
+            ab = bhi + code_of(rp, 0) * RB;
+            read_x2a<CQ>(PL[0], PH[0], aa, ab, 0, 0);
+        }
+        if (next_t1) {
+            // pass k's row -1 input: pass k-1's stores of columns 0..SG-1
+            // (this wave's own, one or more sub-groups ago) complete first
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
         if (has_next) {
             load_codes<SG>(rn, a.residues + base + noff, next_lo);
-            if (!first && next_lo) {
+            if (!next_first && next_lo) {
                 if (PAIR && in_ring) ring_load<SG>(bin_n, ring, (ncol / SG) % kRingSlots, lane);
                 else load_pairs<SG>(bin_n, reinterpret_cast<const int32_t*>(bnd) + base + noff);
             }
@@ -744,7 +838,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
                     ab = bhi + code_of(rp, jn) * RB;
                 }
                 read_x2a<CQ>(PL[(t + 1) & 1], PH[(t + 1) & 1], aa, ab, kn, dep);
-            } else if (has_next) {
+            } else if (has_next && !next_t1 && !next_t2) {
                 aa = blo + code_of(rn, 0) * RB;
                 ab = bhi + code_of(rc, 0) * RB;
                 read_x2a<CQ>(PL[(t + 1) & 1], PH[(t + 1) & 1], aa, ab, 0, dep);
@@ -762,12 +856,15 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
             __builtin_amdgcn_sched_barrier(0);
         }
         // the high strip just finished columns [col0 - SG, col0)
-        if (!last && col0 >= SG) {
+        // the high strip's pass: the low strip's, or the one before while
+        // the low strip is in its first sub-group
+        const bool high_last = CHAIN ? (lo_c == 0 ? lo_p : lo_p + 1) >= npass : last;
+        if (!high_last && col0 >= SG) {
             // boundary out = the high halves of the delay line just written
             uint32_t hb[SG];
 #pragma unroll
             for (int q = 0; q < SG; ++q) hb[q] = AFFINE ? hi_hi(dl_h[q], dl_f[q]) : (dl_h[q] >> 16);
-            const uint32_t pc = col0 - SG;
+            const uint32_t pc = CHAIN ? (lo_c == 0 ? ncols - SG : lo_c - SG) : col0 - SG;
             if (PAIR && out_ring) {
                 ring_store<SG>(ring, (pc / SG) % kRingSlots, lane, hb);
             } else {
@@ -782,14 +879,24 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
                 rc[q] = rn[q];
             }
 #pragma unroll
-            for (int q = 0; q < SG; ++q) bin[q] = (first || !next_lo) ? bz[q] : bin_n[q];
+            for (int q = 0; q < SG; ++q) bin[q] = (next_first || !next_lo) ? bz[q] : bin_n[q];
         }
         if constexpr (PAIR) {
             __syncthreads();  // one tick of the pair's clock
             ++*tick;
         }
+        if constexpr (CHAIN) {
+            t2 = t1;
+            lo_c = nreal;
+            lo_p += wrap ? 1u : 0u;
+        }
     }
 }
+
+#ifndef SW_X2_CHAIN
+#define SW_X2_CHAIN 1
+#endif
+constexpr bool kChainPasses = SW_X2_CHAIN != 0;
 
 template <int R, int SG, bool AFFINE, bool F16, int CR>
 __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>& L, int lane) {
@@ -798,8 +905,13 @@ __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>&
     Best<F16> best;
     best.init();
     const uint64_t t0 = trace_now();
-    for (int s0 = 0; s0 < a.qpad && ncols > 0; s0 += 2 * R)
-        x2s_pass<R, SG, AFFINE, F16, false, CR>(a, L, ncols, base, lane, s0, best, nullptr, false, false, nullptr);
+    if (kChainPasses && ncols >= 32 && a.qpad > 2 * R) {
+        x2s_pass<R, SG, AFFINE, F16, false, CR, true>(a, L, ncols, base, lane, 0, best, nullptr, false, false, nullptr);
+    } else {
+        for (int s0 = 0; s0 < a.qpad && ncols > 0; s0 += 2 * R)
+            x2s_pass<R, SG, AFFINE, F16, false, CR>(a, L, ncols, base, lane, s0, best, nullptr, false, false,
+                                                    nullptr);
+    }
     x2s_finish<F16>(a, blk, lane, best.value(a));
     trace_block(a, blk, t0, lane, 0);
 }
