@@ -1,5 +1,5 @@
-# Transition images loaded a sub-group ahead (default) vs loaded at the
-# transition (lib_base): full GPU suite, then C2 / C3 A/B.
+# Chained-pass transitions staged by LDS-DMA a sub-group ahead (default) vs
+# ordinary loads at the transition (lib_base): full GPU suite, then C2 / C3 A/B.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/preload
