@@ -816,13 +816,22 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         const int32_t cnt = db->h_icount[0], span = db->h_icount[1] + 1;
         // most of [nr, span) flagged: not a few high-scoring hits far out
         if (cnt > 0 && span > db->icount_nr && 2 * static_cast<int64_t>(cnt) >= span - db->icount_nr) {
-            bool seen = false;
-            for (auto& e : db->i16_span)
-                if (e.key == db->icount_key && e.qlen == db->icount_qlen) {
-                    e.span = std::max(e.span, span);
-                    seen = true;
-                }
-            if (!seen) db->i16_span.push_back({db->icount_key, db->icount_qlen, span});
+            // keep a staircase per scoring: drop what the new observation
+            // dominates (a query at least as long with a span no larger),
+            // skip it if an existing one dominates it
+            const uint64_t k = db->icount_key;
+            const int32_t q = db->icount_qlen;
+            bool dominated = false;
+            for (const auto& e : db->i16_span)
+                if (e.key == k && e.qlen <= q && e.span >= span) dominated = true;
+            if (!dominated) {
+                db->i16_span.erase(std::remove_if(db->i16_span.begin(), db->i16_span.end(),
+                                                  [&](const sw_db::SpanObs& e) {
+                                                      return e.key == k && e.qlen >= q && e.span <= span;
+                                                  }),
+                                   db->i16_span.end());
+                db->i16_span.push_back({k, q, span});
+            }
         }
     }
     int32_t i16_span = 0;
