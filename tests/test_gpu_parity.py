@@ -528,7 +528,7 @@ def test_inter_widest_blocks_int16_first(sw, oracle, handle, monkeypatch):
     assert handle.last_kernel().endswith("+int16[0,5)")
 
 
-@pytest.mark.parametrize("case", range(24))
+@pytest.mark.parametrize("case", range(int(__import__("os").environ.get("SW_RANDOM_CASES", "24"))))
 def test_random_scoring_and_shapes(sw, oracle, handle, case):
     """Seeded random cases against the oracle: a random symmetric matrix
     (entries -9..13, positive diagonal), gap pairs with open >= extend and a
@@ -536,7 +536,7 @@ def test_random_scoring_and_shapes(sw, oracle, handle, case):
     residues, queries of 1..1,600, and the long threshold at the default, 64
     or 500, so every kernel family and both rescue chains get random inputs.
     Each database is scanned twice (the second scan may take the adaptive
-    int16 paths)."""
+    int16 paths).  SW_RANDOM_CASES=n runs n cases (a stress run)."""
     rng = np.random.default_rng(1000 + case)
     m = rng.integers(-9, 14, size=(25, 25))
     m = np.triu(m) + np.triu(m, 1).T
