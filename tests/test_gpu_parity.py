@@ -536,7 +536,8 @@ def test_random_scoring_and_shapes(sw, oracle, handle, case):
     residues, queries of 1..1,600, and the long threshold at the default, 64
     or 500, so every kernel family and both rescue chains get random inputs.
     Each database is scanned twice (the second scan may take the adaptive
-    int16 paths).  SW_RANDOM_CASES=n runs n cases (a stress run)."""
+    int16 paths).  SW_RANDOM_CASES=n runs n cases and SW_RANDOM_QMAX the
+    longest query (stress runs)."""
     rng = np.random.default_rng(1000 + case)
     m = rng.integers(-9, 14, size=(25, 25))
     m = np.triu(m) + np.triu(m, 1).T
@@ -550,7 +551,8 @@ def test_random_scoring_and_shapes(sw, oracle, handle, case):
     r = np.concatenate(subs)
     o = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     thr = [None, 64, 500][case % 3]
-    q = rng.integers(0, 25, size=int(rng.integers(1, 1600))).astype(np.uint8)
+    qmax = int(__import__("os").environ.get("SW_RANDOM_QMAX", "1600"))
+    q = rng.integers(0, 25, size=int(rng.integers(1, qmax))).astype(np.uint8)
     db = sw.Database(handle, r, o, long_threshold=thr)
     want = oracle.scan(q, r, o, mat=m, gap_open=go, gap_extend=ge)
     for _ in range(2):
