@@ -14,29 +14,40 @@ linear gap 2) is timed the same way right after and reported under
 
 --config c3: the 20 shipped queries (144..5478 aa, sum 41,752) as one batch
 against the same database (configs[2]); --config c4: P07327 against a
-50,000,000-subject database split over the ranks (configs[3]; strong
-scaling), each rank's shard generated in its GPU's HBM from (seed, global
-id) by the counter-based generator (sw_db_create_synthetic); --config c5: a
+50,000,000-subject database split over the ranks by id range (configs[3]),
+each rank's shard generated in its GPU's HBM from (seed, global id) by the
+counter-based generator (sw_db_create_synthetic); --config c5: a
 5,000-residue synthetic query against 10,000 subjects of N(2000, 200)
-residues (configs[4]).  These are the other BASELINE configurations,
-measured with the same code; the driver's headline is the default (c2).
+residues (configs[4]); --config c1: P02232 (144 aa) against 1,000 synthetic
+subjects on the CPU restatement of cpu.cpp's recurrence at one thread and at
+every host core, the literal cpu.cpp beside it (configs[0]; no GPU timing in
+`value`).
 
 One step = one pass of the hot path over the rank's resident shard: build the
 query profile(s), run the scan kernels (intra-sequence for subjects longer
 than the long threshold, inter-sequence for the rest), then the top-K
-exchange (device top-K per query, RCCL all-gather of K (score, id) keys per
-rank, device merge).
+exchange (device top-K per query, RCCL all-gather of K (score, global id)
+keys per rank, device merge).
 
-Multi-GPU (torchrun, one process per GPU): every rank holds its OWN shard of
-the same size (weak scaling; shard = the rank's seed), so the global database
-grows with N (config C4's pattern).  value = all cells processed by all ranks
-/ the max-over-ranks time of K steps.
+Multi-GPU (torchrun, one process per GPU) is STRONG scaling: every rank
+builds the same database and scans only its residue-balanced share (LPT over
+subject lengths, dist.shard_indices; C4: an id range), so N GPUs search one
+database of fixed size.  value = all cells of the database / the max-over-
+ranks time of K steps.  After timing, every rank re-scores its share with
+the CPU oracle (all of it when that fits --verify-seconds, else a random
+sample plus its top-K hits), checks its device top-K against a CPU top-K of
+its scores, and rank 0 checks the RCCL-merged top-K against the merge of
+the oracle's per-rank top-K (the bit-exact top-score list of north_star);
+--shard-of N --shard-rank R measures rank R's share of N GPUs on one GPU.
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import hashlib
 import json
+import math
 import os
+import subprocess
 import sys
 import time
 
@@ -73,9 +84,6 @@ VALU_MODEL = {
     # per 2 x 64 cells: 4.53 v_pk_max_i16, 2.65 v_pk_sub_u16, 0.94 v_pk_mad_u16
     "sw_inter_x2p<32,8,affine>": (8.117 * 4.25) / 128,
     "sw_inter_x2s<32,8,affine>": (8.117 * 4.25) / 128,
-    "sw_inter_x2s<48,4,linear>": (4.688 * 4.25) / 128,
-    "sw_inter_x2<32,8,affine>": ((4.83 + 2.83 + 1) * 4.25 + 2.7) / 128,
-    "sw_inter_x2<16,16,affine>": ((4.87 + 2.87 + 1) * 4.25 + 2.7) / 128,
     # per 64 cells: 1.5 v_max3, 1 v_add_sdwa, 1 v_sub clamp
     "sw_inter<64,8,linear>": (1.5 * 4.4 + 4.2 + 2.45) / 64,
     # per 64 cells: 2.82 v_sub clamp, 1.83 v_max, 1.5 v_max3, 1 v_add_sdwa
@@ -95,6 +103,10 @@ C4_TOTAL = 50_000_000
 C3_QUERIES = ["P02232", "P05013", "P14942", "P07327", "P01008", "P03435", "P42357", "P21177",
               "Q38941", "P27895", "P07756", "P04775", "P19096", "P28167", "P0C6B8", "P20930",
               "P08519", "Q7TMA5", "P33450", "Q9UKN1"]
+# sources whose change can change the dominant kernel's HBM traffic: a stored
+# rocprofv3 --pmc measurement (pmc_traffic.json) is only reported for the
+# build it was taken on
+KERNEL_SOURCES = ["sw_inter_x2.hip", "sw_intra_x2.hip", "sw_kernels.hip", "sw_kernels.h", "sw_capi.cpp"]
 
 
 def log(*a):
@@ -106,8 +118,41 @@ def read_query(name):
         return "".join(f.read().split("\n")[1:])
 
 
+def kernel_source_hash():
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES:
+        with open(os.path.join(REPO, "ece1782-smith-waterman-cuda_amd", "csrc", name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def workload_key(args, qlen):
     return "%s/%d/%d/%s-%d-%d" % (args.query, args.db_seqs, qlen, args.matrix, args.gap_open, args.gap_extend)
+
+
+def host_cores():
+    """(cores this process may use, logical CPUs in its affinity mask, the
+    cgroup CPU quota in cores or None).  GPU boxes show the whole host's CPUs
+    in the mask; the quota is the share actually granted."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                p = int(f.read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    eff = aff if quota is None else max(1, min(aff, int(math.ceil(quota))))
+    return eff, aff, quota
 
 
 def valu_roofline(kernel, cells_rank, scan_ms, kernel_gcups):
@@ -125,8 +170,11 @@ def valu_roofline(kernel, cells_rank, scan_ms, kernel_gcups):
 
 
 def host_sampler(res, offs):
-    """Subjects idx of a host-generated shard as (residues, offsets)."""
+    """Subjects idx of a host-resident shard as (residues, offsets)."""
     def take(idx):
+        idx = np.asarray(idx, dtype=np.int64)
+        if len(idx) == len(offs) - 1:
+            return res, offs
         lens = offs[idx + 1] - offs[idx]
         so = np.zeros(len(idx) + 1, dtype=np.int64)
         so[1:] = np.cumsum(lens)
@@ -151,83 +199,247 @@ def counter_sampler(sw, seed, id_base):
     return take
 
 
-def cpu_baseline(sw, queries, sampler, n, gpu_scores, seconds, threads, scoring):
-    """The oracle (C restatement of cpu.cpp's recurrence, Gotoh for affine;
-    kind "port") on a bounded random sample of the same shard, every query of
-    the workload, on this host's cores, with the same scoring as the GPU run.
-    sampler(idx) -> (residues, offsets) of shard subjects idx; gpu_scores:
-    [nq][n] scores of the measured run (parity check)."""
-    mat, go, ge = scoring
+def oracle_scan(queries, sr, so, scoring, threads):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import sw_oracle
+    mat, go, ge = scoring
+    return [sw_oracle.scan(q, sr, so, mat=mat, gap_open=go, gap_extend=ge, nthreads=threads) for q in queries]
+
+
+def cpu_baseline(queries, sampler, n, gpu_scores, seconds, threads, scoring, one_thread_seconds):
+    """The oracle (C restatement of cpu.cpp's recurrence, Gotoh for affine;
+    kind "port") on a bounded random sample of the same shard, every query of
+    the workload, with the same scoring as the GPU run: at `threads` threads
+    (the cores this process may use) and at one thread.  sampler(idx) ->
+    (residues, offsets) of shard subjects idx; gpu_scores: [nq][n] scores of
+    the measured run (parity check of the sample)."""
     rng = np.random.default_rng(1782)
     perm = rng.permutation(n)
+    qtot = sum(len(q) for q in queries)
 
-    def sample(m):
+    def timed(m, nt):
         idx = np.sort(perm[:m])
         sr, so = sampler(idx)
-        return idx, sr, so
-
-    def run(sr, so):
-        return [sw_oracle.scan(q, sr, so, mat=mat, gap_open=go, gap_extend=ge, nthreads=threads) for q in queries]
-
-    # calibrate on growing samples until one takes >= 0.5 s (thread start-up
-    # dominates tiny samples), then size the real one to ~`seconds`
-    m0 = min(n, 200)
-    while True:
-        idx, sr, so = sample(m0)
         t = time.perf_counter()
-        run(sr, so)
-        dt = max(time.perf_counter() - t, 1e-3)
-        if dt >= 0.5 or m0 >= n:
-            break
-        m0 = min(n, m0 * 4)
-    m = int(min(n, max(m0, m0 * seconds / dt)))
-    idx, sr, so = sample(m)
-    t = time.perf_counter()
-    cpu = run(sr, so)
-    dt = time.perf_counter() - t
-    qtot = sum(len(q) for q in queries)
+        out = oracle_scan(queries, sr, so, scoring, nt)
+        return idx, so, out, time.perf_counter() - t
+
+    def sized(nt, budget):
+        # calibrate on growing samples until one takes >= 0.3 s (thread
+        # start-up dominates tiny samples), then size the real one to budget
+        m0 = min(n, 50)
+        while True:
+            idx, so, out, dt = timed(m0, nt)
+            if dt >= 0.3 or m0 >= n:
+                break
+            m0 = min(n, m0 * 4)
+        m = int(min(n, max(m0, m0 * budget / max(dt, 1e-3))))
+        return timed(m, nt) if m != m0 else (idx, so, out, dt)
+
+    idx, so, cpu, dt = sized(threads, seconds)
     cells = qtot * int(so[-1])
     parity = all(bool(np.array_equal(c, gpu_scores[k][idx])) for k, c in enumerate(cpu))
+    idx1, so1, cpu1, dt1 = sized(1, one_thread_seconds)
+    cells1 = qtot * int(so1[-1])
+    parity = parity and all(bool(np.array_equal(c, gpu_scores[k][idx1])) for k, c in enumerate(cpu1))
     return {"value": round(cells / dt / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": "port",
+            "one_thread": round(cells1 / dt1 / 1e9, 4),
             "sample": "%d of %d subjects (%d residues) of rank 0's shard x %d quer%s (%d residues), %.3g cells, "
-                      "%.1f s on %d threads; scores equal to the GPU's: %s"
-                      % (m, n, int(so[-1]), len(queries), "y" if len(queries) == 1 else "ies", qtot, cells, dt,
-                         threads, parity)}, parity
+                      "%.1f s on %d threads; one thread: %d subjects, %.3g cells, %.1f s; scores equal to the "
+                      "GPU's: %s" % (len(idx), n, int(so[-1]), len(queries), "y" if len(queries) == 1 else "ies",
+                                     qtot, cells, dt, threads, len(idx1), cells1, dt1, parity)}, parity
 
 
-def make_workload(sw, args, rank):
-    """(queries [code arrays], query names, residues, offsets, description)."""
-    if args.config == "c2":
-        res, offs = sw.synth.database(args.db_seqs, shard=rank)
-        return [sw.encode(read_query(args.query))], [args.query], res, offs, \
-            "C2: query %s (%d aa) vs synthetic Swiss-Prot-sized db" % (args.query, len(read_query(args.query)))
+def verify(sw, dist, world, rank, queries, sampler, n, gids, gpu_scores, dev_top, final, K, scoring, threads,
+           seconds, backend):
+    """Parity of the measured run at any N (outside the timed region).
+
+    Every rank: (1) its device top-K == a CPU top-K of its GPU scores (global
+    ids, score desc / id asc); (2) the oracle re-scores its share (all of it
+    if the estimate fits `seconds`, else a random sample) and every score must
+    be equal; its top-K hits are re-scored too.  Rank 0: (3) when every rank
+    scored its whole share, the RCCL-merged top-K must equal the merge of the
+    per-rank ORACLE top-K (the bit-exact top-score list); otherwise the merge
+    of the per-rank CPU top-K of the GPU scores."""
+    nq = len(queries)
+    qtot = sum(len(q) for q in queries)
+    ok_topk = all(np.array_equal(dev_top[k], sw.dist.local_topk(gpu_scores[k], gids, K)) for k in range(nq))
+    # the rank's top-K hits (local indices) are always re-scored
+    pos = {int(g): i for i, g in enumerate(gids)} if len(gids) else {}
+    hit_local = set()
+    for k in range(nq):
+        ids, _ = sw.capi.decode_keys(dev_top[k])
+        hit_local.update(pos[int(g)] for g in ids if g >= 0)
+    # estimate the oracle's rate from a small calibration sample
+    rng = np.random.default_rng(1782 + rank)
+    perm = rng.permutation(n)
+    m0 = min(n, 256)
+    cal = np.sort(perm[:m0])
+    sr, so = sampler(cal)
+    t = time.perf_counter()
+    oracle_scan(queries, sr, so, scoring, threads)
+    rate = qtot * int(so[-1]) / max(time.perf_counter() - t, 1e-4)
+    res_total = None
+    try:
+        _, offs = sampler.full
+        res_total = int(offs[-1])
+    except AttributeError:
+        pass
+    full = res_total is not None and qtot * res_total / rate <= seconds
+    if full:
+        idx = np.arange(n)
+    else:
+        m = int(min(n, max(m0, m0 * seconds / max(qtot * int(so[-1]) / rate, 1e-4))))
+        idx = np.unique(np.concatenate([perm[:m], np.fromiter(hit_local, dtype=np.int64, count=len(hit_local))]))
+    sr, so = sampler(idx)
+    t = time.perf_counter()
+    cpu = oracle_scan(queries, sr, so, scoring, threads)
+    dt = time.perf_counter() - t
+    ok_scores = all(bool(np.array_equal(c, gpu_scores[k][idx])) for k, c in enumerate(cpu))
+    # per-rank top-K keys: of the oracle's scores (whole share) or of the GPU's
+    src = cpu if full else gpu_scores
+    sel = gids[idx] if full else gids
+    mine = np.stack([_pad_keys(sw.dist.local_topk(src[k], sel, K), K) for k in range(nq)])
+    checked = np.array([len(idx), n, int(full), int(ok_topk), int(ok_scores)], dtype=np.int64)
+    if world > 1:
+        allkeys = dist.allgather_np(mine)
+        allchk = dist.allgather_np(checked)
+    else:
+        allkeys = mine[None]
+        allchk = checked[None]
+    merged_ok = all(np.array_equal(sw.dist.merge_topk([allkeys[r][k] for r in range(world)], K),
+                                   final[k][final[k] != np.iinfo(np.int64).min]) for k in range(nq))
+    all_full = bool(allchk[:, 2].all())
+    res = {"subjects_checked": int(allchk[:, 0].sum()), "subjects": int(allchk[:, 1].sum()),
+           "whole_database": all_full,
+           "rank_topk_equal_cpu_topk": bool(allchk[:, 3].all()),
+           "scores_equal_oracle": bool(allchk[:, 4].all()),
+           "merged_topk_equal": merged_ok,
+           "merged_topk_reference": ("merge of the per-rank oracle top-%d (every subject re-scored)" % K)
+           if all_full else ("merge of the per-rank CPU top-%d of the GPU scores (oracle sample)" % K),
+           "oracle_threads_per_rank": threads, "oracle_seconds_rank0": round(dt, 2),
+           "cells_checked_rank0": float(qtot * int(so[-1]))}
+    ok = res["rank_topk_equal_cpu_topk"] and res["scores_equal_oracle"] and merged_ok
+    return res, ok
+
+
+def _pad_keys(keys, K):
+    out = np.full(K, np.iinfo(np.int64).min, dtype=np.int64)
+    out[:len(keys)] = keys[:K]
+    return out
+
+
+def c1_main(args):
+    """configs[0]: P02232 (144 aa) vs 1,000 synthetic subjects on the CPU
+    reference path — the oracle at one thread and at every core this process
+    may use, the literal cpu.cpp (oracle/_ref/cpu_ref, +/-3 scoring, prints
+    its matrices) on a few pairs beside it, and the GPU on the same database
+    for comparison.  value = the oracle at all cores (the reference path)."""
+    import _swpkg
+    sw = _swpkg.load()
+    eff, aff, quota = host_cores()
+    threads = args.cpu_threads or eff
+    q = sw.encode(read_query("P02232"))
+    res, offs = sw.synth.database(args.db_seqs or 1000, shard=0)
+    n = len(offs) - 1
+    scoring = (sw.capi.builtin_matrix(0), 2, 2)
+    cells = float(len(q)) * int(offs[-1])
+
+    def rate(nt, reps):
+        best = 1e30
+        for _ in range(reps):
+            t = time.perf_counter()
+            out = oracle_scan([q], res, offs, scoring, nt)[0]
+            best = min(best, time.perf_counter() - t)
+        return out, cells / best / 1e9, best
+
+    want, r1, t1 = rate(1, 3)
+    _, rall, tall = rate(threads, 5)
+    out = {"metric": METRIC, "value": round(rall, 3), "unit": "GCUPS", "n_gpus": 0, "steps": 5, "warmup": 0,
+           "ms_per_step": round(tall * 1e3, 3), "higher_is_better": True, "scaling": "none",
+           "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+           "config": {"workload": "C1: P02232 (144 aa) vs %d synthetic subjects (%d residues), BLOSUM50 "
+                                  "(SWSolver.cu:54-81) linear gap 2, CPU restatement of cpu.cpp:43-74" % (n, offs[-1]),
+                      "config": "c1", "cells": cells},
+           "cpu_baseline": {"value": round(rall, 3), "unit": "GCUPS", "cores": threads, "kind": "port",
+                            "one_thread": round(r1, 4),
+                            "sample": "the whole C1 database, best of 5 runs at %d threads, best of 3 at one "
+                                      "thread" % threads},
+           "host": {"cores_used": threads, "affinity_cpus": aff, "cgroup_quota_cpus": quota}}
+    ref = os.path.join(REPO, "oracle", "_ref", "cpu_ref")
+    if os.path.exists(ref):
+        # the literal cpu.cpp: one pair per process, +/-3 scoring, prints
+        # its alignment and both matrices (to /dev/null here)
+        letters = "ARNDCQEGHILKMFPSTWYVBJZX*"
+        qs = "".join(letters[c] for c in q)
+        npairs = min(n, 40)
+        c = 0
+        t = time.perf_counter()
+        for k in range(npairs):
+            s = "".join(letters[x] for x in res[offs[k]:offs[k + 1]])
+            subprocess.run([ref, qs, s], stdout=subprocess.DEVNULL, check=True)
+            c += len(q) * len(s)
+        dt = time.perf_counter() - t
+        out["reference_cpu_cpp"] = {"value": round(c / dt / 1e9, 5), "unit": "GCUPS", "cores": 1,
+                                    "kind": "reference",
+                                    "sample": "oracle/_ref/cpu_ref (built from the untouched cpu.cpp) on the first "
+                                              "%d pairs, +/-3 scoring as cpu.cpp hard-codes, one process per pair "
+                                              "printing its matrices to /dev/null: %.3g cells in %.2f s" % (npairs, c, dt)}
+    if not args.no_gpu:
+        h = sw.Handle(0)
+        db = sw.Database(h, res, offs)
+        got = db.scan(q, *scoring)
+        best = 1e30
+        for _ in range(5):
+            t = time.perf_counter()
+            db.scan(q, *scoring)
+            best = min(best, time.perf_counter() - t)
+        out["gpu_same_workload"] = {"value": round(cells / best / 1e9, 2), "unit": "GCUPS",
+                                    "note": "synchronous sw_scan incl. profile upload and D2H of %d scores, "
+                                            "best of 5 (latency-bound at this size)" % n}
+        out["parity_sample_ok"] = bool(np.array_equal(got, want))
+        db.close()
+        h.close()
+    print(json.dumps(out), flush=True)
+
+
+def make_workload(sw, args, world, rank):
+    """(queries, query names, residues, offsets, global ids, description, full
+    database) for this rank's share of ONE database."""
     if args.config == "c4":
-        return [sw.encode(read_query(args.query))], [args.query], None, None, \
+        return [sw.encode(read_query(args.query))], [args.query], None, None, None, \
             "C4: query %s (%d aa) vs a %d-subject synthetic db generated on the devices" % (
-                args.query, len(read_query(args.query)), C4_TOTAL)
-    if args.config == "c3":
-        res, offs = sw.synth.database(args.db_seqs, shard=rank)
-        qs = [sw.encode(read_query(n)) for n in C3_QUERIES]
-        return qs, C3_QUERIES, res, offs, \
-            "C3: batch of the %d shipped queries (%d..%d aa, sum %d) vs synthetic Swiss-Prot-sized db" % (
-                len(qs), min(map(len, qs)), max(map(len, qs)), sum(map(len, qs)))
-    # c5: one 5,000-residue query vs 10,000 subjects of N(2000, 200)
-    res, offs = sw.synth.fixed_length_database(args.db_seqs, 2000, 200, shard=rank)
-    return [sw.synth.query(5000)], ["synthetic-5000"], res, offs, \
-        "C5: synthetic 5000-aa query vs N(2000, 200)-residue subjects"
+                args.query, len(read_query(args.query)), C4_TOTAL), None
+    if args.config in ("c2", "c3"):
+        res, offs = sw.synth.database(args.db_seqs, shard=0)
+    else:  # c5: one 5,000-residue query vs 10,000 subjects of N(2000, 200)
+        res, offs = sw.synth.fixed_length_database(args.db_seqs, 2000, 200, shard=0)
+    gids, r_res, r_offs = sw.dist.shard(res, offs, rank, world)
+    if args.config == "c2":
+        qs, names = [sw.encode(read_query(args.query))], [args.query]
+        desc = "C2: query %s (%d aa) vs synthetic Swiss-Prot-sized db" % (args.query, len(qs[0]))
+    elif args.config == "c3":
+        qs, names = [sw.encode(read_query(n)) for n in C3_QUERIES], C3_QUERIES
+        desc = "C3: batch of the %d shipped queries (%d..%d aa, sum %d) vs synthetic Swiss-Prot-sized db" % (
+            len(qs), min(map(len, qs)), max(map(len, qs)), sum(map(len, qs)))
+    else:
+        qs, names = [sw.synth.query(5000)], ["synthetic-5000"]
+        desc = "C5: synthetic 5000-aa query vs N(2000, 200)-residue subjects"
+    return qs, names, r_res, r_offs, gids, desc, (res, offs)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"],
-                    help="c2 = the headline (BASELINE configs[1]); c3 / c4 / c5 = configs[2] / [3] / [4]")
-    ap.add_argument("--steps", type=int, default=None, help="default 10 (c2, c5) / 3 (c3)")
-    ap.add_argument("--warmup", type=int, default=None, help="default 2 (c2, c5) / 1 (c3)")
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"],
+                    help="c2 = the headline (BASELINE configs[1]); c1 / c3 / c4 / c5 = configs[0] / [2] / [3] / [4]")
+    ap.add_argument("--steps", type=int, default=None, help="default 100 (c2, c5) / 3 (c3, c4)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 5 (c2, c5) / 1 (c3, c4)")
     ap.add_argument("--db-seqs", type=int, default=None,
-                    help="subjects per rank (default 570000; c4: 50M / ranks; c5: 10000)")
+                    help="subjects of the WHOLE database (default 570000; c1: 1000; c4: 50M; c5: 10000)")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="measure one rank's share of this many GPUs on this GPU (strong-scaling rehearsal)")
+    ap.add_argument("--shard-rank", type=int, default=0)
     ap.add_argument("--query", default="P07327")
     ap.add_argument("--topk", type=int, default=100)
     ap.add_argument("--matrix", default="blosum62", choices=sorted(MATRICES))
@@ -236,9 +448,13 @@ def main():
     ap.add_argument("--no-reference-scoring", action="store_true",
                     help="skip the second timed loop with the reference's BLOSUM50 / linear 2")
     ap.add_argument("--long-threshold", type=int, default=0, help="0 = library default")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify-seconds", type=float, default=15.0,
+                    help="oracle budget per rank for the parity leg (whole share if it fits)")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-gpu", action="store_true", help="c1: skip the GPU comparison")
     # the latest rocprofv3 --pmc measurement of the C2 launch (FETCH_SIZE x2 +
     # WRITE_SIZE, scripts/pmc_traffic.py); kept at the root because profiles/
     # does not travel to the GPU box
@@ -247,36 +463,43 @@ def main():
                     help="gloo = rehearse the multi-rank path on one GPU (CPU collectives)")
     ap.add_argument("--device", type=int, default=None, help="override the GPU index (rehearsal)")
     args = ap.parse_args()
+    if args.config == "c1":
+        return c1_main(args)
     if args.steps is None:
-        args.steps = 3 if args.config == "c3" else 10
+        args.steps = 3 if args.config in ("c3", "c4") else 100
     if args.warmup is None:
-        args.warmup = 1 if args.config == "c3" else 2
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+        args.warmup = 1 if args.config in ("c3", "c4") else 5
     if args.db_seqs is None:
-        args.db_seqs = {"c5": 10000, "c4": -(-C4_TOTAL // world_env)}.get(args.config, 570000)
+        args.db_seqs = {"c5": 10000, "c4": C4_TOTAL}.get(args.config, 570000)
 
     import torch
-    import torch.distributed as dist
+    import torch.distributed as tdist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    # the database is split over shard_world ranks; this process scans share
+    # shard_rank (= its rank, or the rehearsed one with --shard-of)
+    shard_world, shard_rank = (args.shard_of, args.shard_rank) if args.shard_of else (world, rank)
+    if args.shard_of and world > 1:
+        raise SystemExit("--shard-of is a one-process rehearsal")
     gpu = local if args.device is None else args.device
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     if world > 1:
         if args.backend == "nccl":
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+            tdist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
+            tdist.init_process_group("gloo", rank=rank, world_size=world)
 
     import _swpkg
     sw = _swpkg.load()
 
     t0 = time.perf_counter()
-    queries, qnames, res, offs, desc = make_workload(sw, args, rank)
+    queries, qnames, res, offs, gids, desc, full_db = make_workload(sw, args, shard_world, shard_rank)
     nq = len(queries)
     qtot = sum(len(q) for q in queries)
 
@@ -287,28 +510,34 @@ def main():
     stream = torch.cuda.Stream(dev)
     handle.set_stream(stream.cuda_stream)
     torch.cuda.set_stream(stream)
-    if res is None:  # c4: the shard is generated in this GPU's HBM
-        id_base = rank * args.db_seqs
-        db = sw.Database.synthetic(handle, SEED, args.db_seqs, id_base=id_base,
+    if res is None:  # c4: an id range of the database, generated in this GPU's HBM
+        per = -(-args.db_seqs // shard_world)
+        id_base = shard_rank * per
+        n_mine = max(0, min(per, args.db_seqs - id_base))
+        db = sw.Database.synthetic(handle, SEED, n_mine, id_base=id_base,
                                    long_threshold=(args.long_threshold or None))
         lens, _ = db.subjects()
         offs = np.zeros(len(lens) + 1, dtype=np.int64)
         offs[1:] = np.cumsum(lens)
         sampler = counter_sampler(sw, SEED, id_base)
+        gids = np.arange(id_base, id_base + n_mine, dtype=np.int32)
     else:
         db = sw.Database(handle, res, offs, long_threshold=(args.long_threshold or None))
         sampler = host_sampler(res, offs)
+        sampler.full = (res, offs)
+        id_base = None
     n = len(offs) - 1
     residues = int(offs[-1])
     st = db.stats()
-    log("rank %d: shard %d subjects, %d residues, generated + packed + resident in %.1fs: %s"
-        % (rank, n, residues, time.perf_counter() - t0, st))
+    log("rank %d: share %d/%d: %d subjects, %d residues, generated + packed + resident in %.1fs: %s"
+        % (rank, shard_rank, shard_world, n, residues, time.perf_counter() - t0, st))
 
-    scores = torch.zeros((nq, n), dtype=torch.int32, device=dev)
-    K = min(args.topk, n)
+    scores = torch.zeros((nq, max(n, 1)), dtype=torch.int32, device=dev)
+    K = args.topk
     top = torch.empty((nq, K), dtype=torch.int64, device=dev)
     gathered = torch.empty((world, nq, K), dtype=torch.int64, device=dev)
     final = torch.empty((nq, K), dtype=torch.int64, device=dev)
+    gid_dev = torch.from_numpy(gids).to(dev) if id_base is None else None
 
     mat = sw.capi.builtin_matrix(MATRICES[args.matrix])
     scoring = (mat, args.gap_open, args.gap_extend)
@@ -320,14 +549,17 @@ def main():
             db.scan_batch_device(queries, scores.data_ptr(), *scoring)
         # device top-K per query: int64 keys (score << 32 | 2^31-1-global id), best first
         for k in range(nq):
-            handle.topk_device(scores[k].data_ptr(), n, K, top[k].data_ptr(), id_base=rank * n)
+            if gid_dev is not None:
+                handle.topk_device_ids(scores[k].data_ptr(), n, gid_dev.data_ptr(), K, top[k].data_ptr())
+            else:
+                handle.topk_device(scores[k].data_ptr(), n, K, top[k].data_ptr(), id_base=id_base)
         if world == 1:
             return
         if args.backend == "nccl":
-            dist.all_gather_into_tensor(gathered, top)  # RCCL over xGMI: nq x K x 8 B per rank
+            tdist.all_gather_into_tensor(gathered, top)  # RCCL over xGMI: nq x K x 8 B per rank
         else:
             parts = [torch.empty((nq, K), dtype=torch.int64) for _ in range(world)]
-            dist.all_gather(parts, top.cpu())
+            tdist.all_gather(parts, top.cpu())
             gathered.copy_(torch.stack(parts))
         for k in range(nq):
             merged = gathered[:, k, :].contiguous()
@@ -343,7 +575,7 @@ def main():
             step()
         torch.cuda.synchronize()
         if world > 1:
-            dist.barrier()
+            tdist.barrier()
         torch.cuda.synchronize()
         handle.timing_reset()
         t_start = time.perf_counter()
@@ -351,7 +583,7 @@ def main():
             step()
         torch.cuda.synchronize()
         if world > 1:
-            dist.barrier()
+            tdist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t_start
         kt = handle.timing_total()
@@ -359,8 +591,8 @@ def main():
             t = torch.tensor([elapsed, cells_rank], dtype=torch.float64,
                              device=dev if args.backend == "nccl" else "cpu")
             tmax = t.clone()
-            dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            tdist.all_reduce(tmax, op=tdist.ReduceOp.MAX)
+            tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
             return float(tmax[0]), float(t[1]), kt, (handle.last_kernel(), handle.last_intra_kernel())
         return elapsed, cells_rank, kt, (handle.last_kernel(), handle.last_intra_kernel())
 
@@ -368,7 +600,9 @@ def main():
     st = db.stats()  # the coop split of the timed scans
     final_keys = (final if world > 1 else top).cpu().numpy()
     top_ids, top_scores = sw.capi.decode_keys(final_keys[0])
-    gs = scores.cpu().numpy() if (not args.no_cpu_baseline and world == 1 and rank == 0) else None
+    # the measured run's scores and keys, for the parity leg
+    gs = scores.cpu().numpy()[:, :n]
+    dev_top = top.cpu().numpy()
 
     ref = None
     if not args.no_reference_scoring:
@@ -383,6 +617,15 @@ def main():
                                       "sw_inter_coop": round(r_kt["coop_ms"] / r_n, 4),
                                       "sw_intra": round(r_kt["intra_ms"] / r_n, 4),
                                       "scan_total": round(r_kt["total_ms"] / r_n, 4)}}
+        scoring = (mat, args.gap_open, args.gap_extend)
+
+    eff, aff, quota = host_cores()
+    # the parity leg runs on every rank at once: split this host's cores
+    vthreads = max(1, (args.cpu_threads or eff) // max(1, local_world))
+    verify_res, verify_ok = None, None
+    if not args.no_verify:
+        verify_res, verify_ok = verify(sw, sw.dist, world, rank, queries, sampler, n, gids, gs, dev_top, final_keys,
+                                       K, scoring, vthreads, args.verify_seconds, args.backend)
 
     if rank == 0:
         value = cells_all * args.steps / elapsed_max / 1e9
@@ -420,13 +663,19 @@ def main():
             kernel_ms = intra_ms
             wave_gcups = float(qtot) / nq * intra_res / (intra_ms * 1e-3) / 1e9 if intra_ms > 0 else 0.0
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
-        traffic = None
+        traffic, traffic_note = None, "no rocprofv3 --pmc measurement of this workload and build"
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if (args.config == "c2" and tj.get("workload_key") == workload_key(args, qtot)
-                    and tj.get("kernel") == roof_kernel):
-                traffic = tj.get("hbm_bytes_per_launch")
+            if (args.config == "c2" and not args.shard_of and world == 1
+                    and tj.get("workload_key") == workload_key(args, qtot) and tj.get("kernel") == roof_kernel):
+                if tj.get("kernel_src_sha16") == kernel_source_hash():
+                    traffic = tj.get("hbm_bytes_per_launch")
+                    traffic_note = ("stored rocprofv3 --pmc measurement (FETCH_SIZE x2 + WRITE_SIZE) of this "
+                                    "workload, taken on a build with the same kernel sources (%s, %s)"
+                                    % (tj.get("kernel_src_sha16"), tj.get("measured", "?")))
+                else:
+                    traffic_note = "stored PMC measurement is of other kernel sources; not reported"
         except (OSError, ValueError):
             pass
         out = {
@@ -438,7 +687,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "strong" if args.config == "c4" else "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": ("fp16" if ("fp16" in roof_kernel or "intra_x2" in roof_kernel)
                       else "int16" if "_x2" in roof_kernel else "int32"),
@@ -447,46 +696,55 @@ def main():
                           "scores are bit-exact int32",
             "data": "synthetic",
             "config": {
-                "workload": "%s, %d subjects/rank (%d residues/rank), %s, gap open %d / extend %d%s, top-%d "
-                            "all-gathered" % (desc, n, residues, args.matrix.upper(), args.gap_open,
-                                              args.gap_extend,
-                                              " (BLAST 11/1)" if (args.gap_open, args.gap_extend) == (12, 1) else "",
-                                              K),
+                "workload": "%s, %d subjects (%d on this rank's share, %d residues), %s, gap open %d / extend "
+                            "%d%s, top-%d all-gathered" % (
+                                desc, args.db_seqs, n, residues, args.matrix.upper(), args.gap_open,
+                                args.gap_extend,
+                                " (BLAST 11/1)" if (args.gap_open, args.gap_extend) == (12, 1) else "", K),
                 "config": args.config,
                 "scoring": {"matrix": args.matrix, "gap_open": args.gap_open, "gap_extend": args.gap_extend},
                 "queries": qnames if nq > 1 else qnames[0], "query_residues": int(qtot),
-                "subjects_per_rank": n, "residues_per_rank": residues,
+                "database_subjects": args.db_seqs,
+                "subjects_rank0": n, "residues_rank0": residues,
+                "sharding": ("id range of the database per rank" if args.config == "c4" else
+                             "LPT over subject lengths (residue-balanced) of one database"),
                 "parallelism": "db-shard x%d + RCCL allgather top-K" % world,
-                "long_threshold": st["long_threshold"], "long_subjects": st["n_long"],
+                "long_threshold": st["long_threshold"], "long_subjects_rank0": st["n_long"],
                 "cells_per_step": cells_all,
             },
             "kernel_ms_per_scan": {"inter_phase": round(inter_ms, 4), "sw_inter": round(wave_ms, 4),
                                    "sw_inter_coop": round(coop_ms, 4), "sw_intra": round(intra_ms, 4),
                                    "scan_total": round(kt["total_ms"] / nsc, 4)},
-            "cells_split_per_step": {"sw_inter": float(qtot) * wave_res,
-                                     "sw_inter_coop": float(qtot) * side_res,
-                                     "sw_intra": float(qtot) * (residues - inter_res)},
+            "cells_split_per_step_rank0": {"sw_inter": float(qtot) * wave_res,
+                                           "sw_inter_coop": float(qtot) * side_res,
+                                           "sw_intra": float(qtot) * (residues - inter_res)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                         "traffic": traffic,
+                         "traffic": traffic, "traffic_note": traffic_note,
                          "kernel": roof_kernel,
                          "alg_bytes_per_launch": int(alg_bytes), "kernel_ms": round(kernel_ms, 4)},
             "valu_roofline": valu_roofline(roof_kernel, cells_all / world, kt["total_ms"] / nsc * nq, wave_gcups),
             "kernels": {"inter": kernel, "intra": intra_kernel},
             "top_hit": {"id": int(top_ids[0]), "score": int(top_scores[0])},
+            "host": {"cores_used": args.cpu_threads or eff, "affinity_cpus": aff, "cgroup_quota_cpus": quota},
         }
+        if args.shard_of:
+            out["rehearsal"] = "rank %d's share of %d GPUs measured alone on one GPU" % (shard_rank, shard_world)
         if ref is not None:
             out["reference_scoring"] = ref
-        if gs is not None:
-            threads = min(args.cpu_threads, os.cpu_count() or 1)
-            cb, parity = cpu_baseline(sw, queries, sampler, n, gs, args.cpu_seconds, threads,
-                                      scoring=(mat, args.gap_open, args.gap_extend))
+        if verify_res is not None:
+            out["parity"] = verify_res
+            out["parity_sample_ok"] = verify_ok
+        if not args.no_cpu_baseline and world == 1 and not args.shard_of:
+            threads = args.cpu_threads or eff
+            cb, cparity = cpu_baseline(queries, sampler, n, gs, args.cpu_seconds, threads, scoring,
+                                       args.cpu_seconds / 2)
             out["cpu_baseline"] = cb
-            out["parity_sample_ok"] = parity
+            out["parity_sample_ok"] = bool(cparity and out.get("parity_sample_ok", True))
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+        tdist.barrier()
+        tdist.destroy_process_group()
     db.close()
     handle.close()
 

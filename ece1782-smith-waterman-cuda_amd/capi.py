@@ -28,7 +28,7 @@ EXPORTED = (
     "sw_db_create", "sw_db_free", "sw_db_get_stats", "sw_db_set_long_threshold",
     "sw_scan", "sw_scan_device", "sw_scan_batch", "sw_scan_batch_device", "sw_get_timing",
     "sw_timing_reset", "sw_timing_total", "sw_last_kernel", "sw_last_intra_kernel",
-    "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_score_pair", "sw_align",
+    "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_topk_device_ids", "sw_score_pair", "sw_align",
     "sw_db_save", "sw_db_load", "sw_db_subjects", "sw_db_create_synthetic", "sw_synth_tables",
     "sw_synth_lengths",
 )
@@ -125,6 +125,7 @@ def lib():
         "sw_topk": (ctypes.c_int, [i32p, i64, i32, i32p, i32p]),
         "sw_topk_device": (ctypes.c_int, [vp, vp, i64, i64, i32, vp]),
         "sw_topk_keys_device": (ctypes.c_int, [vp, vp, i64, i32, vp]),
+        "sw_topk_device_ids": (ctypes.c_int, [vp, vp, i64, vp, i32, vp]),
         "sw_score_pair": (ctypes.c_int, [vp, u8p, i32, u8p, i32, ctypes.POINTER(Scoring), i32p]),
     }
     for name, (res, args) in sig.items():
@@ -237,6 +238,11 @@ class Handle:
         """Asynchronous device top-k into an int64 key buffer (best first)."""
         _check(lib().sw_topk_device(self._h, ctypes.c_void_p(scores_dev_ptr), n, id_base, k,
                                     ctypes.c_void_p(keys_out_dev_ptr)))
+
+    def topk_device_ids(self, scores_dev_ptr, n, ids_dev_ptr, k, keys_out_dev_ptr):
+        """Device top-k with global ids from a device int32 id map."""
+        _check(lib().sw_topk_device_ids(self._h, ctypes.c_void_p(scores_dev_ptr), n, ctypes.c_void_p(ids_dev_ptr),
+                                        k, ctypes.c_void_p(keys_out_dev_ptr)))
 
     def topk_keys_device(self, keys_dev_ptr, n, k, keys_out_dev_ptr):
         _check(lib().sw_topk_keys_device(self._h, ctypes.c_void_p(keys_dev_ptr), n, k,

@@ -598,14 +598,13 @@ struct Profiles {
     int8_t* dev = nullptr;  // device copy of this scan's profiles
     int32_t stride = 0;      // inter profiles: entries per code row
     size_t off8 = 0;         // int8 inter profile (biased for linear)
-    size_t off16 = 0;        // int16 inter profile (16-bit kernel)
-    size_t off32 = 0;        // int32 inter profile (p32 kernel)
+    size_t off16 = 0;        // int16 inter profile (packed kernels)
     size_t intra_off = 0;    // lane-slotted intra profile
     size_t total = 0;
 };
 
 int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* mat, int go, bool affine,
-                   int32_t qpad_inter, bool want16, bool want32, int ri, int32_t qpad_intra, Profiles* P) {
+                   int32_t qpad_inter, bool want16, int ri, int32_t qpad_intra, Profiles* P) {
     for (int32_t i = 0; i < qlen; ++i)
         if (q[i] >= SW_ALPHABET) return fail(SW_E_INVALID, "query residue code out of range (use sw_encode)");
     const int bias = affine ? 0 : go;
@@ -619,7 +618,6 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     };
     P->off8 = take(n);
     P->off16 = want16 ? take(2 * n) : 0;
-    P->off32 = want32 ? take(4 * n) : 0;
     const int rip = swk::intra_rip(ri);
     const size_t intra_bytes = ri ? static_cast<size_t>(qpad_intra / (swk::kLanes * ri)) * swk::intra_chunk_bytes(ri) : 0;
     P->intra_off = take(intra_bytes);
@@ -649,14 +647,12 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     };
     int8_t* p8 = hp + P->off8;
     int16_t* p16 = reinterpret_cast<int16_t*>(hp + P->off16);
-    int32_t* p32 = reinterpret_cast<int32_t*>(hp + P->off32);
     for (int c = 0; c < swk::kProfileRows; ++c)
         for (int32_t i = 0; i < P->stride; ++i) {
             const int v = value(c, i);
             const size_t k = static_cast<size_t>(c) * P->stride + i;
             p8[k] = static_cast<int8_t>(v);
             if (want16) p16[k] = static_cast<int16_t>(v);
-            if (want32) p32[k] = v;
         }
     if (ri) {
         const int64_t CH = static_cast<int64_t>(swk::kLanes) * ri;
@@ -857,8 +853,6 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         return SW_OK;
     }
     Profiles P;
-    const bool p32 = swk::inter_profile32(affine, x2_ok);
-    const bool i16 = swk::inter_uses_16bit(affine, x2_ok);
     const bool x2 = swk::inter_uses_x2(affine, x2_ok);
     // int32 re-scoring of blocks a 16-bit kernel flags near saturation
     const bool rescue = swk::inter_needs_rescue(affine, x2_ok);
@@ -875,14 +869,13 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     const char* pm = std::getenv("SW_PAIR_MERGED");
     const bool pair_merged = !(pm && pm[0] == '0');
     const int32_t ncoop =
-        (!npair && !i16 && !p32 && db->nblocks) ? coop_blocks(db, swk::inter_coop_divisor(affine, x2_ok)) : 0;
+        (!npair && db->nblocks) ? coop_blocks(db, swk::inter_coop_divisor(affine, x2_ok)) : 0;
     db->last_ncoop = ncoop;
     db->last_npair = npair;
     db->last_pair_merged = npair && pair_merged;
     const int32_t qpad_coop = ncoop ? static_cast<int32_t>(round_up(qlen, swk::inter_coop_rows())) : 0;
     if ((rc = build_profiles(h, query, qlen, mat, go, affine, std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2}),
-                             i16 || x2 || intra_x2,
-                             p32, ri, qpad_intra, &P)))
+                             x2 || intra_x2, ri, qpad_intra, &P)))
         return rc;
     if (rescue && db->nblocks && !db->d_rescue) {
         // lists A and B, then the fp16 pass's largest flagged block
@@ -996,7 +989,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         a.blk_groups = db->d_blk_groups;
         a.lane_ids = db->d_lane_ids;
         a.nblocks = static_cast<int32_t>(db->nblocks);
-        a.prof = P.dev + ((i16 || x2) ? P.off16 : p32 ? P.off32 : P.off8);
+        a.prof = P.dev + (x2 ? P.off16 : P.off8);
         a.prof_stride = P.stride;
         a.qpad = qpad_inter;
         a.gap_open = go;
@@ -1184,8 +1177,8 @@ int ensure_scores(sw_handle* h, size_t n) {
 }  // namespace
 
 namespace {
-int topk_impl(sw_handle* h, const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, int32_t k,
-              int64_t* out) {
+int topk_impl(sw_handle* h, const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base,
+              const int32_t* ids, int32_t k, int64_t* out) {
     if (!h || !out || n < 0 || k <= 0 || k > 4096 || (n > 0 && !scores && !keys))
         return fail(SW_E_INVALID, "bad top-k arguments (1 <= k <= 4096)");
     if (id_base < 0 || id_base + n > (int64_t(1) << 31)) return fail(SW_E_INVALID, "ids must fit in 31 bits");
@@ -1199,7 +1192,7 @@ int topk_impl(sw_handle* h, const int32_t* scores, const int64_t* keys, int64_t 
         h->topk_cap = std::max<size_t>(need, 1 << 20);
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&h->d_topk_work), h->topk_cap));
     }
-    HIPCHECK(swk::launch_topk(scores, keys, n, id_base, k, out, h->d_topk_work, h->stream));
+    HIPCHECK(swk::launch_topk(scores, keys, n, id_base, ids, k, out, h->d_topk_work, h->stream));
     return SW_OK;
 }
 }  // namespace
@@ -1691,11 +1684,17 @@ int sw_topk(const int32_t* scores, int64_t n, int32_t k, int32_t* out_ids, int32
 
 int sw_topk_device(sw_handle* h, const int32_t* scores_dev, int64_t n, int64_t id_base, int32_t k,
                    int64_t* keys_out_dev) {
-    return topk_impl(h, scores_dev, nullptr, n, id_base, k, keys_out_dev);
+    return topk_impl(h, scores_dev, nullptr, n, id_base, nullptr, k, keys_out_dev);
+}
+
+int sw_topk_device_ids(sw_handle* h, const int32_t* scores_dev, int64_t n, const int32_t* ids_dev, int32_t k,
+                       int64_t* keys_out_dev) {
+    if (n > 0 && !ids_dev) return fail(SW_E_INVALID, "null id map");
+    return topk_impl(h, scores_dev, nullptr, n, 0, ids_dev, k, keys_out_dev);
 }
 
 int sw_topk_keys_device(sw_handle* h, const int64_t* keys_dev, int64_t n, int32_t k, int64_t* keys_out_dev) {
-    return topk_impl(h, nullptr, keys_dev, n, 0, k, keys_out_dev);
+    return topk_impl(h, nullptr, keys_dev, n, 0, nullptr, k, keys_out_dev);
 }
 
 int sw_align(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen, const sw_scoring* sc,

@@ -1,5 +1,8 @@
-// sw_inter_x2.hip — inter-sequence Smith-Waterman, two subjects per lane,
-// packed 16-bit cells, no pair table.
+// sw_inter_x2.hip — inter-sequence Smith-Waterman, packed 16-bit cells
+// (sw_inter_x2s: one subject per lane, two query strips per pass; its wave-
+// pair form sw_inter_x2p).  The first packed form, two SUBJECTS per lane
+// (sw_inter_x2, described below), was measured slower (profiles/r01_x2/) and
+// removed in round 2; its profile-image helpers remain in use.
 //
 // Why: the scan is bound by VALU issue.  On gfx950 every 32-bit max/max3 and
 // the SDWA byte add issue at the slow ~4.3-cycle rate, so an int32 affine cell
@@ -145,152 +148,6 @@ __device__ __forceinline__ void store_pairs(int32_t* p, const uint32_t (&v)[SG])
 #pragma unroll
     for (int q = 0; q < SG / 4; ++q)
         *reinterpret_cast<int4*>(p + 4 * q) = make_int4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-}
-
-template <int R, int SG, bool AFFINE>
-__global__ __launch_bounds__(256) void sw_inter_x2(InterArgs a) {
-    static_assert(R % 16 == 0 && SG % 4 == 0, "shape");
-    __shared__ __attribute__((aligned(16))) X2Lds<R> lds[kWavesPerWG];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    X2Lds<R>& L = lds[wave];
-    const int pair = blockIdx.x * kWavesPerWG + wave;
-    const int b0 = a.blk_first + 2 * pair;
-    const int b1 = b0 + 1;
-    if (b0 >= a.nblocks) return;  // wave-uniform; waves never synchronise
-    const bool has1 = b1 < a.nblocks;
-    const uint32_t ncols = a.blk_groups[b0] * kGroupCols;
-    const uint32_t ncols1 = has1 ? a.blk_groups[b1] * kGroupCols : 0;
-    const uint64_t base0 = a.blk_off[b0] + static_cast<uint64_t>(lane) * kGroupCols;
-    const uint64_t base1 = has1 ? a.blk_off[b1] + static_cast<uint64_t>(lane) * kGroupCols : 0;
-    const int16_t* prof16 = reinterpret_cast<const int16_t*>(a.prof);
-    const u2 go2 = {static_cast<unsigned short>(a.gap_open), static_cast<unsigned short>(a.gap_open)};
-    const u2 ge2 = {static_cast<unsigned short>(a.gap_extend), static_cast<unsigned short>(a.gap_extend)};
-    s2 best = {0, 0};
-
-    for (int s0 = 0; s0 < a.qpad && ncols > 0; s0 += R) {
-        const bool first = (s0 == 0);
-        const bool last = (s0 + R >= a.qpad);
-        stage_x2<R>(L, prof16, a.prof_stride, s0, lane);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-
-        s2 H[R];
-        s2 E[AFFINE ? R : 1];
-#pragma unroll
-        for (int r = 0; r < R; ++r) H[r] = s2{0, 0};
-#pragma unroll
-        for (int r = 0; r < (AFFINE ? R : 1); ++r) E[r] = s2{0, 0};
-        s2 dtop = {0, 0};
-
-        uint32_t ra[SG / 4], rb[SG / 4], na[SG / 4], nb[SG / 4];
-        uint32_t bh[SG], bh_n[SG];
-        uint32_t bf[AFFINE ? SG : 1], bf_n[AFFINE ? SG : 1];
-        load_codes<SG>(ra, a.residues + base0, true);
-        load_codes<SG>(rb, a.residues + base1, ncols1 > 0);
-        if (!first) {
-            load_pairs<SG>(bh, a.bnd_h + base0);
-            if constexpr (AFFINE) load_pairs<SG>(bf, a.bnd_f + base0);
-        } else {
-#pragma unroll
-            for (int q = 0; q < SG; ++q) bh[q] = 0;
-#pragma unroll
-            for (int q = 0; q < (AFFINE ? SG : 1); ++q) bf[q] = 0;
-        }
-        // Flat (column, 16-row chunk) schedule, ping-pong chunk buffers: the
-        // next step's profile rows are read while this step computes.
-        constexpr int NCH = R / 16;
-        constexpr int STEPS = SG * NCH;
-        int4 PL[2][4], PH[2][4];
-        read_x2<R>(PL[0], PH[0], L, code_of(ra, 0), code_of(rb, 0), 0, 0);
-
-        for (uint32_t col0 = 0; col0 < ncols; col0 += SG) {
-            const uint64_t off = (col0 >> 4) * kGroupBytes + (col0 & 15);
-            const bool more = col0 + SG < ncols;
-            const uint32_t ncol = col0 + SG;
-            const uint64_t noff = (ncol >> 4) * kGroupBytes + (ncol & 15);
-            if (more) {
-                load_codes<SG>(na, a.residues + base0 + noff, true);
-                load_codes<SG>(nb, a.residues + base1 + noff, ncol < ncols1);
-                if (!first) {
-                    load_pairs<SG>(bh_n, a.bnd_h + base0 + noff);
-                    if constexpr (AFFINE) load_pairs<SG>(bf_n, a.bnd_f + base0 + noff);
-                }
-            }
-            s2 up = {0, 0}, diag = {0, 0}, f = {0, 0};
-#pragma unroll
-            for (int t = 0; t < STEPS; ++t) {
-                const int jj = t / NCH;
-                const int k = t % NCH;
-                const uint32_t dep = as_u32(k == 0 ? H[R - 1] : H[16 * k - 1]);
-                if (t + 1 < STEPS) {
-                    const int jn = (t + 1) / NCH, kn = (t + 1) % NCH;
-                    read_x2<R>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(ra, jn), code_of(rb, jn), kn, dep);
-                } else if (more) {
-                    read_x2<R>(PL[(t + 1) & 1], PH[(t + 1) & 1], L, code_of(na, 0), code_of(nb, 0), 0, dep);
-                }
-                if (k == 0) {
-                    up = as_s2(bh[jj]);
-                    diag = dtop;
-                    dtop = up;
-                    if constexpr (AFFINE) f = as_s2(bf[AFFINE ? jj : 0]);
-                }
-                const int4(&pl)[4] = PL[t & 1];
-                const int4(&ph)[4] = PH[t & 1];
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int r = 16 * k + i;
-                    const s2 sc = as_s2(word(pl, i) | word(ph, i));
-                    if constexpr (!AFFINE) {
-                        const s2 h = usub2(max2(max2(H[r], up), diag + sc), go2);
-                        diag = H[r];
-                        H[r] = h;
-                        up = h;
-                        best = max2(best, h);
-                    } else {
-                        const s2 h = max2(max2(E[r], f), diag + sc);
-                        const s2 n = usub2(h, go2);
-                        E[r] = max2(usub2(E[r], ge2), n);
-                        f = max2(usub2(f, ge2), n);
-                        diag = H[r];
-                        H[r] = h;
-                        up = h;
-                        best = max2(best, h);
-                    }
-                }
-                if (k == NCH - 1) {
-                    bh[jj] = as_u32(up);
-                    if constexpr (AFFINE) bf[jj] = as_u32(f);
-                }
-                asm volatile("" : "+v"(best));
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            if (!last) {
-                store_pairs<SG>(a.bnd_h + base0 + off, bh);
-                if constexpr (AFFINE) store_pairs<SG>(a.bnd_f + base0 + off, bf);
-            }
-            if (more) {
-#pragma unroll
-                for (int q = 0; q < SG / 4; ++q) {
-                    ra[q] = na[q];
-                    rb[q] = nb[q];
-                }
-#pragma unroll
-                for (int q = 0; q < SG; ++q) bh[q] = first ? 0u : bh_n[q];
-                if constexpr (AFFINE) {
-#pragma unroll
-                    for (int q = 0; q < SG; ++q) bf[q] = first ? 0u : bf_n[q];
-                }
-            }
-        }
-    }
-    const int id0 = a.lane_ids[static_cast<size_t>(b0) * kLanes + lane];
-    if (id0 >= 0) a.scores[id0] = best.x;
-    if (has1) {
-        const int id1 = a.lane_ids[static_cast<size_t>(b1) * kLanes + lane];
-        if (id1 >= 0) a.scores[id1] = best.y;
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1066,24 +923,6 @@ hipError_t launch_inter_x2s_list(const InterArgs& a, bool affine, hipStream_t s)
     if (affine) hipLaunchKernelGGL((sw_inter_x2s<32, 8, true, false, true>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((sw_inter_x2s<48, 4, false, false, true>), grid, block, 0, s, a);
     return hipGetLastError();
-}
-
-template <int R, int SG>
-static hipError_t launch_x2_shape(const InterArgs& a, bool affine, hipStream_t s) {
-    const int npairs = (a.nblocks - a.blk_first + 1) / 2;
-    const dim3 grid((npairs + kWavesPerWG - 1) / kWavesPerWG), block(kWavesPerWG * kLanes);
-    if (affine) hipLaunchKernelGGL((sw_inter_x2<R, SG, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((sw_inter_x2<R, SG, false>), grid, block, 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_inter_x2(const InterArgs& a, int R, int SG, bool affine, hipStream_t s) {
-    if (a.nblocks - a.blk_first <= 0 || a.qpad <= 0) return hipSuccess;
-    if (R == 16 && SG == 8) return launch_x2_shape<16, 8>(a, affine, s);
-    if (R == 16 && SG == 16) return launch_x2_shape<16, 16>(a, affine, s);
-    if (R == 32 && SG == 8) return launch_x2_shape<32, 8>(a, affine, s);
-    if (R == 48 && SG == 8) return launch_x2_shape<48, 8>(a, affine, s);
-    return hipErrorInvalidValue;
 }
 
 }  // namespace swk

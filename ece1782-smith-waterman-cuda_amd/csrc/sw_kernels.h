@@ -119,9 +119,7 @@ struct IntraArgs {
 // provably int16-safe (any packed kernel may run); 1 = a guarded packed
 // kernel may run (saturating blocks are re-scored at int32); 0 = int32 only.
 int inter_rows(bool affine, int x2_ok);
-// true: the inter kernel takes an int32 profile [kProfileRows][prof_stride] int32
-bool inter_profile32(bool affine, int x2_ok);
-// true if the packed two-subjects-per-lane kernel is used (int16 profile).
+// true if the packed two-strips kernel is used (int16 profile).
 bool inter_uses_x2(bool affine, int x2_ok);
 // Wide-block cut-off for the cooperative kernel: residues / divisor columns
 // (0 = the chosen inter kernel does not use it).
@@ -139,15 +137,6 @@ hipError_t launch_inter(const InterArgs& a, bool affine, int x2_ok, hipStream_t 
 // over query strips (linear gap).  Returns the strip height it uses.
 hipError_t launch_inter_coop(const InterArgs& a, int ncoop, bool affine, hipStream_t s);
 int inter_coop_rows();
-// Linear gap: true if the 16-bit inter kernel is used (profile int16 [32][stride]).
-bool inter_uses_16bit(bool affine, int x2_ok);
-// The 16-bit inter kernel (sw_inter16.hip, its own translation unit).
-hipError_t launch_inter16(const InterArgs& a, int R, int SG, hipStream_t s);
-// The packed two-subjects-per-lane kernel (sw_inter_pk.hip).
-hipError_t launch_inter_pk(const InterArgs& a, int R, int SG, hipStream_t s);
-// Two subjects per lane, packed int16, dual profile images (sw_inter_x2.hip);
-// blocks [blk_first, nblocks) in pairs.
-hipError_t launch_inter_x2(const InterArgs& a, int R, int SG, bool affine, hipStream_t s);
 // One subject per lane, two R-row query strips per pass in the two int16
 // halves (sw_inter_x2.hip); qpad is a multiple of 2R; boundary rows are
 // (H | F << 16) dwords in bnd_h.
@@ -226,7 +215,7 @@ size_t topk_workspace_bytes(int64_t n, int k);
 // One thread zeroes the rescue lists' counters (c = -1: a largest-id slot);
 // null pointers are skipped.
 hipError_t launch_reset_counters(int32_t* a, int32_t* b, int32_t* c, int32_t* d, int32_t* e, hipStream_t s);
-hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, int k,
+hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, const int32_t* ids, int k,
                        int64_t* out, int64_t* work, hipStream_t s);
 
 }  // namespace swk

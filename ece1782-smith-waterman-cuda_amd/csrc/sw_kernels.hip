@@ -477,149 +477,6 @@ hipError_t launch_inter_coop(const InterArgs& a, int ncoop, bool affine, hipStre
 }
 
 // ---------------------------------------------------------------------------
-// inter-sequence, linear gap, int32 profile ("p32")
-// ---------------------------------------------------------------------------
-// Same scheme as sw_inter, but the profile slice in LDS holds int32 scores so
-// the per-cell add is the fast-rate v_add_u32 instead of the slow SDWA form
-// (profiles/r01_valu_rate_*.txt).  Per column a lane reads R*4 bytes; the
-// reads are pipelined one 16-row chunk ahead over a flat (column, chunk)
-// schedule with ping-pong buffers.
-__host__ __device__ constexpr int inter32_stride(int R) {
-    // R*4 bytes + 16, with an odd number of 16-byte slots (bank spread)
-    return ((R * 4 + 16) / 16) % 2 == 1 ? R * 4 + 16 : R * 4 + 32;
-}
-
-template <int R>
-__device__ __forceinline__ void stage_profile32(uint8_t* lp, const int32_t* __restrict__ prof, int stride,
-                                                int s0, int lane) {
-    constexpr int kChunks = kProfileRows * (R / 4);  // 16-byte chunks
-    constexpr int S = inter32_stride(R);
-#pragma unroll
-    for (int t = lane; t < kChunks; t += kLanes) {
-        const int c = t / (R / 4);
-        const int k = t % (R / 4);
-        const int4 v = *reinterpret_cast<const int4*>(prof + static_cast<size_t>(c) * stride + s0 + 4 * k);
-        *reinterpret_cast<int4*>(lp + c * S + 16 * k) = v;
-    }
-}
-
-__device__ __forceinline__ void read_chunk(int4 (&p)[4], const uint8_t* lp, uint32_t off, int dep) {
-    asm volatile("" : "+v"(off) : "v"(dep));
-    const int4* pp = reinterpret_cast<const int4*>(lp + off);
-    p[0] = pp[0];
-    p[1] = pp[1];
-    p[2] = pp[2];
-    p[3] = pp[3];
-}
-
-template <int R, int SG>
-__global__ __launch_bounds__(256) void sw_inter_p32(InterArgs a) {
-    constexpr int S = inter32_stride(R);
-    constexpr int NCH = R / 16;          // 16-row chunks per column
-    constexpr int STEPS = SG * NCH;      // (column, chunk) steps per sub-group
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerWG * kProfileRows * S];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int blk = blockIdx.x * kWavesPerWG + wave;
-    if (blk >= a.nblocks) return;
-    uint8_t* lp = lds + wave * (kProfileRows * S);
-    const int32_t* prof32 = reinterpret_cast<const int32_t*>(a.prof);
-
-    const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
-    const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
-    const uint32_t go = static_cast<uint32_t>(a.gap_open);
-    int best = 0;
-    if (ncols == 0) goto done;
-
-    for (int s0 = 0; s0 < a.qpad; s0 += R) {
-        const bool first = (s0 == 0);
-        const bool last = (s0 + R >= a.qpad);
-        stage_profile32<R>(lp, prof32, a.prof_stride, s0, lane);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-
-        int H[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) H[r] = 0;
-        int dtop = 0;
-
-        Residues<SG> rs, rs_next;
-        int bh[SG], bh_next[SG];
-        rs.load(a.residues + base);
-        if (!first) {
-            load_row<SG>(bh, a.bnd_h + base);
-        } else {
-#pragma unroll
-            for (int q = 0; q < SG; ++q) bh[q] = 0;
-        }
-        int4 P[2][4];
-        read_chunk(P[0], lp, rs.code(0) * S, 0);
-
-        for (uint32_t col0 = 0; col0 < ncols; col0 += SG) {
-            const uint64_t idx = base + (col0 >> 4) * kGroupBytes + (col0 & 15);
-            const bool more = col0 + SG < ncols;
-            const uint64_t nidx = base + ((col0 + SG) >> 4) * kGroupBytes + ((col0 + SG) & 15);
-            if (more) {
-                rs_next.load(a.residues + nidx);
-                if (!first) load_row<SG>(bh_next, a.bnd_h + nidx);
-            }
-            int up = 0, diag = 0;
-#pragma unroll
-            for (int t = 0; t < STEPS; ++t) {
-                const int jj = t / NCH;
-                const int k = t % NCH;
-                // prefetch the next step's chunk (next column's first chunk at a column end)
-                if (t + 1 < STEPS) {
-                    const int jn = (t + 1) / NCH, kn = (t + 1) % NCH;
-                    read_chunk(P[(t + 1) & 1], lp, rs.code(jn) * S + 64 * kn, k == 0 ? H[R - 1] : H[16 * k - 1]);
-                } else if (more) {
-                    read_chunk(P[(t + 1) & 1], lp, rs_next.code(0) * S, H[16 * k - 1]);
-                }
-                if (k == 0) {
-                    up = bh[jj];
-                    diag = dtop;
-                    dtop = up;
-                }
-                const int4(&pc)[4] = P[t & 1];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int sv[4] = {pc[q].x, pc[q].y, pc[q].z, pc[q].w};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int r = 16 * k + 4 * q + e;
-                        const int h = usub(max(max(H[r], up), diag + sv[e]), go);
-                        diag = H[r];
-                        H[r] = h;
-                        up = h;
-                        best = max(best, h);
-                    }
-                }
-                if (k == NCH - 1) {
-                    bh[jj] = up;
-                    asm volatile("" : "+v"(best));
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            if (!last) store_row<SG>(a.bnd_h + idx, bh);
-            if (more) {
-                rs = rs_next;
-                if (!first) {
-#pragma unroll
-                    for (int q = 0; q < SG; ++q) bh[q] = bh_next[q];
-                } else {
-#pragma unroll
-                    for (int q = 0; q < SG; ++q) bh[q] = 0;
-                }
-            }
-        }
-    }
-done:
-    const int id = a.lane_ids[static_cast<size_t>(blk) * kLanes + lane];
-    if (id >= 0) a.scores[id] = best;
-}
-
-// ---------------------------------------------------------------------------
 // intra-sequence wavefront (one long subject per wave)
 // ---------------------------------------------------------------------------
 // DPP controls (GFX9 family): wave_shr:1 moves lane t-1's value to lane t;
@@ -775,72 +632,43 @@ __device__ __forceinline__ void intra_subject(const IntraArgs& a, int sid, uint8
 // ---------------------------------------------------------------------------
 // Inter-kernel shape: R query rows per strip x SG columns per software-
 // pipelined sub-group.  SW_INTER_VARIANT="RxSG" overrides (tuning only).
-struct InterShape { int R, SG; bool p32; bool i16; bool pk; bool skew = false; bool x2 = false; bool x2s = false; bool f16 = false; };
+struct InterShape { int R, SG; bool x2s = false; bool f16 = false; };
 static InterShape inter_shape(bool affine, int x2_ok) {
-    // measured on MI355X (scripts/tune_inter.py, profiles/r01_tune_inter.jsonl):
-    // 64x8 is fastest for the linear kernel (170 VGPRs, 2 waves/SIMD, half
-    // the boundary traffic of 32-row strips); affine keeps 32x8.
-    // measured on MI355X: 64x8 int32 beats the 16-bit-value (h*) and int32-
-    // profile (p*) variants on C2 (profiles/r01_tune_inter*.jsonl)
-    // int16-safe scans (the common case): the packed two-strips-per-lane
-    // kernel sw_inter_x2s, one subject per lane (profiles/r01_x2s/):
-    //   affine y32x8: 6.2 TCUPS on C2 BLOSUM62 11/1 (int32 32x8: 4.66;
-    //   two-subjects-per-lane x32x8 + coop: 5.92);
-    //   linear y48x4: 10.4 TCUPS on C2 BLOSUM50/2 (int32 64x8 + coop: 9.9).
-    // Otherwise int32: affine 32x8, linear 64x8 (+ the cooperative kernel).
+    // measured on MI355X (scripts/tune_inter.py, profiles/r01_tune_inter*.jsonl,
+    // r01_x2s/): int16-safe scans (the common case) run the packed two-strips-
+    // per-lane kernel sw_inter_x2s, one subject per lane, in its fp16 form
+    // (biased cell, v_pk_maximum3_f16; C2 affine 9.4 TCUPS vs 6.25 int16),
+    // always guarded (rescue chain fp16 -> int16 -> int32).  Otherwise int32:
+    // affine 32x8, linear 64x8 (+ the cooperative kernel for wide blocks).
     // Beyond the static int16 bound the packed kernel runs guarded (blocks
     // reaching kSat16 are re-scored at int32); SW_INT16_GUARD=0 disables that.
     // x2_ok: 2 = int16 provably exact, 1 = guarded int16 allowed, 0 = int32 only
+    // (Measured slower and removed in round 2: 16-bit-value and int32-profile
+    // one-subject kernels, pair-table packing, two subjects per lane, the
+    // column-skewed int32 kernel; their numbers are in profiles/r01_tune_*.)
     const char* ge = std::getenv("SW_INT16_GUARD");
     const bool y_ok = x2_ok == 2 || (x2_ok == 1 && !(ge && ge[0] == '0'));
-    // Both gap models: the fp16 form of the two-strips kernel (biased cell,
-    // v_pk_maximum3_f16; C2 affine 9.4 TCUPS vs 6.25 int16), always guarded
-    // (rescue chain fp16 -> int16 -> int32).  SW_INTER_VARIANT=y32x8 forces
-    // the int16 form (linear: 3 waves per SIMD, 11.2 TCUPS).
-    InterShape v = affine ? (y_ok ? InterShape{64, 8, false, false, false, false, false, true, true}
-                                  : InterShape{32, 8, false, false, false})
-                          : (y_ok ? InterShape{64, 8, false, false, false, false, false, true, true}
-                                  : InterShape{64, 8, false, false, false});
+    InterShape v = y_ok ? InterShape{64, 8, true, true} : InterShape{affine ? 32 : 64, 8};
+    // SW_INTER_VARIANT (tests / A-B only): "RxSG" int32 (32x8, 64x8),
+    // "y32x8" the int16 two-strips kernel, "f32x8" / "f32x4" its fp16 form
     if (const char* e = std::getenv("SW_INTER_VARIANT")) {
         int r = 0, g = 0;
-        if (std::sscanf(e, "k%dx%d", &r, &g) == 2 && !affine &&
-            ((r == 16 && (g == 8 || g == 16 || g == 9)) || (r == 32 && g == 8)))
-            v = InterShape{r, g, false, true, true};
-        else if (std::sscanf(e, "h%dx%d", &r, &g) == 2 && !affine &&
-            ((r == 64 && (g == 8 || g == 16)) || (r == 32 && (g == 8 || g == 16)) || (r == 48 && g == 8)))
-            v = InterShape{r, g, false, true, false};
-        else if (std::sscanf(e, "p%dx%d", &r, &g) == 2 && !affine &&
-            ((r == 64 && (g == 8 || g == 4)) || (r == 32 && g == 8) || (r == 48 && g == 8)))
-            v = InterShape{r, g, true, false, false};
-        else if (std::sscanf(e, "f%dx%d", &r, &g) == 2 && y_ok && r == 32 && (g == 8 || (g == 4 && affine)))
-            v = InterShape{2 * r, g, false, false, false, false, false, true, true};
-        else if (std::sscanf(e, "y%dx%d", &r, &g) == 2 && y_ok &&
-                 ((r == 32 && (g == 8 || g == 4)) || (r == 16 && g == 8) || (r == 48 && g == 4)))
-            v = InterShape{2 * r, g, false, false, false, false, false, true};  // R = rows per pass
-        else if (std::sscanf(e, "x%dx%d", &r, &g) == 2 && x2_ok == 2 &&
-            ((r == 16 && (g == 8 || g == 16)) || (r == 32 && g == 8) || (r == 48 && g == 8)))
-            v = InterShape{r, g, false, false, false, false, true};
-        else if (std::sscanf(e, "s%dx%d", &r, &g) == 2 &&
-            ((r == 32 && (g == 8 || g == 16)) || (r == 48 && g == 8) || (r == 64 && g == 8) || (r == 16 && g == 16)))
-            v = InterShape{r, g, false, false, false, true};
-        else if (std::sscanf(e, "%dx%d", &r, &g) == 2 &&
-            ((r == 32 && (g == 8 || g == 16)) || (r == 48 && g == 8) || (r == 64 && g == 8) || (r == 16 && g == 16)))
-            v = InterShape{r, g, false, false, false};
+        if (std::sscanf(e, "f%dx%d", &r, &g) == 2 && y_ok && r == 32 && (g == 8 || (g == 4 && affine)))
+            v = InterShape{2 * r, g, true, true};
+        else if (std::sscanf(e, "y%dx%d", &r, &g) == 2 && y_ok && r == 32 && g == 8)
+            v = InterShape{2 * r, g, true, false};  // R = rows per pass
+        else if (std::sscanf(e, "%dx%d", &r, &g) == 2 && g == 8 && (r == 32 || r == 64))
+            v = InterShape{r, g};
     }
     return v;
 }
 
 int inter_rows(bool affine, int x2_ok) { return inter_shape(affine, x2_ok).R; }
-bool inter_profile32(bool affine, int x2_ok) { return inter_shape(affine, x2_ok).p32; }
-bool inter_uses_16bit(bool affine, int x2_ok) { return inter_shape(affine, x2_ok).i16; }
-bool inter_uses_x2(bool affine, int x2_ok) {
-    const InterShape v = inter_shape(affine, x2_ok);
-    return v.x2 || v.x2s;
-}
+bool inter_uses_x2(bool affine, int x2_ok) { return inter_shape(affine, x2_ok).x2s; }
 
 bool inter_needs_rescue(bool affine, int x2_ok) {
     const InterShape v = inter_shape(affine, x2_ok);
-    return v.i16 || v.f16 || (v.x2s && x2_ok != 2);
+    return v.f16 || (v.x2s && x2_ok != 2);
 }
 
 bool inter_uses_f16(bool affine, int x2_ok) { return inter_shape(affine, x2_ok).f16; }
@@ -856,9 +684,7 @@ int inter_coop_divisor(bool affine, int x2_ok) {
     // blocks at least residues / divisor columns wide go to the cooperative
     // kernel; 0 = none.  One subject per lane with two strips per pass has
     // no long single-wave tail (measured: coop on/off within 1 %).
-    const InterShape v = inter_shape(affine, x2_ok);
-    if (v.x2s || v.pk || v.i16 || v.p32) return 0;
-    return v.x2 ? 200000 : 530000;
+    return inter_shape(affine, x2_ok).x2s ? 0 : 530000;
 }
 
 const char* inter_kernel_name(bool affine, int x2_ok) {
@@ -869,11 +695,8 @@ const char* inter_kernel_name(bool affine, int x2_ok) {
                       v.f16 ? ",fp16" : "");
         return b2;
     }
-    const char* kind = v.x2 ? "sw_inter_x2" : v.pk ? "sw_inter_pk" : v.i16 ? "sw_inter16" : v.p32 ? "sw_inter_p32"
-                                                                                               : "sw_inter";
     static thread_local char buf[96];
-    std::snprintf(buf, sizeof buf, "%s<%d,%d,%s%s>", kind, v.R, v.SG, affine ? "affine" : "linear",
-                  v.skew ? ",skew" : "");
+    std::snprintf(buf, sizeof buf, "sw_inter<%d,%d,%s>", v.R, v.SG, affine ? "affine" : "linear");
     return buf;
 }
 
@@ -912,36 +735,15 @@ hipError_t launch_inter(const InterArgs& a, bool affine, int x2_ok, hipStream_t 
     const dim3 grid((a.nblocks - a.blk_first + kWavesPerWG - 1) / kWavesPerWG);
     const dim3 block(kWavesPerWG * kLanes);
     const InterShape v = inter_shape(affine, x2_ok);
-    if (v.x2) return launch_inter_x2(a, v.R, v.SG, affine, s);
     if (v.x2s) return launch_inter_x2s(a, v.R / 2, v.SG, affine, v.f16, s);
-    if (v.pk) return launch_inter_pk(a, v.R, v.SG, s);
-    if (v.i16) return launch_inter16(a, v.R, v.SG, s);
-    if (v.p32) {
-#define SW_LAUNCH_P32(R_, SG_)                                                               \
-        if (v.R == R_ && v.SG == SG_) {                                                      \
-            hipLaunchKernelGGL((sw_inter_p32<R_, SG_>), grid, block, 0, s, a);               \
-            return hipGetLastError();                                                        \
-        }
-        SW_LAUNCH_P32(64, 8)
-        SW_LAUNCH_P32(64, 4)
-        SW_LAUNCH_P32(32, 8)
-        SW_LAUNCH_P32(48, 8)
-#undef SW_LAUNCH_P32
-        return hipErrorInvalidValue;
-    }
 #define SW_LAUNCH_INTER(R_, SG_)                                                                         \
     if (v.R == R_ && v.SG == SG_) {                                                                      \
-        if (affine && v.skew) hipLaunchKernelGGL((sw_inter<R_, SG_, true, true>), grid, block, 0, s, a); \
-        else if (affine) hipLaunchKernelGGL((sw_inter<R_, SG_, true, false>), grid, block, 0, s, a);     \
-        else if (v.skew) hipLaunchKernelGGL((sw_inter<R_, SG_, false, true>), grid, block, 0, s, a);     \
+        if (affine) hipLaunchKernelGGL((sw_inter<R_, SG_, true, false>), grid, block, 0, s, a);          \
         else hipLaunchKernelGGL((sw_inter<R_, SG_, false, false>), grid, block, 0, s, a);                \
         return hipGetLastError();                                                                        \
     }
     SW_LAUNCH_INTER(32, 8)
-    SW_LAUNCH_INTER(32, 16)
-    SW_LAUNCH_INTER(48, 8)
     SW_LAUNCH_INTER(64, 8)
-    SW_LAUNCH_INTER(16, 16)
 #undef SW_LAUNCH_INTER
     return hipErrorInvalidValue;
 }

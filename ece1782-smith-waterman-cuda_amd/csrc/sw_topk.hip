@@ -36,12 +36,15 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     return (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo);
 }
 
-// in_scores != nullptr: keys are built from scores (ids = id_base + i);
-// otherwise they come from in_keys.  FINAL: one workgroup, sorted output.
+// in_scores != nullptr: keys are built from scores (ids = id_base + i, or
+// ids[i] when an id map is given: a rank's residue-balanced shard of one
+// database holds scattered global ids); otherwise they come from in_keys.
+// FINAL: one workgroup, sorted output.
 template <bool FINAL>
 __global__ __launch_bounds__(kTopkThreads) void sw_topk_select(const int32_t* __restrict__ in_scores,
                                                               const int64_t* __restrict__ in_keys, int64_t n,
-                                                              int64_t id_base, int k, int64_t* __restrict__ out) {
+                                                              int64_t id_base, const int32_t* __restrict__ ids,
+                                                              int k, int64_t* __restrict__ out) {
     __shared__ uint32_t hist[256];
     __shared__ uint64_t red[2][kTopkThreads / 64];
     __shared__ int ctl[5];  // digit, keys above it, keys at it, output slot, tie ticket
@@ -57,7 +60,7 @@ __global__ __launch_bounds__(kTopkThreads) void sw_topk_select(const int32_t* __
         u[j] = 0;
         if (i < m) {
             const int64_t g = start + i;
-            u[j] = key_ord(in_scores ? make_key(in_scores[g], id_base + g) : in_keys[g]);
+            u[j] = key_ord(in_scores ? make_key(in_scores[g], ids ? ids[g] : id_base + g) : in_keys[g]);
             all_and &= u[j];
             all_or |= u[j];
         }
@@ -211,8 +214,8 @@ size_t topk_workspace_bytes(int64_t n, int k) {
     return total + 256;
 }
 
-hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, int k,
-                       int64_t* out, int64_t* work, hipStream_t s) {
+hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, const int32_t* ids,
+                       int k, int64_t* out, int64_t* work, hipStream_t s) {
     if (k <= 0 || k > kTopkMaxK) return hipErrorInvalidValue;
     const int32_t* sc = scores;
     const int64_t* kin = keys;
@@ -221,7 +224,7 @@ hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, in
     while (cur > kTopkChunk) {  // each stage keeps k of every 16,384 keys (k <= 4,096)
         const int64_t chunks = (cur + kTopkChunk - 1) / kTopkChunk;
         hipLaunchKernelGGL((sw_topk_select<false>), dim3(static_cast<unsigned>(chunks)), dim3(kTopkThreads), 0, s,
-                           sc, kin, cur, id_base, k, w);
+                           sc, kin, cur, id_base, ids, k, w);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         sc = nullptr;
@@ -229,7 +232,8 @@ hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, in
         cur = chunks * k;
         w += cur;
     }
-    hipLaunchKernelGGL((sw_topk_select<true>), dim3(1), dim3(kTopkThreads), 0, s, sc, kin, cur, id_base, k, out);
+    hipLaunchKernelGGL((sw_topk_select<true>), dim3(1), dim3(kTopkThreads), 0, s, sc, kin, cur, id_base,
+                       sc ? ids : nullptr, k, out);
     return hipGetLastError();
 }
 

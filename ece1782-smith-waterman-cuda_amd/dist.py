@@ -8,6 +8,8 @@ identically on every rank.  K x 8 bytes per rank: latency-bound and tiny.
 
 Ordering of hits: score descending, global id ascending (deterministic).
 """
+import heapq
+
 import numpy as np
 
 ID_BITS = 31
@@ -19,15 +21,44 @@ def shard_indices(lengths, world):
     lightest rank (LPT), balancing residues (= DP cells for a fixed query).
     Returns one sorted index array per rank.  Deterministic."""
     lengths = np.asarray(lengths, dtype=np.int64)
+    if world == 1:
+        return [np.arange(len(lengths), dtype=np.int64)]
     order = np.argsort(-lengths, kind="stable")
-    load = np.zeros(world, dtype=np.int64)
     owner = np.empty(len(lengths), dtype=np.int64)
-    # LPT with a heap would be O(n log w); w <= 8 so a vector argmin is fine
-    for i in order:
-        r = int(np.argmin(load))
+    # heap of (load, rank): the lightest rank, the lowest index among equals
+    heap = [(0, r) for r in range(world)]
+    for i, L in zip(order.tolist(), lengths[order].tolist()):
+        load, r = heapq.heappop(heap)
         owner[i] = r
-        load[r] += lengths[i]
-    return [np.sort(np.nonzero(owner == r)[0]) for r in range(world)]
+        heapq.heappush(heap, (load + L, r))
+    return [np.nonzero(owner == r)[0] for r in range(world)]
+
+
+def shard(residues, offsets, rank, world):
+    """Rank `rank`'s share of ONE database (strong scaling): (global ids
+    int32 [n_r], residues, offsets) of its LPT subjects, in id order."""
+    idx = shard_indices(offsets[1:] - offsets[:-1], world)[rank]
+    if world == 1:
+        return idx.astype(np.int32), residues, offsets
+    res, offs = subset(residues, offsets, idx)
+    return idx.astype(np.int32), res, offs
+
+
+def allgather_np(arr, group=None):
+    """All-gather one equally shaped numpy array per rank -> [world, ...]
+    (device tensors over nccl/RCCL, CPU tensors over gloo)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    t = torch.from_numpy(np.ascontiguousarray(arr))
+    if dist.get_backend(group) == "nccl":
+        t = t.to(torch.device("cuda", torch.cuda.current_device()))
+        out = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=group)
+        return out.cpu().numpy()
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t, group=group)
+    return np.stack([o.numpy() for o in outs])
 
 
 def subset(residues, offsets, idx):

@@ -232,6 +232,12 @@ SW_API int sw_topk_device(sw_handle* h, const int32_t* scores_dev, int64_t n, in
                    int32_t k, int64_t* keys_out_dev);
 SW_API int sw_topk_keys_device(sw_handle* h, const int64_t* keys_dev, int64_t n, int32_t k,
                         int64_t* keys_out_dev);
+/* Same as sw_topk_device with the global id of entry i read from
+ * ids_dev[i] (device int32, >= 0) instead of id_base + i: a rank's
+ * residue-balanced shard of one database holds scattered
+ * global ids, and the merged ranking breaks ties by global id.            */
+SW_API int sw_topk_device_ids(sw_handle* h, const int32_t* scores_dev, int64_t n, const int32_t* ids_dev,
+                              int32_t k, int64_t* keys_out_dev);
 
 /* ---- alignments of chosen hits (traceback) ------------------------------
  * The GPU analogue of the cpu.cpp pair program's traceback (cpu.cpp:47-108;

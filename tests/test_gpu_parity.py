@@ -244,16 +244,16 @@ def test_device_topk_radix_select(sw, handle, n, k, dist):
     assert (ids[m:] == -1).all()
 
 
-INTER_VARIANTS = ["32x8", "s32x8", "32x16", "s32x16", "48x8", "s48x8", "64x8", "s64x8", "16x16", "s16x16",
-                  "x16x8", "x16x16", "x32x8", "x48x8", "y16x8", "y32x8", "y32x4",
-                  "y48x4", "f32x8", "f32x4"]
+# the shapes the library still builds: int32 (fall-back and rescue), the
+# int16 two-strips kernel (rescue-chain stage 2), its fp16 form (default)
+INTER_VARIANTS = ["32x8", "64x8", "y32x8", "f32x8", "f32x4"]
 
 
 @pytest.mark.parametrize("variant", INTER_VARIANTS)
 @pytest.mark.parametrize("coop", ["0", "128:0", "128:1"])
 def test_inter_variants_vs_oracle(sw, oracle, handle, monkeypatch, variant, coop):
-    """Every inter-kernel shape, plain and column-skewed, with the cooperative
-    wide-block kernel off / on (plain) / on (skewed), linear and affine."""
+    """Every inter-kernel shape with the cooperative wide-block kernel off /
+    on (plain) / on (skewed), linear and affine."""
     width, _, skew = coop.partition(":")
     monkeypatch.setenv("SW_INTER_VARIANT", variant)
     monkeypatch.setenv("SW_COOP_WIDTH", width)
@@ -269,11 +269,10 @@ def test_inter_variants_vs_oracle(sw, oracle, handle, monkeypatch, variant, coop
 
 
 @pytest.mark.parametrize("guard", ["1", "0"])
-@pytest.mark.parametrize("variant", ["", "x32x8", "y32x8"])
+@pytest.mark.parametrize("variant", ["", "y32x8"])
 def test_long_query_int16_guard(sw, oracle, handle, monkeypatch, variant, guard):
     """A query long enough that (qlen + 2) * (max S + gap open) >= 32767: the
-    two-strips kernel runs guarded (SW_INT16_GUARD unset / 1) — the two-
-    subjects x2 kernel, which has no guard, is never chosen — or the int32
+    two-strips kernel runs guarded (SW_INT16_GUARD unset / 1) or the int32
     kernel runs (SW_INT16_GUARD=0).  Scores stay exact either way."""
     monkeypatch.setenv("SW_INT16_GUARD", guard)
     if variant:
