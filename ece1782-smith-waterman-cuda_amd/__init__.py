@@ -9,7 +9,7 @@ Load with `import sw_amd` after `_swpkg.load()` (the directory name carries
 hyphens, so it is registered under the module name `sw_amd`).
 """
 from . import capi, dist, fasta, solver, synth  # noqa: F401
-from .capi import Database, Handle, SWError, builtin_matrix, encode, topk  # noqa: F401
+from .capi import Database, Group, Handle, SWError, builtin_matrix, encode, topk  # noqa: F401
 from .fasta import FASTADatabase, FASTAQuery, SubjectSequence  # noqa: F401
 from .solver import smith_waterman_cuda, smith_waterman_cuda_char  # noqa: F401
 

@@ -30,7 +30,8 @@ EXPORTED = (
     "sw_timing_reset", "sw_timing_total", "sw_last_kernel", "sw_last_intra_kernel",
     "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_topk_device_ids", "sw_score_pair", "sw_align",
     "sw_db_save", "sw_db_load", "sw_db_subjects", "sw_db_create_synthetic", "sw_synth_tables",
-    "sw_synth_lengths",
+    "sw_synth_lengths", "sw_group_create", "sw_group_destroy", "sw_group_info", "sw_group_handle",
+    "sw_group_db_create", "sw_group_db_free", "sw_group_db_shard", "sw_group_scan", "sw_group_topk",
 )
 
 
@@ -127,6 +128,15 @@ def lib():
         "sw_topk_keys_device": (ctypes.c_int, [vp, vp, i64, i32, vp]),
         "sw_topk_device_ids": (ctypes.c_int, [vp, vp, i64, vp, i32, vp]),
         "sw_score_pair": (ctypes.c_int, [vp, u8p, i32, u8p, i32, ctypes.POINTER(Scoring), i32p]),
+        "sw_group_create": (ctypes.c_int, [i32p, i32, ctypes.POINTER(vp)]),
+        "sw_group_destroy": (ctypes.c_int, [vp]),
+        "sw_group_info": (ctypes.c_char_p, [vp]),
+        "sw_group_handle": (ctypes.c_int, [vp, i32, ctypes.POINTER(vp)]),
+        "sw_group_db_create": (ctypes.c_int, [vp, u8p, i64p, i64, i32p, ctypes.POINTER(vp)]),
+        "sw_group_db_free": (ctypes.c_int, [vp]),
+        "sw_group_db_shard": (ctypes.c_int, [vp, i32, i64p, i64p]),
+        "sw_group_scan": (ctypes.c_int, [vp, vp, u8p, i32, ctypes.POINTER(Scoring), i32p]),
+        "sw_group_topk": (ctypes.c_int, [vp, vp, u8p, i32, ctypes.POINTER(Scoring), i32, i64p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -413,6 +423,82 @@ class Database:
         _check(lib().sw_scan_batch(self.handle.ptr, self._d, cp,
                                    offs.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), len(queries),
                                    sc.ptr(), out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return out
+
+
+class Group:
+    """Several GPUs of this process searching one database (sw_group_*):
+    residue-balanced shards, one host thread per device, RCCL all-gather of
+    the per-device top-K (a device listed twice: host exchange)."""
+
+    def __init__(self, devices):
+        devs = np.ascontiguousarray(devices, dtype=np.int32)
+        g = ctypes.c_void_p()
+        _check(lib().sw_group_create(devs.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(devs),
+                                     ctypes.byref(g)))
+        self._g = g
+        self.n = len(devs)
+
+    def info(self):
+        return lib().sw_group_info(self._g).decode()
+
+    def close(self):
+        if self._g:
+            lib().sw_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def database(self, residues, offsets, ids=None):
+        return GroupDatabase(self, residues, offsets, ids)
+
+
+class GroupDatabase:
+    def __init__(self, group, residues, offsets, ids=None):
+        self.group = group
+        r, rp = _u8(residues)
+        o = np.ascontiguousarray(offsets, dtype=np.int64)
+        n = len(o) - 1
+        idp = None
+        self.n_out = n
+        if ids is not None:
+            self._ids = np.ascontiguousarray(ids, dtype=np.int32)
+            idp = self._ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+            self.n_out = int(self._ids.max()) + 1 if n else 0
+        d = ctypes.c_void_p()
+        _check(lib().sw_group_db_create(group._g, rp, o.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n, idp,
+                                        ctypes.byref(d)))
+        self._d = d
+
+    def shard(self, k):
+        n, r = ctypes.c_int64(), ctypes.c_int64()
+        _check(lib().sw_group_db_shard(self._d, k, ctypes.byref(n), ctypes.byref(r)))
+        return n.value, r.value
+
+    def close(self):
+        if self._d:
+            lib().sw_group_db_free(self._d)
+            self._d = None
+
+    def scan(self, query_codes, matrix=None, gap_open=2, gap_extend=None):
+        q, qp = _u8(query_codes)
+        sc = _ScoringArg(matrix, gap_open, gap_extend)
+        out = np.zeros(self.n_out, dtype=np.int32)
+        _check(lib().sw_group_scan(self.group._g, self._d, qp, len(q), sc.ptr(),
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return out
+
+    def topk(self, query_codes, k, matrix=None, gap_open=2, gap_extend=None):
+        """int64 keys (score << 32 | 2^31-1-id), best first."""
+        q, qp = _u8(query_codes)
+        sc = _ScoringArg(matrix, gap_open, gap_extend)
+        out = np.zeros(k, dtype=np.int64)
+        _check(lib().sw_group_topk(self.group._g, self._d, qp, len(q), sc.ptr(), k,
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
         return out
 
 

@@ -7,7 +7,9 @@
 // main.cpp:20,62-72).
 //
 // Extra, optional: --metrics-json prints one JSON line after the METRICS
-// block with the kernel-only time and algorithmic GCUPS (unpadded cells).
+// block with the wall-clock split (FASTA parse, flatten + encode, upload =
+// pack + H2D, scan); --gpus N shards the database over N GPUs (sw_group:
+// residue-balanced shards, one host thread per device; same output).
 // Binary databases: --make-db OUT with --db FASTA
 // writes OUT (sw_db_save) and exits; --db X.swdb scans such a file with the
 // same output (same ids, same order) as the FASTA it came from, without
@@ -24,8 +26,7 @@
 #include "FASTAParsers.h"
 #include "SWSolver.h"
 #include "sw_amd.h"
-
-void sw_save_fasta_db(FASTADatabase& fdb, const std::string& path);  // swsolver.cpp
+#include "sw_solver_ext.h"
 
 namespace {
 
@@ -40,7 +41,8 @@ void usage() {
               << "  --help                Display this help message\n"
               << "  --query arg           Path to query file (required)\n"
               << "  --db arg              Path to database file (required; FASTA, or a .swdb file)\n"
-              << "  --make-db arg         Write the FASTA --db as a binary .swdb database and exit\n";
+              << "  --make-db arg         Write the FASTA --db as a binary .swdb database and exit\n"
+              << "  --gpus arg            Shard the FASTA database over this many GPUs (default 1)\n";
 }
 
 }  // namespace
@@ -63,7 +65,7 @@ int main(int argc, char* argv[]) {
             if (i + 1 >= argc) { usage(); return 1; }
             val = argv[++i];
         }
-        if (key != "query" && key != "db" && key != "metrics-json" && key != "make-db") {
+        if (key != "query" && key != "db" && key != "metrics-json" && key != "make-db" && key != "gpus") {
             std::cerr << "unrecognised option '--" << key << "'\n";
             return 1;
         }
@@ -87,6 +89,11 @@ int main(int argc, char* argv[]) {
         usage();
         return 1;
     }
+    if (opt.count("gpus")) {
+        const int n = std::atoi(opt["gpus"].c_str());
+        if (n < 1) { usage(); return 1; }
+        sw_solver_set_gpus(n);
+    }
     const std::string& dbpath = opt["db"];
     const bool binary = dbpath.size() > 5 && dbpath.compare(dbpath.size() - 5, 5, ".swdb") == 0;
 
@@ -99,11 +106,18 @@ int main(int argc, char* argv[]) {
     vector<seqid_score> result;
     result.reserve(600000);
     int64_t num_subjects = 0, length_sum = 0;
-    double solve_s = 0;
+    double solve_s = 0, parse_s = 0;
     if (!binary) {
+        const double t_parse = now_s();
         FASTADatabase db(dbpath);
+        parse_s = now_s() - t_parse;
         const double t_solve = now_s();
-        smith_waterman_cuda(query, db, result);
+        try {
+            smith_waterman_cuda(query, db, result);
+        } catch (const std::exception& e) {
+            std::cerr << e.what() << "\n";
+            return 1;
+        }
         solve_s = now_s() - t_solve;
         num_subjects = db.numSubjects;
         length_sum = db.subjectLengthSum;
@@ -155,9 +169,12 @@ int main(int argc, char* argv[]) {
     cout << "Performance: " << 1E-9 * (querySequence.length() * static_cast<double>(length_sum)) / seconds_elapsed
          << " GCUPS." << endl;
     if (opt.count("metrics-json")) {
+        const sw_solver_timing t = sw_solver_last_timing();
         cout << "{\"query_len\": " << querySequence.length() << ", \"subjects\": " << num_subjects
              << ", \"padded_residues\": " << length_sum << ", \"wall_s\": " << seconds_elapsed
-             << ", \"solve_s\": " << solve_s << "}" << endl;
+             << ", \"parse_s\": " << parse_s << ", \"solve_s\": " << solve_s << ", \"flatten_s\": " << t.flatten_s
+             << ", \"upload_s\": " << t.upload_s << ", \"scan_s\": " << t.scan_s << ", \"gpus\": " << t.gpus
+             << "}" << endl;
     }
     return 0;
 }

@@ -155,6 +155,8 @@ void parallel_for(int64_t n, F&& f) {
 
 }  // namespace
 
+int swk::set_error(int code, const std::string& msg) { return fail(code, msg); }
+
 // ---------------------------------------------------------------------------
 struct ScanEvents {
     // 0 fork, 1 intra done (side), 2 inter done (main), 3 end, and around

@@ -5,7 +5,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace swk {
+
+// Record `msg` as this thread's sw_last_error() text and return `code`
+// (sw_capi.cpp; used by the other host translation units, e.g. sw_group.cpp).
+int set_error(int code, const std::string& msg);
 
 constexpr int kLanes = 64;        // one database subject per lane (wave64)
 constexpr int kGroupCols = 16;    // residue columns per packed group

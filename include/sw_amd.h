@@ -269,6 +269,39 @@ SW_API int sw_score_pair(sw_handle* h, const uint8_t* query, int32_t qlen,
                   const uint8_t* subject, int32_t slen, const sw_scoring* sc,
                   int32_t* score);
 
+/* ---- several GPUs of one process -------------------------
+ * Replaces the reference's single-GPU scan loop (main.cpp:54-56 ->
+ * smith_waterman_cuda, SWSolver.cu:266-404) with one database sharded over
+ * the devices of a group.  sw_group_create: one handle per listed device and,
+ * for two or more DISTINCT devices, an RCCL communicator over them
+ * (ncclCommInitAll; librccl is loaded at run time).  A device listed twice
+ * is allowed (one-GPU tests): the top-K exchange then goes through the host.
+ * sw_group_db_create: LPT shards over subject lengths (longest first, each to
+ * the lightest shard, lowest index on ties: residue-balanced and
+ * deterministic), one resident sw_db per device, built in parallel.
+ * sw_group_scan: scores_host[id] of every subject (as sw_scan), the devices
+ * scanning concurrently (one host thread each).  sw_group_topk: the k best
+ * (score desc, id asc) as sw_topk_device keys in keys_host[k]: per-device
+ * top-k with global ids, ONE ncclAllGather of k int64 keys per device, merge
+ * on device 0.  All synchronous.                                          */
+typedef struct sw_group sw_group;
+typedef struct sw_gdb sw_gdb;
+SW_API int sw_group_create(const int32_t* devices, int32_t ndev, sw_group** out);
+SW_API int sw_group_destroy(sw_group* g);
+/* "rccl allgather (N ranks)" or "host (...)". */
+SW_API const char* sw_group_info(const sw_group* g);
+/* The handle of device slot d (owned by the group). */
+SW_API int sw_group_handle(sw_group* g, int32_t d, sw_handle** out);
+SW_API int sw_group_db_create(sw_group* g, const uint8_t* residues, const int64_t* offsets, int64_t n,
+                              const int32_t* ids, sw_gdb** out);
+SW_API int sw_group_db_free(sw_gdb* gdb);
+/* Subjects and residues of shard d. */
+SW_API int sw_group_db_shard(const sw_gdb* gdb, int32_t d, int64_t* n_subjects, int64_t* residues);
+SW_API int sw_group_scan(sw_group* g, const sw_gdb* gdb, const uint8_t* query, int32_t qlen,
+                         const sw_scoring* sc, int32_t* scores_host);
+SW_API int sw_group_topk(sw_group* g, const sw_gdb* gdb, const uint8_t* query, int32_t qlen,
+                         const sw_scoring* sc, int32_t k, int64_t* keys_host);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,129 @@
+#!/usr/bin/env python3
+"""The drop-in C++ path at Swiss-Prot scale (VERDICT r01 "what's missing" 2-3).
+
+Writes a deterministic synthetic FASTA of N records (synth.database, seed
+1782: the bench's C2 database; Swiss-Prot itself is not shipped),
+runs the reference's CLI contract (lib/main --query Q --db FASTA, main.cpp:
+19-74) on it with the wall-clock split (--metrics-json), checks EVERY id:score
+against the oracle (test infrastructure: the C restatement of cpu.cpp's
+recurrence with SWSolver.cu's BLOSUM50 / gap 2), writes the oracle's scores as
+golden files keyed by record index (the test/reference/*.txt format) and runs
+lib/sw_tests --suite all on them (swissprot_tests.cpp:40-75: Comparison of
+every id for P01008 and P02232, Performance of 17 queries).  Optionally the
+same with --gpus 2 over one device listed twice (SW_DEVICES=0,0).
+
+usage: dropin_scale.py [--n 570000] [--out DIR] [--threads T] [--gpus2]
+Prints one JSON summary line.
+"""
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+LIB = os.path.join(REPO, "ece1782-smith-waterman-cuda_amd", "lib")
+QDIR = os.path.join(REPO, "tests", "golden", "queries")
+LETTERS = np.frombuffer(b"ARNDCQEGHILKMFPSTWYV", dtype=np.uint8)
+
+
+def write_fasta(path, res, offs, width=60):
+    with open(path, "wb") as f:
+        for k in range(len(offs) - 1):
+            s = LETTERS[res[offs[k]:offs[k + 1]]].tobytes()
+            f.write(b">sp|S%07d|SYN_%d synthetic\n" % (k, k))
+            for j in range(0, len(s), width):
+                f.write(s[j:j + width] + b"\n")
+
+
+def read_query(name):
+    with open(os.path.join(QDIR, name + ".fasta")) as f:
+        return "".join(f.read().split("\n")[1:])
+
+
+def run_main(query, fasta, gpus=1, env=None):
+    cmd = [os.path.join(LIB, "main"), "--query", os.path.join(QDIR, query + ".fasta"), "--db", fasta,
+           "--metrics-json"]
+    if gpus > 1:
+        cmd += ["--gpus", str(gpus)]
+    t = time.perf_counter()
+    out = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=900)
+    wall = time.perf_counter() - t
+    if out.returncode:
+        raise SystemExit("main failed: " + out.stderr[-2000:])
+    lines = out.stdout.split("\n")
+    pairs = np.array([tuple(map(int, ln.split(":"))) for ln in lines if ln and ln[0].isdigit() and ":" in ln],
+                     dtype=np.int64)
+    metrics = json.loads([ln for ln in lines if ln.startswith("{")][-1])
+    gcups = float(re.search(r"Performance: ([0-9.eE+-]+) GCUPS", out.stdout).group(1))
+    metrics["reference_formula_gcups"] = gcups
+    metrics["process_wall_s"] = round(wall, 3)
+    return pairs, metrics, out.stdout
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=570000)
+    ap.add_argument("--out", default="/tmp/dropin")
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--gpus2", action="store_true")
+    ap.add_argument("--no-harness", action="store_true")
+    args = ap.parse_args()
+    import _swpkg
+    import sw_oracle
+    sw = _swpkg.load()
+    os.makedirs(args.out, exist_ok=True)
+    fasta = os.path.join(args.out, "synth%d.fasta" % args.n)
+    t = time.perf_counter()
+    res, offs = sw.synth.database(args.n, shard=0)
+    write_fasta(fasta, res, offs)
+    gen_s = time.perf_counter() - t
+    summary = {"records": args.n, "residues": int(offs[-1]), "fasta_bytes": os.path.getsize(fasta),
+               "fasta_write_s": round(gen_s, 2), "runs": {}}
+    mat = sw_oracle.matrix()
+    ok_all = True
+    for q in ("P02232", "P01008"):
+        qs = read_query(q)
+        qs += "/" * (-len(qs) % 8)  # the reference pads the query to x8 (SWSolver.cu:267-269)
+        t = time.perf_counter()
+        want = sw_oracle.scan(sw_oracle.encode(qs), res, offs, mat=mat, gap_open=2, gap_extend=2,
+                              nthreads=args.threads)
+        oracle_s = time.perf_counter() - t
+        with open(os.path.join(args.out, q + ".synth.scores"), "w") as f:
+            f.write("\n".join(str(int(x)) for x in want) + "\n")
+        pairs, metrics, _ = run_main(q, fasta)
+        got = np.zeros(args.n, dtype=np.int64)
+        got[pairs[:, 0]] = pairs[:, 1]
+        ok = len(pairs) == args.n and len(np.unique(pairs[:, 0])) == args.n and bool(np.array_equal(got, want))
+        run = {"main": metrics, "all_scores_equal_oracle": ok, "mismatches": int((got != want).sum()),
+               "oracle_s": round(oracle_s, 2), "oracle_threads": args.threads}
+        if args.gpus2:
+            env = dict(os.environ, SW_DEVICES="0,0")
+            pairs2, m2, _ = run_main(q, fasta, gpus=2, env=env)
+            run["main_gpus2_one_device_twice"] = m2
+            run["gpus2_output_identical"] = bool(np.array_equal(pairs2, pairs))
+            ok = ok and run["gpus2_output_identical"]
+        ok_all = ok_all and ok
+        summary["runs"][q] = run
+    if not args.no_harness:
+        t = time.perf_counter()
+        h = subprocess.run([os.path.join(LIB, "sw_tests"), "--suite", "all", "--db", fasta, "--golden-dir", args.out,
+                            "--golden-suffix", ".synth.scores", "--queries", QDIR],
+                           capture_output=True, text=True, timeout=1800)
+        summary["sw_tests"] = {"rc": h.returncode, "wall_s": round(time.perf_counter() - t, 1),
+                               "tail": h.stdout.strip().split("\n")[-1],
+                               "performance_lines": [ln for ln in h.stdout.split("\n") if "GCUPS" in ln]}
+        ok_all = ok_all and h.returncode == 0
+    summary["ok"] = ok_all
+    print(json.dumps(summary), flush=True)
+    return 0 if ok_all else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
