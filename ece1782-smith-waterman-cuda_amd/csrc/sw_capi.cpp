@@ -306,12 +306,23 @@ namespace {
 // inter, profiles/r01_c5/), so everything longer than 64 residues goes there.
 constexpr int64_t kSmallDbSubjects = 64 * 1000;
 
+// Databases smaller than ~kFillSubjects (C2's 570,000 subjects are ~4.3
+// 64-subject blocks per wave slot of the 256-CU GPU) — e.g. a rank's share
+// of a strong-scaled database — have too few blocks to hide the widest ones:
+// the scan time becomes the widest block's latency (width x passes / 2 for
+// a wave pair) while a long subject on the wavefront kernel takes only
+// (length + 64) steps.  The threshold then shrinks as sqrt(n / kFillSubjects),
+// measured on C2's 1/2, 1/4 and 1/8 shares (profiles/r02_strong/
+// threshold_sweep_*: best 1,536-2,048 / 1,024 / 600-704).
+constexpr double kFillSubjects = 570000.0;
+
 int32_t default_long_threshold(const sw_db* db) {
     if (db->n == 0) return 1536;
     const double mean = static_cast<double>(db->residues) / static_cast<double>(db->n);
     if (db->n < kSmallDbSubjects && mean >= 256) return 64;
-    const double t = 5.7 * mean;
-    return static_cast<int32_t>(std::min(8192.0, std::max(1024.0, t)));
+    const double fill = db->n < kSmallDbSubjects ? 1.0 : std::min(1.0, static_cast<double>(db->n) / kFillSubjects);
+    const double t = 5.7 * mean * std::sqrt(fill);
+    return static_cast<int32_t>(std::min(8192.0, std::max(fill < 1.0 ? 512.0 : 1024.0, t)));
 }
 
 void free_dev(sw_db* db) {
@@ -702,6 +713,17 @@ int32_t coop_blocks(const sw_db* db, int divisor) {
 // disables).
 constexpr int64_t kPairDivisor = 200000;
 
+// Waves per group for those blocks: pairs; SW_PAIR_GROUP=4 runs quads.
+// Measured on C2's 1/8 share (profiles/r02_strong/): the inter kernel alone
+// is fastest with quads over every block >= 64 wide (1.08 ms vs 1.29 for
+// pairs), but beside the concurrent long-subject kernel, whose workgroups
+// are dispatched first, a quad waits for a whole free workgroup slot and the
+// scan is slower (2.21 vs 1.77 ms).
+int pair_group(const sw_db*) {
+    if (const char* e = std::getenv("SW_PAIR_GROUP")) return std::atoi(e) == 4 ? 4 : 2;
+    return 2;
+}
+
 int32_t pair_blocks(const sw_db* db) {
     int64_t wmin = std::max<int64_t>(256, db->residues / kPairDivisor);
     if (const char* e = std::getenv("SW_PAIR_WIDTH")) wmin = std::atoll(e);
@@ -1042,7 +1064,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             HIPCHECK(hipEventRecord(h->fork2, h->stream));
             HIPCHECK(hipStreamWaitEvent(h->side2, h->fork2, 0));
             HIPCHECK(hipEventRecord(h->ev[4], h->side2));
-            HIPCHECK(swk::launch_inter_x2p(c, affine, f16, false, h->side2));
+            HIPCHECK(swk::launch_inter_x2p(c, affine, f16, false, pair_group(db), h->side2));
             HIPCHECK(hipEventRecord(h->ev[5], h->side2));
             HIPCHECK(hipEventRecord(h->coop_done, h->side2));
             ++h->launches;
@@ -1059,7 +1081,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             HIPCHECK(hipEventRecord(h->fork2, h->stream));
             HIPCHECK(hipStreamWaitEvent(h->side2, h->fork2, 0));
             HIPCHECK(hipEventRecord(h->ev[4], h->side2));
-            HIPCHECK(swk::launch_inter_x2p(c, affine, false, false, h->side2));
+            HIPCHECK(swk::launch_inter_x2p(c, affine, false, false, 2, h->side2));
             HIPCHECK(hipEventRecord(h->ev[5], h->side2));
             HIPCHECK(hipEventRecord(h->coop_done, h->side2));
             ++h->launches;
@@ -1072,7 +1094,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             // one launch: pairs for blocks [nr, npair), one wave per block after
             a.blk_base = nr;
             a.blk_first = std::max(npair, nr);
-            HIPCHECK(swk::launch_inter_x2p(a, affine, f16, true, h->stream));
+            HIPCHECK(swk::launch_inter_x2p(a, affine, f16, true, pair_group(db), h->stream));
         } else {
             HIPCHECK(swk::launch_inter(a, affine, x2_ok, h->stream));
         }

@@ -434,8 +434,8 @@ __device__ __forceinline__ void ring_load(uint32_t (&v)[SG], const int4* ring, i
 
 // One pass (rows [s0, s0 + 2R)) of one 64-subject block.  PAIR: the pass
 // is part of a wave pair's pipeline (sw_inter_x2p): the boundary comes from /
-// goes to the partner wave through an LDS ring instead of HBM when in_ring /
-// out_ring, and every sub-group ends with one workgroup barrier (a tick).
+// goes to the partner wave through an LDS ring instead of HBM when ring_in /
+// ring_out are set, and every sub-group ends with one workgroup barrier (a tick).
 //
 // CHAIN (single-wave blocks): all passes of the block in ONE sweep over
 // npass x ncols virtual columns.  The low strip enters pass k at virtual
@@ -448,7 +448,7 @@ __device__ __forceinline__ void ring_load(uint32_t (&v)[SG], const int4* ring, i
 // k-1's high strip at least one sub-group earlier (ncols >= 32).
 template <int R, int SG, bool AFFINE, bool F16, bool PAIR, int CR = 16, bool CHAIN = false>
 __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32_t ncols, uint64_t base, int lane,
-                                         int s0, Best<F16>& best, int4* ring, bool in_ring, bool out_ring,
+                                         int s0, Best<F16>& best, const int4* ring_in, int4* ring_out,
                                          int* tick) {
     static_assert(!(CHAIN && PAIR), "chained passes: single-wave blocks only");
     // SG: sub-group width = the lag (columns) between the two strips
@@ -512,7 +512,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     for (int q = 0; q < SG / 4; ++q) rp[q] = 0x19191919u;  // virtual columns before the subject
     load_codes<SG>(rc, a.residues + base, true);
     if (!first) {
-        if (PAIR && in_ring) ring_load<SG>(bin, ring, 0, lane);
+        if (PAIR && ring_in) ring_load<SG>(bin, ring_in, 0, lane);
         else load_pairs<SG>(bin, reinterpret_cast<const int32_t*>(bnd) + base);
     }
     int4 PL[2][CQ], PH[2][CQ];
@@ -580,7 +580,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
         if (has_next) {
             load_codes<SG>(rn, a.residues + base + noff, next_lo);
             if (!next_first && next_lo) {
-                if (PAIR && in_ring) ring_load<SG>(bin_n, ring, (ncol / SG) % kRingSlots, lane);
+                if (PAIR && ring_in) ring_load<SG>(bin_n, ring_in, (ncol / SG) % kRingSlots, lane);
                 else load_pairs<SG>(bin_n, reinterpret_cast<const int32_t*>(bnd) + base + noff);
             }
         }
@@ -722,8 +722,8 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
 #pragma unroll
             for (int q = 0; q < SG; ++q) hb[q] = AFFINE ? hi_hi(dl_h[q], dl_f[q]) : (dl_h[q] >> 16);
             const uint32_t pc = CHAIN ? (lo_c == 0 ? ncols - SG : lo_c - SG) : col0 - SG;
-            if (PAIR && out_ring) {
-                ring_store<SG>(ring, (pc / SG) % kRingSlots, lane, hb);
+            if (PAIR && ring_out) {
+                ring_store<SG>(ring_out, (pc / SG) % kRingSlots, lane, hb);
             } else {
                 const uint64_t poff = (pc >> 4) * kGroupBytes + (pc & 15);
                 store_pairs<SG>(reinterpret_cast<int32_t*>(bnd) + base + poff, hb);
@@ -763,77 +763,87 @@ __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>&
     best.init();
     const uint64_t t0 = trace_now();
     if (kChainPasses && ncols >= 32 && a.qpad > 2 * R) {
-        x2s_pass<R, SG, AFFINE, F16, false, CR, true>(a, L, ncols, base, lane, 0, best, nullptr, false, false, nullptr);
+        x2s_pass<R, SG, AFFINE, F16, false, CR, true>(a, L, ncols, base, lane, 0, best, nullptr, nullptr, nullptr);
     } else {
         for (int s0 = 0; s0 < a.qpad && ncols > 0; s0 += 2 * R)
-            x2s_pass<R, SG, AFFINE, F16, false, CR>(a, L, ncols, base, lane, s0, best, nullptr, false, false,
-                                                    nullptr);
+            x2s_pass<R, SG, AFFINE, F16, false, CR>(a, L, ncols, base, lane, s0, best, nullptr, nullptr, nullptr);
     }
     x2s_finish<F16>(a, blk, lane, best.value(a));
     trace_block(a, blk, t0, lane, 0);
 }
 
 // ---------------------------------------------------------------------------
-// sw_inter_x2p: a wave PAIR per wide block
+// sw_inter_x2p: a wave PAIR (or QUAD) per wide block
 // ---------------------------------------------------------------------------
 // The single-wave kernel runs a block's passes one after another, so a wide
 // block's latency is passes x width and the widest blocks (and the last,
 // ragged round of short ones) bound the scan (profiles/r01_tail/).  Here the
-// two waves of a pair split the passes: wave 0 runs passes 0, 2, 4, ..., wave 1
-// passes 1, 3, 5, ..., kPairLag sub-groups behind.  Within a round the
-// boundary (H | F << 16) goes from wave 0 to wave 1 through an LDS ring; from
-// one round to the next (wave 1 -> wave 0) through HBM as in the single-wave
-// kernel.  All four waves of the workgroup (two pairs, two blocks) share one
-// clock: one __syncthreads per sub-group.  Schedule of a block whose pass
-// takes S = width / SG + 1 ticks: round r of wave w starts at tick
-// r * max(S, 2 kPairLag) + kPairLag w, so
-//   * wave 1 reads sub-group g of the ring 2 ticks after wave 0 wrote it and
-//     wave 0 overwrites that slot only 3 ticks after the read (4 slots);
-//   * wave 0 of round r+1 prefetches from HBM what wave 1 of round r stored
-//     at least one tick earlier (period >= 6).
-// Block latency drops from 2P x S to P x S + kPairLag ticks for 2P passes;
-// the extra cost is one barrier per sub-group and the idle lag, so only the
-// widest blocks use it (sw_capi.cpp pair_blocks).
+// G waves of a group (G = 2: a pair, two groups per workgroup; G = 4: a quad,
+// the whole workgroup) split the passes: wave w runs passes w, w + G,
+// w + 2G, ..., kPairLag sub-groups behind wave w - 1.  Within a round the
+// boundary (H | F << 16) goes from wave w to wave w + 1 through an LDS ring;
+// from one round to the next (wave G-1 -> wave 0) through HBM as in the
+// single-wave kernel.  All four waves of the workgroup share one clock: one
+// __syncthreads per sub-group.  Schedule of a block whose pass takes
+// S = width / SG + 1 ticks: round r of wave w starts at tick
+// r * max(S, G kPairLag) + kPairLag w, so
+//   * wave w + 1 reads sub-group g of a ring 2 ticks after wave w wrote it and
+//     wave w overwrites that slot only 3 ticks after the read (4 slots); a
+//     new round's first write comes after the old round's last read;
+//   * wave 0 of round r+1 prefetches from HBM what wave G-1 of round r stored
+//     at least one tick earlier (period >= G kPairLag).
+// Block latency drops from P x S to ceil(P / G) x S + kPairLag (G - 1)
+// ticks for P passes; the extra cost is one barrier per sub-group and the
+// idle lag.  Pairs take the widest blocks of large databases; quads those of
+// small ones (a rank's share of a strong-scaled database), where too few
+// blocks exist to fill the GPU and the widest block's latency bounds the
+// scan (sw_capi.cpp pair_blocks / pair_group).
 constexpr int kPairLag = 3;
 
-__device__ __forceinline__ int pair_ticks(uint32_t ncols, int passes, int SG) {
+template <int G>
+__device__ __forceinline__ int group_ticks(uint32_t ncols, int passes, int SG) {
     if (ncols == 0 || passes <= 0) return 0;
     const int S = static_cast<int>(ncols) / SG + 1;
-    const int per = max(S, 2 * kPairLag);
-    return ((passes + 1) / 2 - 1) * per + S + (passes > 1 ? kPairLag : 0);
+    const int per = max(S, G * kPairLag);
+    int t = 0;
+    for (int p = max(0, passes - G); p < passes; ++p) t = max(t, (p / G) * per + kPairLag * (p % G) + S);
+    return t;
 }
 
-// MERGED: one launch for the whole scan — workgroups [0, (P+1)/2) run the
-// P = a.blk_first widest blocks by wave pairs, the rest run blocks
-// [P, nblocks) one per wave (x2s_block), so the dispatcher hands out work
-// widest-first across both forms (the LDS of the pair form, 53 KB, still
-// leaves 2 workgroups per CU, the register-bound occupancy of both).
-template <int R, int SG, bool AFFINE, bool F16, bool MERGED>
+// MERGED: one launch for the whole scan — workgroups [0, nwg_groups) run the
+// P = a.blk_first widest blocks by G-wave groups (4 / G blocks per
+// workgroup), the rest run blocks [P, nblocks) one per wave (x2s_block), so
+// the dispatcher hands out work widest-first across both forms (the LDS of
+// the group form, 53 KB for pairs and 61 KB for quads, still leaves 2
+// workgroups per CU, the register-bound occupancy of both).
+template <int R, int SG, bool AFFINE, bool F16, bool MERGED, int G>
 __global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
     static_assert(R % 16 == 0 && SG % 4 == 0, "shape");
+    static_assert(G == 2 || G == 4, "groups of 2 or 4 waves");
+    constexpr int NG = kWavesPerWG / G;  // groups (blocks) per workgroup
     __shared__ __attribute__((aligned(16))) X2Lds<R> lds[kWavesPerWG];
-    __shared__ int4 ring[kWavesPerWG / 2][kRingSlots * (SG / 4) * kLanes];
-    __shared__ uint32_t part[kWavesPerWG / 2][kLanes];
+    __shared__ int4 ring[NG * (G - 1)][kRingSlots * (SG / 4) * kLanes];
+    __shared__ uint32_t part[kWavesPerWG][kLanes];
     using P = PkCell<F16>;
     using V = typename P::V;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int npair = MERGED ? a.blk_first : a.nblocks;  // blocks [blk_base, npair) by pairs
-    const int pwg = (npair - a.blk_base + 1) / 2;           // their workgroups
+    const int npair = MERGED ? a.blk_first : a.nblocks;  // blocks [blk_base, npair) by groups
+    const int pwg = (npair - a.blk_base + NG - 1) / NG;    // their workgroups
     if (MERGED && static_cast<int>(blockIdx.x) >= pwg) {
         const int blk = npair + (blockIdx.x - pwg) * kWavesPerWG + wave;
         if (blk < a.nblocks) x2s_block<R, SG, AFFINE, F16>(a, blk, lds[wave], lane);
         return;  // workgroup-uniform branch: no barrier below is skipped by part of it
     }
-    const int pr = wave >> 1, w = wave & 1;
+    const int gi = wave / G, w = wave % G;
     const int passes = (a.qpad + 2 * R - 1) / (2 * R);
-    // the workgroup's clock runs to the longer of its two blocks
+    // the workgroup's clock runs to the longest of its blocks
     int tmax = 0;
-    for (int q = 0; q < 2; ++q) {
-        const int b = a.blk_base + blockIdx.x * 2 + q;
-        if (b < npair) tmax = max(tmax, pair_ticks(a.blk_groups[b] * kGroupCols, passes, SG));
+    for (int q = 0; q < NG; ++q) {
+        const int b = a.blk_base + blockIdx.x * NG + q;
+        if (b < npair) tmax = max(tmax, group_ticks<G>(a.blk_groups[b] * kGroupCols, passes, SG));
     }
-    const int blk = a.blk_base + blockIdx.x * 2 + pr;
+    const int blk = a.blk_base + blockIdx.x * NG + gi;
     Best<F16> best;
     best.init();
     int tick = 0;
@@ -841,53 +851,60 @@ __global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
     if (blk < npair) {
         const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
         const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
-        const int per = max(static_cast<int>(ncols) / SG + 1, 2 * kPairLag);
-        for (int p = w; p < passes && ncols > 0; p += 2) {
-            const int start = (p >> 1) * per + kPairLag * w;
+        const int per = max(static_cast<int>(ncols) / SG + 1, G * kPairLag);
+        const int4* rin = w > 0 ? ring[gi * (G - 1) + w - 1] : nullptr;
+        int4* rout = w < G - 1 ? ring[gi * (G - 1) + w] : nullptr;
+        for (int p = w; p < passes && ncols > 0; p += G) {
+            const int start = (p / G) * per + kPairLag * w;
             while (tick < start) {
                 __syncthreads();
                 ++tick;
             }
-            x2s_pass<R, SG, AFFINE, F16, true>(a, lds[wave], ncols, base, lane, p * 2 * R, best, ring[pr], w == 1,
-                                               w == 0, &tick);
+            x2s_pass<R, SG, AFFINE, F16, true>(a, lds[wave], ncols, base, lane, p * 2 * R, best, rin, rout, &tick);
         }
     }
     while (tick < tmax) {
         __syncthreads();
         ++tick;
     }
-    if (blk < npair && w == 1) part[pr][lane] = P::bits(best.value(a));
+    if (blk < npair && w > 0) part[wave][lane] = P::bits(best.value(a));
     __syncthreads();
     if (blk < npair && w == 0) {
-        const V o = P::from(part[pr][lane]);
         V b = best.value(a);
-        if constexpr (F16) b = __builtin_elementwise_maximum(b, o);
-        else b = max2(b, o);
+#pragma unroll
+        for (int u = 1; u < G; ++u) {
+            const V o = P::from(part[wave + u][lane]);
+            if constexpr (F16) b = __builtin_elementwise_maximum(b, o);
+            else b = max2(b, o);
+        }
         x2s_finish<F16>(a, blk, lane, b);
         trace_block(a, blk, t0, lane, 1);
     }
 }
 
-// merged = false: blocks [a.blk_base, a.nblocks) by wave pairs (the caller
-// passes the pair range's end as nblocks).  merged = true: the whole scan in
-// one launch, blocks [a.blk_base, a.blk_first) by pairs and [a.blk_first,
+// merged = false: blocks [a.blk_base, a.nblocks) by wave groups (the caller
+// passes the group range's end as nblocks).  merged = true: the whole scan in
+// one launch, blocks [a.blk_base, a.blk_first) by groups and [a.blk_first,
 // a.nblocks) one per wave.  The two-strips 32x8 shapes only.
-template <bool M>
+template <bool M, int G>
 static hipError_t launch_x2p(const InterArgs& a, bool affine, bool f16, hipStream_t s) {
+    constexpr int NG = kWavesPerWG / G;
     const int np = M ? a.blk_first : a.nblocks;
-    const int nwg = (np - a.blk_base + 1) / 2 + (M ? (a.nblocks - np + kWavesPerWG - 1) / kWavesPerWG : 0);
+    const int nwg = (np - a.blk_base + NG - 1) / NG + (M ? (a.nblocks - np + kWavesPerWG - 1) / kWavesPerWG : 0);
     if (nwg <= 0) return hipSuccess;
     const dim3 grid(nwg), block(kWavesPerWG * kLanes);
-    if (f16 && affine) hipLaunchKernelGGL((sw_inter_x2p<32, 8, true, true, M>), grid, block, 0, s, a);
-    else if (f16) hipLaunchKernelGGL((sw_inter_x2p<32, 8, false, true, M>), grid, block, 0, s, a);
-    else if (affine) hipLaunchKernelGGL((sw_inter_x2p<32, 8, true, false, M>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((sw_inter_x2p<32, 8, false, false, M>), grid, block, 0, s, a);
+    if (f16 && affine) hipLaunchKernelGGL((sw_inter_x2p<32, 8, true, true, M, G>), grid, block, 0, s, a);
+    else if (f16) hipLaunchKernelGGL((sw_inter_x2p<32, 8, false, true, M, G>), grid, block, 0, s, a);
+    else if (affine) hipLaunchKernelGGL((sw_inter_x2p<32, 8, true, false, M, G>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((sw_inter_x2p<32, 8, false, false, M, G>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_inter_x2p(const InterArgs& a, bool affine, bool f16, bool merged, hipStream_t s) {
+hipError_t launch_inter_x2p(const InterArgs& a, bool affine, bool f16, bool merged, int group, hipStream_t s) {
     if (a.nblocks <= 0 || a.qpad <= 0) return hipSuccess;
-    return merged ? launch_x2p<true>(a, affine, f16, s) : launch_x2p<false>(a, affine, f16, s);
+    if (group == 4) return merged ? launch_x2p<true, 4>(a, affine, f16, s) : launch_x2p<false, 4>(a, affine, f16, s);
+    if (group != 2) return hipErrorInvalidValue;
+    return merged ? launch_x2p<true, 2>(a, affine, f16, s) : launch_x2p<false, 2>(a, affine, f16, s);
 }
 
 template <int R, int SG>
@@ -909,9 +926,6 @@ hipError_t launch_inter_x2s(const InterArgs& a, int R, int SG, bool affine, bool
         return hipGetLastError();
     }
     if (R == 32 && SG == 8) return launch_x2s_shape<32, 8>(a, affine, s);
-    if (R == 32 && SG == 4) return launch_x2s_shape<32, 4>(a, affine, s);
-    if (R == 16 && SG == 8) return launch_x2s_shape<16, 8>(a, affine, s);
-    if (R == 48 && SG == 4) return launch_x2s_shape<48, 4>(a, affine, s);
     return hipErrorInvalidValue;
 }
 

@@ -153,11 +153,12 @@ bool inter_uses_f16(bool affine, int x2_ok);
 // The int16 packed kernel in list mode (blk_list / blk_count set): the
 // second stage of the fp16 rescue chain.
 hipError_t launch_inter_x2s_list(const InterArgs& a, bool affine, hipStream_t s);
-// Wave pairs over the widest blocks of a two-strips 32x8 scan (sw_inter_x2p):
-// same results as launch_inter_x2s, half the block latency.  merged: one
-// launch, blocks [0, blk_first) by pairs, [blk_first, nblocks) one per wave;
-// otherwise blocks [0, nblocks) by pairs only.
-hipError_t launch_inter_x2p(const InterArgs& a, bool affine, bool f16, bool merged, hipStream_t s);
+// Wave groups over the widest blocks of a two-strips 32x8 scan
+// (sw_inter_x2p; group = 2: pairs, 4: quads): same results as
+// launch_inter_x2s, 1/group of the block latency.  merged: one launch, blocks
+// [blk_base, blk_first) by groups, [blk_first, nblocks) one per wave;
+// otherwise blocks [blk_base, nblocks) by groups only.
+hipError_t launch_inter_x2p(const InterArgs& a, bool affine, bool f16, bool merged, int group, hipStream_t s);
 // true if the chosen inter kernel has a wave-pair form (two-strips 32x8).
 bool inter_has_pair(bool affine, int x2_ok);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.

@@ -1,0 +1,60 @@
+"""Block timeline of one rank's share of a strong-scaled C2 database (run
+with a -DSW_TRACE_BLOCKS build via SW_AMD_LIB and SW_TRACE_FILE set):
+blocks in flight over the launch, block durations against their width and
+form (single wave / group), the critical blocks.
+usage: exp_share_trace.py SHARD_OF [LONG_THRESHOLD]"""
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import _swpkg  # noqa: E402
+
+sw = _swpkg.load()
+path = os.environ["SW_TRACE_FILE"]
+S = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+T = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+res, offs = sw.synth.database(570000, shard=0)
+_, r, o = sw.dist.shard(res, offs, 0, S)
+with open(os.path.join(REPO, "tests", "golden", "queries", "P07327.fasta")) as f:
+    q = sw.encode("".join(f.read().split("\n")[1:]))
+h = sw.Handle(0)
+db = sw.Database(h, r, o, long_threshold=(T or None))
+m = sw.builtin_matrix(sw.MATRIX_BLOSUM62)
+for _ in range(4):
+    db.scan(q, matrix=m, gap_open=12, gap_extend=1)
+st = db.stats()
+tm = h.timing()
+db.close()
+t = np.fromfile(path, dtype=np.uint64).reshape(-1, 4)
+t0, t1 = t[:, 0].astype(np.int64), t[:, 1].astype(np.int64)
+ok = t1 > 0
+T0 = t0[ok].min()
+s, e = (t0[ok] - T0) / 100.0, (t1[ok] - T0) / 100.0  # microseconds (100 MHz)
+kind = t[ok, 3] >> 32
+blk = np.nonzero(ok)[0]
+lens = np.sort(o[1:] - o[:-1])[::-1][st["n_long"]:]
+width = np.array([lens[b * 64] for b in blk])  # longest subject of the block
+span = e.max()
+out = {"shard_of": S, "long_threshold": st["long_threshold"], "n_long": st["n_long"], "blocks": int(ok.sum()),
+       "group_blocks": int((kind == 1).sum()), "span_us": round(float(span), 1), "timing_ms": tm}
+grid = np.linspace(0, span, 21)
+out["inflight_every_5pct"] = [int(((s <= x) & (e > x)).sum()) for x in grid]
+dur = e - s
+for kd in (0, 1):
+    sel = kind == kd
+    if sel.any():
+        ww = width[sel]
+        out["form%d" % kd] = {"n": int(sel.sum()), "width_min_max": [int(ww.min()), int(ww.max())],
+                              "dur_us_min_med_max": [round(float(np.min(dur[sel])), 1),
+                                                     round(float(np.median(dur[sel])), 1),
+                                                     round(float(np.max(dur[sel])), 1)],
+                              "us_per_column_med": round(float(np.median(dur[sel] / ww)), 3),
+                              "start_us_max": round(float(s[sel].max()), 1)}
+crit = np.argsort(-e)[:6]
+out["last_to_end"] = [[int(blk[i]), int(kind[i]), int(width[i]), round(float(s[i]), 1), round(float(e[i]), 1)]
+                      for i in crit]
+print(json.dumps(out))

@@ -383,14 +383,17 @@ def test_fp16_guard_band(sw, oracle, handle, monkeypatch, qlen, selfhit, scoring
 
 @pytest.mark.parametrize("variant", ["f32x8", "y32x8"])
 @pytest.mark.parametrize("width", ["16", "300"])
-def test_wave_pair_kernel(sw, oracle, handle, monkeypatch, variant, width):
-    """sw_inter_x2p (the widest blocks by wave pairs; width 16 = every block):
-    1 to 15 passes (odd and even counts), narrow blocks (the 6-tick period
-    floor), an odd number of pair blocks, linear and affine, and planted
+@pytest.mark.parametrize("group", ["2", "4"])
+def test_wave_pair_kernel(sw, oracle, handle, monkeypatch, variant, width, group):
+    """sw_inter_x2p (the widest blocks by wave pairs or quads; width 16 =
+    every block): 1 to 15 passes (odd and even counts, fewer passes than
+    waves), narrow blocks (the 6- / 12-tick period floor), a block count not
+    a multiple of the groups per workgroup, linear and affine, and planted
     near-copies of the query whose blocks the fp16 kernel flags for the
     rescue chain — all against the oracle."""
     monkeypatch.setenv("SW_INTER_VARIANT", variant)
     monkeypatch.setenv("SW_PAIR_WIDTH", width)
+    monkeypatch.setenv("SW_PAIR_GROUP", group)
     r, o = sw.synth.database(1000, shard=17)
     q0 = sw.synth.query(900, shard=3)
     extra = [q0, q0[:450], q0[100:700]]
