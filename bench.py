@@ -656,7 +656,13 @@ def main():
         wave_gcups = float(qtot) / nq * wave_res / (wave_ms * 1e-3) / 1e9 if wave_ms > 0 else 0.0
         intra_res = residues - inter_res
         roof_kernel = kernel
-        if intra_res > inter_res:
+        if "+lpt" in kernel:
+            # one merged launch (sw_scan_lpt) scans every subject: the inter
+            # blocks and the long subjects' fp16 pass, longest work first
+            wave_res = residues
+            alg_bytes = residues + 12 * n
+            wave_gcups = float(qtot) / nq * residues / (wave_ms * 1e-3) / 1e9 if wave_ms > 0 else 0.0
+        elif intra_res > inter_res:
             # long-subject regime (C5): the intra kernel scans most cells
             roof_kernel = intra_kernel
             alg_bytes = intra_res + 12 * st["n_long"]
@@ -715,7 +721,7 @@ def main():
             "kernel_ms_per_scan": {"inter_phase": round(inter_ms, 4), "sw_inter": round(wave_ms, 4),
                                    "sw_inter_coop": round(coop_ms, 4), "sw_intra": round(intra_ms, 4),
                                    "scan_total": round(kt["total_ms"] / nsc, 4)},
-            "cells_split_per_step_rank0": {"sw_inter": float(qtot) * wave_res,
+            "cells_split_per_step_rank0": {"sw_inter": float(qtot) * (inter_res - side_res),
                                            "sw_inter_coop": float(qtot) * side_res,
                                            "sw_intra": float(qtot) * (residues - inter_res)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

@@ -262,6 +262,14 @@ struct sw_db {
     std::vector<int64_t> h_blk_res;      // unpadded residues per block
     int32_t last_ncoop = 0;              // blocks the last scan gave the coop kernel
     int32_t last_npair = 0;              // blocks the last scan ran by wave pairs
+    bool last_lpt = false;               // the last scan was one merged launch (sw_scan_lpt)
+    std::vector<int32_t> h_llen;         // long subjects' lengths, longest first
+    // sw_scan_lpt work tables (longest first), per scan shape
+    struct LptTable {
+        int32_t qpad, qpad_intra, ri, npair, group, n;
+        int32_t* d_order;
+    };
+    std::vector<LptTable> lpt_tables;
     bool last_pair_merged = false;
     // intra part (long subjects)
     int64_t nlong = 0;
@@ -335,6 +343,8 @@ void free_dev(sw_db* db) {
     db->d_bnd_h = nullptr; db->d_bnd_f = nullptr; db->d_rescue = nullptr; db->d_lres = nullptr; db->d_loff = nullptr;
     db->d_llen = nullptr; db->d_lid = nullptr; db->d_lbnd_h = nullptr; db->d_lbnd_f = nullptr;
     db->d_lrescue = nullptr;
+    for (auto& t : db->lpt_tables) (void)hipFree(t.d_order);
+    db->lpt_tables.clear();
     db->lcount_pending = false;
     db->i16_first.clear();  // the long partition may change
     db->icount_pending = false;
@@ -552,6 +562,7 @@ int build_db(sw_db* db) {
     HIPCHECK(hipStreamSynchronize(s));  // host vectors go out of scope
     db->h_blk_groups = blk_groups;
     db->h_blk_res = blk_res;
+    db->h_llen = llen;
     db->res_bytes = total;
     db->lres_bytes = ltotal;
     db->nblocks = nblocks;
@@ -733,6 +744,82 @@ int32_t pair_blocks(const sw_db* db) {
            static_cast<int64_t>(db->h_blk_groups[n]) * swk::kGroupCols >= wmin)
         ++n;
     return n;
+}
+
+// ---- one merged launch, longest work first (sw_scan_lpt) -----------------
+// Estimated duration of each workgroup of the merged grid: an inter tick (8
+// columns x 64 rows of a 64-subject block, one wave) ~7.4 us and an intra
+// step of sw_intra_x2<RI> ~0.157 us at RI = 6, scaled by its modeled
+// SIMD cycles (RI x 28.8 + 80) — measured on C2's 1/8 share
+// (profiles/r02_strong/traces/).  Only the order matters: the dispatcher
+// starts workgroups in grid order, so the longest work starts first.
+constexpr double kTickUs = 7.4;
+double intra_step_us(int ri) { return 0.157 * (ri * 28.8 + 80.0) / (6 * 28.8 + 80.0); }
+
+// Ticks of a single-wave block (x2s_block: chained passes when ncols >= 32).
+double single_ticks(int64_t ncols, int passes) {
+    if (ncols <= 0) return 0;
+    if (ncols >= 32 && passes > 1) return static_cast<double>(passes) * ncols / 8 + 1;
+    return static_cast<double>(passes) * (ncols / 8 + 1);
+}
+
+double group_ticks_host(int64_t ncols, int passes, int G) {
+    if (ncols <= 0 || passes <= 0) return 0;
+    const int64_t S = ncols / 8 + 1;
+    const int64_t per = std::max<int64_t>(S, 3 * G);
+    int64_t t = 0;
+    for (int p = std::max(0, passes - G); p < passes; ++p) t = std::max<int64_t>(t, (p / G) * per + 3 * (p % G) + S);
+    return static_cast<double>(t);
+}
+
+// The work table of sw_scan_lpt for this scan shape (built once, cached).
+int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int group, const int32_t** order,
+              int* n) {
+    for (const auto& t : db->lpt_tables)
+        if (t.qpad == qpad && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == group) {
+            *order = t.d_order;
+            *n = t.n;
+            return SW_OK;
+        }
+    const int passes = qpad / 64;
+    const int NG = swk::kWavesPerWG / group;
+    const int64_t nb = db->nblocks;
+    const int64_t pwg = (npair + NG - 1) / NG;
+    const int64_t swg = (nb - npair + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
+    const int64_t iwg = (((db->nlong + 1) / 2) + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
+    const int nch = qpad_intra / (swk::kLanes * ri);
+    std::vector<std::pair<double, int32_t>> w;
+    w.reserve(static_cast<size_t>(pwg + swg + iwg));
+    auto width = [&](int64_t b) { return static_cast<int64_t>(db->h_blk_groups[b]) * swk::kGroupCols; };
+    for (int64_t g = 0; g < pwg; ++g) {
+        double c = 0;
+        for (int q = 0; q < NG; ++q)
+            if (g * NG + q < npair) c = std::max(c, group_ticks_host(width(g * NG + q), passes, group));
+        w.emplace_back(c * kTickUs, static_cast<int32_t>(g));
+    }
+    for (int64_t g = 0; g < swg; ++g)  // widest first: the workgroup's first block bounds it
+        w.emplace_back(single_ticks(width(npair + g * swk::kWavesPerWG), passes) * kTickUs,
+                       static_cast<int32_t>(pwg + g));
+    for (int64_t g = 0; g < iwg; ++g)
+        w.emplace_back((db->h_llen[static_cast<size_t>(8 * g)] + swk::kLanes - 1) * nch * intra_step_us(ri),
+                       static_cast<int32_t>(-1 - g));
+    std::stable_sort(w.begin(), w.end(), [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) {
+        return x.first > y.first;
+    });
+    std::vector<int32_t> ord(w.size());
+    for (size_t k = 0; k < w.size(); ++k) ord[k] = w[k].second;
+    sw_db::LptTable t{qpad, qpad_intra, ri, npair, group, static_cast<int32_t>(ord.size()), nullptr};
+    HIPCHECK(hipMalloc(reinterpret_cast<void**>(&t.d_order), ord.size() * sizeof(int32_t)));
+    HIPCHECK(hipMemcpy(t.d_order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    db->device_bytes += ord.size() * sizeof(int32_t);
+    if (db->lpt_tables.size() >= 8) {
+        (void)hipFree(db->lpt_tables.front().d_order);
+        db->lpt_tables.erase(db->lpt_tables.begin());
+    }
+    db->lpt_tables.push_back(t);
+    *order = t.d_order;
+    *n = t.n;
+    return SW_OK;
 }
 
 int next_events(sw_handle* h) {
@@ -926,16 +1013,34 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         int32_t* c2 = c1 ? db->d_lrescue + db->nlong + 1 : nullptr;
         if (cA || c1) HIPCHECK(swk::launch_reset_counters(cA, cB, mA, c1, c2, h->stream));
     }
+    // One merged launch for the fp16 scan, longest work first (sw_scan_lpt):
+    // the inter groups + single waves and the long subjects' fp16 pass, when
+    // the scan takes exactly that shape, on databases that do not fill the
+    // GPU many times over (n < kFillSubjects: a rank's share of a strong-
+    // scaled database).  Measured (profiles/r02_strong/lpt/): C2's 1/8 share
+    // 1.92 -> 1.45 ms, 1/4 2.57 -> 2.29, 1/2 equal; the whole C2 database
+    // 7.55 -> 7.70 ms, so it keeps two concurrent launches.  SW_LPT=0 / 1
+    // forces either form.
+    const char* lpt_env = std::getenv("SW_LPT");
+    const bool lpt_want = lpt_env ? lpt_env[0] == '1' : static_cast<double>(db->n) < kFillSubjects;
+    const bool lpt = lpt_want && db->nlong && db->nblocks && intra_x2 && !intra_i16_first &&
+                     f16 && rescue && npair && pair_merged && !ncoop && i16_span == 0 &&
+                     swk::lpt_supported(pair_group(db), ri2);
+    db->last_lpt = lpt;
     // fork: the side stream starts when the main stream reaches ev[0]
     HIPCHECK(hipEventRecord(h->ev[0], h->stream));
     h->last_intra = "none";
     // the long subjects' stream: a side stream, concurrent with the inter
     // kernels (SW_INTRA_SERIAL=1: the main stream, before them — to measure
-    // what the concurrency costs the inter kernel)
+    // what the concurrency costs the inter kernel); with the merged launch,
+    // the main stream after it (only the rescue stages are left to run)
     const char* iser = std::getenv("SW_INTRA_SERIAL");
-    hipStream_t is = (iser && iser[0] == '1') ? h->stream : h->side;
-    if (db->nlong) {
-        HIPCHECK(hipStreamWaitEvent(is, h->ev[0], 0));
+    hipStream_t is = (lpt || (iser && iser[0] == '1')) ? h->stream : h->side;
+    swk::IntraArgs lpt_intra{};
+    // the long subjects' kernels: all of them, or (lpt_done) those after the
+    // fp16 pass the merged launch ran
+    auto launch_long = [&](bool lpt_done) -> int {
+        if (!lpt_done) HIPCHECK(hipStreamWaitEvent(is, h->ev[0], 0));
         swk::IntraArgs ia{};
         ia.residues = db->d_lres;
         ia.subj_off = db->d_loff;
@@ -970,7 +1075,11 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             } else {
                 x.rescue_count = list1;
                 x.rescue_list = list1 + 1;
-                HIPCHECK(swk::launch_intra_x2(x, ri2, is));
+                if (lpt && !lpt_done) {  // the merged launch runs this pass
+                    lpt_intra = x;
+                    return SW_OK;
+                }
+                if (!lpt_done) HIPCHECK(swk::launch_intra_x2(x, ri2, is));
                 // the fp16 pass's flagged count, read by a later scan
                 if (!db->h_lcount) {
                     HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&db->h_lcount), sizeof(int32_t),
@@ -1004,8 +1113,10 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         h->last_intra = intra_x2 ? "sw_intra_x2<" + std::to_string(ri2) + (intra_i16_first ? ",int16>" : ">")
                                  : "sw_intra<" + std::to_string(ri) + (affine ? ",affine>" : ",linear>");
         h->had_intra = true;
-    }
-    HIPCHECK(hipEventRecord(h->ev[1], db->nlong ? is : h->stream));
+        return SW_OK;
+    };
+    if (db->nlong && (rc = launch_long(false))) return rc;
+    if (!lpt) HIPCHECK(hipEventRecord(h->ev[1], db->nlong ? is : h->stream));
     if (db->nblocks) {
         swk::InterArgs a{};
         a.residues = db->d_res;
@@ -1090,7 +1201,20 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             HIPCHECK(hipEventRecord(h->ev[5], h->stream));
         }
         HIPCHECK(hipEventRecord(h->ev[6], h->stream));
-        if (npair && pair_merged) {
+        if (lpt) {
+            // one launch: the inter groups + single waves and the long
+            // subjects' fp16 pass, longest work first; then the long
+            // subjects' rescue stages
+            a.blk_base = 0;
+            a.blk_first = npair;
+            const int32_t* order = nullptr;
+            int nwg = 0;
+            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, pair_group(db), &order, &nwg))) return rc;
+            HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, order, nwg, affine, pair_group(db), ri2, h->stream));
+            HIPCHECK(hipEventRecord(h->ev[7], h->stream));
+            if ((rc = launch_long(true))) return rc;
+            HIPCHECK(hipEventRecord(h->ev[1], h->stream));
+        } else if (npair && pair_merged) {
             // one launch: pairs for blocks [nr, npair), one wave per block after
             a.blk_base = nr;
             a.blk_first = std::max(npair, nr);
@@ -1101,7 +1225,8 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         h->last_kernel = swk::inter_kernel_name(affine, x2_ok);
         if (npair) h->last_kernel.replace(0, std::strlen("sw_inter_x2s"), "sw_inter_x2p");  // + wave pairs
         if (nr) h->last_kernel += "+int16[0," + std::to_string(nr) + ")";
-        HIPCHECK(hipEventRecord(h->ev[7], h->stream));
+        if (lpt) h->last_kernel += "+lpt";
+        if (!lpt) HIPCHECK(hipEventRecord(h->ev[7], h->stream));
         ++h->launches;
         if (f16 && rescue && !db->icount_pending) {
             // the fp16 pass's flagged count and largest flagged block, read

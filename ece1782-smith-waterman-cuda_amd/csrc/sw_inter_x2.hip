@@ -31,6 +31,7 @@
 // recurrences equal the int32 ones (sw_kernels.hip) bit for bit.  sw_inter_x2s
 // also runs beyond that bound in guarded mode: lanes that reach kSat16 flag
 // their block for the int32 kernel (see the end of the kernel).
+#include "sw_intra_x2.h"
 #include "sw_kernels.h"
 
 namespace swk {
@@ -816,22 +817,33 @@ __device__ __forceinline__ int group_ticks(uint32_t ncols, int passes, int SG) {
 // the dispatcher hands out work widest-first across both forms (the LDS of
 // the group form, 53 KB for pairs and 61 KB for quads, still leaves 2
 // workgroups per CU, the register-bound occupancy of both).
+// The LDS of one workgroup of the group form: the waves' profile images, the
+// rings between consecutive waves of a group, the partial maxima.
+template <int R, int SG, int G>
+struct X2pSmem {
+    static constexpr int NG = kWavesPerWG / G;
+    X2Lds<R> lds[kWavesPerWG];
+    int4 ring[NG * (G - 1)][kRingSlots * (SG / 4) * kLanes];
+    uint32_t part[kWavesPerWG][kLanes];
+};
+
+// One workgroup's work (wgi = its index in the launch's numbering).
 template <int R, int SG, bool AFFINE, bool F16, bool MERGED, int G>
-__global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
+__device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, X2pSmem<R, SG, G>& sm) {
     static_assert(R % 16 == 0 && SG % 4 == 0, "shape");
     static_assert(G == 2 || G == 4, "groups of 2 or 4 waves");
     constexpr int NG = kWavesPerWG / G;  // groups (blocks) per workgroup
-    __shared__ __attribute__((aligned(16))) X2Lds<R> lds[kWavesPerWG];
-    __shared__ int4 ring[NG * (G - 1)][kRingSlots * (SG / 4) * kLanes];
-    __shared__ uint32_t part[kWavesPerWG][kLanes];
+    X2Lds<R>* lds = sm.lds;
+    auto& ring = sm.ring;
+    auto& part = sm.part;
     using P = PkCell<F16>;
     using V = typename P::V;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int npair = MERGED ? a.blk_first : a.nblocks;  // blocks [blk_base, npair) by groups
     const int pwg = (npair - a.blk_base + NG - 1) / NG;    // their workgroups
-    if (MERGED && static_cast<int>(blockIdx.x) >= pwg) {
-        const int blk = npair + (blockIdx.x - pwg) * kWavesPerWG + wave;
+    if (MERGED && wgi >= pwg) {
+        const int blk = npair + (wgi - pwg) * kWavesPerWG + wave;
         if (blk < a.nblocks) x2s_block<R, SG, AFFINE, F16>(a, blk, lds[wave], lane);
         return;  // workgroup-uniform branch: no barrier below is skipped by part of it
     }
@@ -840,10 +852,10 @@ __global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
     // the workgroup's clock runs to the longest of its blocks
     int tmax = 0;
     for (int q = 0; q < NG; ++q) {
-        const int b = a.blk_base + blockIdx.x * NG + q;
+        const int b = a.blk_base + wgi * NG + q;
         if (b < npair) tmax = max(tmax, group_ticks<G>(a.blk_groups[b] * kGroupCols, passes, SG));
     }
-    const int blk = a.blk_base + blockIdx.x * NG + gi;
+    const int blk = a.blk_base + wgi * NG + gi;
     Best<F16> best;
     best.init();
     int tick = 0;
@@ -880,6 +892,68 @@ __global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
         x2s_finish<F16>(a, blk, lane, b);
         trace_block(a, blk, t0, lane, 1);
     }
+}
+
+template <int R, int SG, bool AFFINE, bool F16, bool MERGED, int G>
+__global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
+    __shared__ __attribute__((aligned(16))) X2pSmem<R, SG, G> sm;
+    x2p_wg<R, SG, AFFINE, F16, MERGED, G>(a, blockIdx.x, sm);
+}
+
+// ---------------------------------------------------------------------------
+// sw_scan_lpt: the inter scan (groups + single waves) and the long subjects'
+// fp16 wavefront kernel in ONE launch, longest work first
+// ---------------------------------------------------------------------------
+// Launched side by side on two streams, the long-subject kernel's workgroups
+// are dispatched first and hold slots the inter blocks wait for; on C2 the
+// inter launch takes 7.37 ms alone and 7.70 beside it, and on a rank's share
+// of a strong-scaled database single-wave blocks start hundreds of us late
+// (profiles/r02_strong/traces/).  Here one grid holds both kinds of
+// workgroup and order[blockIdx.x] names the work of each: >= 0 an inter
+// workgroup of the merged group launch (x2p_wg numbering), < 0 intra
+// workgroup -1 - order[..].  The host sorts the table by estimated duration
+// (block widths x passes x the tick cost, subject lengths x the step cost),
+// so the dispatcher starts the longest work first and fills the end with
+// the shortest (LPT).  LDS: the two kinds' buffers overlap (a workgroup is
+// one kind), so the occupancy stays the inter kernel's 2 workgroups per CU.
+template <int R, int SG, bool AFFINE, int G, int RI>
+__global__ __launch_bounds__(256, 2) void sw_scan_lpt(InterArgs a, IntraArgs ia, const int32_t* __restrict__ order) {
+    using Elem = typename ix2::IntraImg<RI, true>::Elem;
+    constexpr size_t kInter = sizeof(X2pSmem<R, SG, G>);
+    constexpr size_t kIntra = sizeof(Elem) * ix2::img_elems<RI, true>();
+    __shared__ __attribute__((aligned(16))) char smem[kInter > kIntra ? kInter : kIntra];
+    const int item = order[blockIdx.x];
+    if (item >= 0)
+        x2p_wg<R, SG, AFFINE, true, true, G>(a, item, *reinterpret_cast<X2pSmem<R, SG, G>*>(smem));
+    else
+        ix2::intra_x2_wg<RI, true, false>(ia, -1 - item, reinterpret_cast<Elem*>(smem));
+}
+
+template <int G, int RI>
+static void launch_lpt_t(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine,
+                         hipStream_t s) {
+    if (affine) hipLaunchKernelGGL((sw_scan_lpt<32, 8, true, G, RI>), dim3(n), dim3(kWavesPerWG * kLanes), 0, s, a, ia,
+                                   order);
+    else hipLaunchKernelGGL((sw_scan_lpt<32, 8, false, G, RI>), dim3(n), dim3(kWavesPerWG * kLanes), 0, s, a, ia,
+                            order);
+}
+
+bool lpt_supported(int group, int ri) { return (group == 2 || group == 4) && (ri == 4 || ri == 6 || ri == 8); }
+
+int lpt_inter_wgs(const InterArgs& a, int group) {
+    const int NG = kWavesPerWG / group;
+    return (a.blk_first - a.blk_base + NG - 1) / NG + (a.nblocks - a.blk_first + kWavesPerWG - 1) / kWavesPerWG;
+}
+
+hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine,
+                           int group, int ri, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (!lpt_supported(group, ri)) return hipErrorInvalidValue;
+#define SW_LPT(G_, RI_) \
+    if (group == G_ && ri == RI_) launch_lpt_t<G_, RI_>(a, ia, order, n, affine, s);
+    SW_LPT(2, 4) SW_LPT(2, 6) SW_LPT(2, 8) SW_LPT(4, 4) SW_LPT(4, 6) SW_LPT(4, 8)
+#undef SW_LPT
+    return hipGetLastError();
 }
 
 // merged = false: blocks [a.blk_base, a.nblocks) by wave groups (the caller

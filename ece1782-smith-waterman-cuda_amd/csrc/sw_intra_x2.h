@@ -1,0 +1,392 @@
+// sw_intra_x2.h — the body of the two-subjects-per-wave intra-sequence
+// kernel (sw_intra_x2.hip), shared with the merged scan launch
+// (sw_inter_x2.hip, sw_scan_lpt).
+//
+// The kernel: intra-sequence wavefront, TWO subjects per wave, packed
+// fp16 cell (the long-subject path; config C5).
+//
+// The anti-diagonal wavefront of sw_intra (sw_kernels.hip): lane t owns query
+// rows [c0 + t·RI, c0 + (t+1)·RI) of a 64·RI-row chunk and handles column
+// k − t at step k; the bottom row (H, F) and the residue codes move one lane
+// per step with DPP wave_shr:1, lane 0 is fed from the previous chunk pass's
+// boundary row, lane 63's output is collected for the next pass.  Here every
+// value is a PAIR: the low fp16 half belongs to subject 2p, the high half to
+// subject 2p+1 (adjacent in the length-sorted order, so their lengths are
+// close; the shorter one runs pad columns, score 0, to the longer one's end).
+// The cell is the two-strips kernel's (sw_inter_x2.hip) Farrar form on
+// v_pk_add_f16 / v_pk_maximum3_f16, so linear gaps run it with open = extend:
+//   h = max3(E, F, H_diag + S);  n = h − go;
+//   E = max3(E − ge, n, 0);      F = max3(F − ge, n, 0)
+// and the substitution pair is one v_perm_b32 of the two subjects' profile
+// words.  The four waves of a workgroup share one fp16 image of the chunk's
+// profile in LDS, [code][4-row quarter][lane][4 halves]: a lane's quarter is
+// 8 bytes at lane·8 within a 512-byte row, so a ds_read_b64 is bank-conflict
+// free whatever code each lane reads.  The waves stage each chunk together
+// and meet at one barrier per chunk (their subjects have near-equal lengths).
+//
+// Exactness: fp16 holds every integer up to 2048.  H grows by at most max S
+// per cell, so a subject whose running maximum reaches a.sat_limit =
+// 2048 − 2·max S − 26·ge (computed exactly) is appended to a.rescue_list.
+// The same kernel in int16 (IntraCell<false>, LIST) re-scores that list and
+// appends subjects near 32767 to a second list for the int32 sw_intra; when
+// the fp16 pass would flag most subjects (cheap linear gaps on long pairs)
+// the host runs the int16 form first over all of them (sw_capi.cpp).
+#pragma once
+
+#include <type_traits>
+
+#include "sw_kernels.h"
+
+namespace swk {
+namespace ix2 {
+
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ h2 hmax3(h2 a, h2 b, h2 c) {
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
+__device__ __forceinline__ uint32_t f16_bits(int v) {
+    return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, static_cast<_Float16>(v)));
+}
+
+// DPP wave_shr:1 (lane t gets lane t-1's value; lane 0 keeps `old`)
+__device__ __forceinline__ uint32_t shr1u(uint32_t old, uint32_t src) {
+    return static_cast<uint32_t>(
+        __builtin_amdgcn_update_dpp(static_cast<int>(old), static_cast<int>(src), 0x138, 0xf, 0xf, false));
+}
+
+constexpr int kCodes = kPadCode + 1;  // residue codes 0..24 and the pad code
+
+// fp16 pair of two int16 profile entries minus `b`
+__device__ __forceinline__ uint32_t f16x2_of(uint32_t w, int b) {
+    return f16_bits(static_cast<int16_t>(w & 0xffffu) - b) | (f16_bits(static_cast<int16_t>(w >> 16) - b) << 16);
+}
+
+typedef short s2 __attribute__((ext_vector_type(2)));
+
+// The cell's number format.  F16: exact integers up to 2048 (the default);
+// int16: up to 32767 (the rescue stage for subjects whose fp16 maximum nears
+// 2048, e.g. linear scoring with cheap gaps), wrapping add, no 3-input max.
+template <bool F16>
+struct IntraCell {
+    using V = h2;
+    static __device__ __forceinline__ V from(uint32_t x) { return __builtin_bit_cast(h2, x); }
+    static __device__ __forceinline__ uint32_t bits(V x) { return __builtin_bit_cast(uint32_t, x); }
+    static __device__ __forceinline__ V max2(V a, V b) { return __builtin_elementwise_maximum(a, b); }
+    static __device__ __forceinline__ V max3(V a, V b, V c) { return hmax3(a, b, c); }
+    static __device__ __forceinline__ uint32_t step(const IntraArgs& a, int j) { return a.f16_step[j]; }
+    static __device__ __forceinline__ uint32_t pair_of(int v) { const uint32_t b = f16_bits(v); return b | (b << 16); }
+    static __device__ __forceinline__ uint32_t convert(uint32_t w, int b) { return f16x2_of(w, b); }
+    static __device__ __forceinline__ int lo(V x) { return static_cast<int>(static_cast<float>(x.x)); }
+    static __device__ __forceinline__ int hi(V x) { return static_cast<int>(static_cast<float>(x.y)); }
+    static __device__ __forceinline__ bool flag(const IntraArgs& a, int b) { return b >= a.sat_limit; }
+};
+template <>
+struct IntraCell<false> {
+    using V = s2;
+    static __device__ __forceinline__ V from(uint32_t x) { return __builtin_bit_cast(s2, x); }
+    static __device__ __forceinline__ uint32_t bits(V x) { return __builtin_bit_cast(uint32_t, x); }
+    static __device__ __forceinline__ V max2(V a, V b) { return __builtin_elementwise_max(a, b); }
+    static __device__ __forceinline__ V max3(V a, V b, V c) { return max2(max2(a, b), c); }
+    static __device__ __forceinline__ uint32_t step(const IntraArgs& a, int j) { return pair_of(j * a.gap_extend); }
+    static __device__ __forceinline__ uint32_t pair_of(int v) {
+        const uint32_t b = static_cast<uint16_t>(v);
+        return b | (b << 16);
+    }
+    static __device__ __forceinline__ uint32_t convert(uint32_t w, int b) {
+        return static_cast<uint16_t>(static_cast<int16_t>(w & 0xffffu) - b) |
+               (static_cast<uint32_t>(static_cast<uint16_t>(static_cast<int16_t>(w >> 16) - b)) << 16);
+    }
+    static __device__ __forceinline__ int lo(V x) { return x.x; }
+    static __device__ __forceinline__ int hi(V x) { return x.y; }
+    // the int16 guard band (the biased values sit up to 26 ge above the true)
+    static __device__ __forceinline__ bool flag(const IntraArgs& a, int b) {
+        return b >= kSat16 - 26 * a.gap_extend || b < 0;
+    }
+};
+
+// A lane's rows of one code in the LDS image, 4 rows (int2) per element when
+// RI is a multiple of 4 (one ds_read_b64), 2 rows (one dword, ds_read_b32)
+// otherwise; either way lane l's element sits at l·size in a 64-element row,
+// so the reads are conflict-free whatever code each lane reads.
+template <int RI, bool F16>
+struct IntraImg {
+    static constexpr int kRows = RI % 4 == 0 ? 4 : 2;
+    using Elem = typename std::conditional<kRows == 4, int2, uint32_t>::type;
+    using LElem = __attribute__((address_space(3))) const Elem;
+    static constexpr int kPer = RI / kRows;  // elements per lane and code
+    static __device__ __forceinline__ uint32_t word(const Elem (&w)[kPer], int r) {
+        if constexpr (kRows == 4) return static_cast<uint32_t>((r & 2) ? w[r >> 2].y : w[r >> 2].x);
+        else return w[r >> 1];
+    }
+    // staging: the element of rows [4q, 4q + 4) or [2q, 2q + 2) of a lane
+    static __device__ __forceinline__ Elem load(const int16_t* p, int b) {
+        using C = IntraCell<F16>;
+        if constexpr (kRows == 4) {
+            const int2 v = *reinterpret_cast<const int2*>(p);
+            return make_int2(static_cast<int>(C::convert(static_cast<uint32_t>(v.x), b)),
+                             static_cast<int>(C::convert(static_cast<uint32_t>(v.y), b)));
+        } else {
+            return C::convert(*reinterpret_cast<const uint32_t*>(p), b);
+        }
+    }
+};
+
+// LIST: the rescue stage — subject pairs come from the device-side list of
+// the subjects the fp16 pass flagged (a.subj_list / a.list_count); the grid
+// covers the longest possible list and surplus workgroups return at once.
+// SW_IX2_PREFETCH: read the next step's profile words from LDS during this
+// step (its codes are known one step ahead), so the LDS latency is hidden
+// even when the SIMD's waves run in lockstep
+#ifndef SW_IX2_PREFETCH
+#define SW_IX2_PREFETCH 1
+#endif
+constexpr bool kPrefetch = SW_IX2_PREFETCH != 0;
+
+// The LDS image of one chunk: [code][element][lane] (img_elems(RI) elements).
+template <int RI, bool F16>
+__host__ __device__ constexpr int img_elems() { return kCodes * IntraImg<RI, F16>::kPer * kLanes; }
+
+// One workgroup's work (wgi = its index in the launch: subject pairs
+// 4 wgi .. 4 wgi + 3, one per wave); img: the workgroup's LDS image.
+template <int RI, bool F16, bool LIST>
+__device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typename IntraImg<RI, F16>::Elem* img) {
+    static_assert(RI % 2 == 0 && RI <= 16, "rows per lane");
+    constexpr int CH = kLanes * RI;  // query rows per chunk
+    using C = IntraCell<F16>;
+    using V = typename C::V;
+    using Img = IntraImg<RI, F16>;
+    using Elem = typename Img::Elem;
+    constexpr int NQ = Img::kPer;    // image elements per lane and code
+    constexpr int NB = 8;            // steps per bias period (one rebase each)
+    constexpr int NACC = RI + NB - 1;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int p = wgi * kWavesPerWG + wave;  // subject pair
+    int sa = 2 * p, sb = 2 * p + 1;
+    bool hasA = sa < a.nsubj, hasB = sb < a.nsubj;
+    if constexpr (LIST) {
+        const int n = __builtin_amdgcn_readfirstlane(*a.list_count);
+        if (wgi * 2 * kWavesPerWG >= n) return;  // workgroup-uniform
+        hasA = sa < n;
+        hasB = sb < n;
+        sa = hasA ? a.subj_list[sa] : 0;
+        sb = hasB ? a.subj_list[sb] : 0;
+    }
+    const int LA = hasA ? a.subj_len[sa] : 0;
+    const int LB = hasB ? a.subj_len[sb] : 0;
+    const int L = max(LA, LB);  // = LA (length-sorted), kept general
+    const uint64_t offA = hasA ? a.subj_off[sa] : 0;
+    const uint8_t* __restrict__ resA = a.residues + offA;
+    const uint8_t* __restrict__ resB = a.residues + (hasB ? a.subj_off[sb] : 0);
+    // the pair's boundary rows live in the longer subject's slots
+    uint32_t* bnd_h = reinterpret_cast<uint32_t*>(a.bnd_h) + (LA >= LB ? offA : (hasB ? a.subj_off[sb] : 0));
+    uint32_t* bnd_f = reinterpret_cast<uint32_t*>(a.bnd_f) + (LA >= LB ? offA : (hasB ? a.subj_off[sb] : 0));
+    const int16_t* prof16 = reinterpret_cast<const int16_t*>(a.prof);
+    auto step = [&](int j) { return C::from(C::step(a, j)); };  // (j ge, j ge)
+    const V gog = C::from(C::pair_of(a.gap_open - a.gap_extend));
+    // Biased cell (the two-strips kernel's, sw_inter_x2.hip): at step k,
+    // row i of a lane holds H~ = H + (i + k % NB) ge, E' and F~ likewise, so
+    // both gap extensions are the drift of the bias:
+    //   h = max3(E', F~, H_diag + S + 2 ge);  m = h - (go - ge)
+    //   E' = max(E', m);  F~ = max3(F~, m, (i + 1 + k % NB) ge)
+    // The bias is a function of the step, the same in every lane, so every
+    // NB steps all lanes rebase together (H, E' and the row -1 diagonal
+    // drop NB ge), and what crosses lanes (the bottom row's H and F, one step
+    // old) drops (RI - 1) ge (+ NB ge at a rebase step).  Maxima per
+    // anti-diagonal i + k % NB, two cells per v_pk_maximum3_f16.
+    V acc[NACC];
+#pragma unroll
+    for (int q = 0; q < NACC; ++q) acc[q] = C::from(0u);
+    constexpr uint32_t kPadPair = kPadCode | (kPadCode << 8);
+
+    for (int c0 = 0; c0 < a.qpad; c0 += CH) {
+        const bool first = (c0 == 0);
+        const bool last = (c0 + CH >= a.qpad);
+        __syncthreads();  // the previous chunk's LDS reads are done
+        // stage rows [c0, c0 + CH) of codes 0..25 as fp16 S + 2 ge (the
+        // linear profile is biased by the gap, a.bias)
+        for (int t = threadIdx.x; t < kCodes * NQ * kLanes; t += kWavesPerWG * kLanes) {
+            const int code = t / (NQ * kLanes);
+            const int u = t % (NQ * kLanes);
+            const int qq = u / kLanes, ln = u % kLanes;
+            img[t] = Img::load(prof16 + static_cast<size_t>(code) * a.prof_stride + c0 + ln * RI + Img::kRows * qq,
+                               a.bias - 2 * a.gap_extend);
+        }
+        __syncthreads();
+        if (!hasA && !hasB) continue;  // wave-uniform; the barriers above are shared
+
+        // state of step -1 (column -1 - lane: H = 0), before step 0's rebase
+        V H[RI], E[RI];
+#pragma unroll
+        for (int r = 0; r < RI; ++r) {
+            H[r] = step(r + NB - 1);
+            E[r] = C::from(0u);
+        }
+        // bottom row (H, F) of this lane one step back, and H of the row above
+        // at the previous column (row 0's diagonal): zeros of step -1
+        uint32_t hl = C::step(a, RI + NB - 2), fl = C::step(a, RI + NB - 1);
+        uint32_t up_prev = C::step(a, NB - 2);
+        uint32_t rc = kPadPair;        // codes (A | B << 8) of this lane's current column
+        uint32_t in_res = kPadPair, in_bh = 0, in_bf = 0, out_h = 0, out_f = 0;
+        const int nsteps = L + kLanes - 1;
+        // LDS byte address of this lane's element of code 0
+        const uint32_t lrow = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(img + lane));
+
+        constexpr uint32_t kCodeBytes = NQ * kLanes * sizeof(Elem);
+        // the profile words of code pair rcx (A | B << 8) for this lane
+        auto read_words = [&](uint32_t rcx, Elem (&wa)[NQ], Elem (&wb)[NQ]) {
+            typename Img::LElem* pa = reinterpret_cast<typename Img::LElem*>(
+                static_cast<uintptr_t>(lrow + (rcx & 0xffu) * kCodeBytes));
+            typename Img::LElem* pb = reinterpret_cast<typename Img::LElem*>(
+                static_cast<uintptr_t>(lrow + ((rcx >> 8) & 0xffu) * kCodeBytes));
+#pragma unroll
+            for (int qq = 0; qq < NQ; ++qq) {
+                wa[qq] = __builtin_bit_cast(Elem, pa[qq * kLanes]);
+                wb[qq] = __builtin_bit_cast(Elem, pb[qq * kLanes]);
+            }
+        };
+        auto codes_at = [&](int col) {
+            const uint32_t ca = col < LA ? resA[col] : kPadCode;
+            const uint32_t cb = col < LB ? resB[col] : kPadCode;
+            return ca | (cb << 8);
+        };
+        uint32_t in_res_nb = codes_at(lane);  // codes of the next block of 64 steps
+        Elem wa_n[NQ], wb_n[NQ];               // prefetched words of the next step
+        uint32_t rc_n = 0;
+
+        for (int k0 = 0; k0 < nsteps; k0 += kLanes) {
+            // lane-0 conveyors for steps k0 .. k0+63 (column k = step); the
+            // first chunk's row -1 is H = 0, F = 0 at the bias lane 0 reads
+            // them with (see the hand-off below)
+            {
+                const int col = k0 + lane;
+                in_res = in_res_nb;
+                in_res_nb = codes_at(col + kLanes);
+                const int bz = RI - 2 + (col % NB) + ((col % NB) == 0 ? NB : 0);
+                in_bh = (!first && col < L) ? bnd_h[col] : C::pair_of(bz * a.gap_extend);
+                in_bf = (!first && col < L) ? bnd_f[col] : C::pair_of((bz + 1) * a.gap_extend);
+            }
+            if (kPrefetch && k0 == 0) {
+                rc_n = shr1u(__builtin_amdgcn_readlane(in_res, 0), rc);
+                read_words(rc_n, wa_n, wb_n);
+            }
+            // whole bias periods (steps past nsteps run pad columns: harmless)
+            const int mend = min(kLanes, nsteps - k0);
+            for (int m0 = 0; m0 < mend; m0 += NB) {
+#pragma unroll
+                for (int b = 0; b < NB; ++b) {
+                    const int m = m0 + b;
+                    const uint32_t sbh = __builtin_amdgcn_readlane(in_bh, m);
+                    const uint32_t sbf = __builtin_amdgcn_readlane(in_bf, m);
+                    Elem wa[NQ], wb[NQ];
+                    if constexpr (kPrefetch) {
+                        rc = rc_n;
+#pragma unroll
+                        for (int qq = 0; qq < NQ; ++qq) {
+                            wa[qq] = wa_n[qq];
+                            wb[qq] = wb_n[qq];
+                        }
+                        // the next step's codes: lane 0 takes the next column
+                        // (the next block's first at the block's last step)
+                        const bool wrap = (b == NB - 1) && (m0 + NB == kLanes);
+                        const uint32_t sres_n = wrap ? __builtin_amdgcn_readlane(in_res_nb, 0)
+                                                     : __builtin_amdgcn_readlane(in_res, (m + 1) & (kLanes - 1));
+                        rc_n = shr1u(sres_n, rc);
+                        read_words(rc_n, wa_n, wb_n);
+                    } else {
+                        rc = shr1u(__builtin_amdgcn_readlane(in_res, m), rc);
+                        read_words(rc, wa, wb);
+                    }
+                    // hand-off: the row above's bottom (H, F) from one step back
+                    const V adj = step(RI - 1 + (b == 0 ? NB : 0));
+                    const uint32_t up0 = C::bits(C::from(shr1u(sbh, hl)) - adj);
+                    V f = C::from(shr1u(sbf, fl)) - adj;
+                    if (b == 0) {  // rebase: the bias period restarts
+                        const V reb = step(NB);
+#pragma unroll
+                        for (int r = 0; r < RI; ++r) {
+                            H[r] = H[r] - reb;
+                            E[r] = E[r] - reb;
+                        }
+                        up_prev = C::bits(C::from(up_prev) - reb);
+                    }
+                    // H_diag + S for every row first (from the previous
+                    // column's H), so H is then updated in place
+                    V T[RI];
+#pragma unroll
+                    for (int r = 0; r < RI; ++r) {
+                        const uint32_t ua = Img::word(wa, r), ub = Img::word(wb, r);
+                        // low half: subject A's S for row r, high half: subject B's
+                        const V sc = C::from(__builtin_amdgcn_perm(ub, ua, (r & 1) ? 0x07060302u : 0x05040100u));
+                        T[r] = (r == 0 ? C::from(up_prev) : H[r - 1]) + sc;
+                    }
+                    up_prev = up0;
+#pragma unroll
+                    for (int r = 0; r < RI; ++r) {
+                        const V h = C::max3(E[r], f, T[r]);
+                        const V mm = h - gog;
+                        E[r] = C::max2(E[r], mm);
+                        f = C::max3(f, mm, step(r + 1 + b));
+                        V& ac = acc[r + b];
+                        if (b & 1) {
+                            if (r + 1 < RI) ac = C::max3(ac, h, H[r + 1]);  // H[r + 1]: cell (r + 1, step - 1)
+                            else ac = C::max2(ac, h);
+                        } else if (r == 0) {  // the even steps' other rows are partners above
+                            ac = C::max2(ac, h);
+                        }
+                        H[r] = h;
+                    }
+                    hl = C::bits(H[RI - 1]);
+                    fl = C::bits(f);
+                    if (!last) {
+                        // lane 63 finished column k - 63: collect it for the next pass
+                        const int oc = k0 + m - (kLanes - 1);
+                        if (oc >= 0 && oc < L) {
+                            const int slot = oc & (kLanes - 1);
+                            const uint32_t vh = __builtin_amdgcn_readlane(hl, kLanes - 1);
+                            const uint32_t vf = __builtin_amdgcn_readlane(fl, kLanes - 1);
+                            out_h = lane == slot ? vh : out_h;
+                            out_f = lane == slot ? vf : out_f;
+                            if (slot == kLanes - 1 || oc == L - 1) {
+                                const int col = (oc & ~(kLanes - 1)) + lane;
+                                if (col <= oc) {
+                                    bnd_h[col] = out_h;
+                                    bnd_f[col] = out_f;
+                                }
+                            }
+                        }
+                    }
+                    // pin the maxima at every step (left free, the compiler
+                    // defers the reductions and keeps every h alive)
+#pragma unroll
+                    for (int q = 0; q < NACC; ++q) asm volatile("" : "+v"(acc[q]));
+                }
+            }
+        }
+    }
+    // the lane's maximum (unbiased), then the wave's
+    V best = acc[0];
+#pragma unroll
+    for (int q = 1; q < NACC; ++q) best = C::max2(best, acc[q] - step(q));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(C::bits(best)), off));
+        best = C::max2(best, C::from(o));
+    }
+    if (lane == 0) {
+        const int ba = C::lo(best);
+        const int bb = C::hi(best);
+        if (hasA) {
+            a.scores[a.subj_id[sa]] = ba;
+            if (a.rescue_list && C::flag(a, ba)) a.rescue_list[atomicAdd(a.rescue_count, 1)] = sa;
+        }
+        if (hasB) {
+            a.scores[a.subj_id[sb]] = bb;
+            if (a.rescue_list && C::flag(a, bb)) a.rescue_list[atomicAdd(a.rescue_count, 1)] = sb;
+        }
+    }
+}
+
+}  // namespace ix2
+}  // namespace swk
