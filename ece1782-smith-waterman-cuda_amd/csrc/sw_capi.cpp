@@ -266,7 +266,7 @@ struct sw_db {
     std::vector<int32_t> h_llen;         // long subjects' lengths, longest first
     // sw_scan_lpt work tables (longest first), per scan shape
     struct LptTable {
-        int32_t qpad, qpad_intra, ri, npair, group, n;
+        int32_t qpad, qpad_intra, ri, npair, group /* quad blocks */, n;
         int32_t* d_order;
     };
     std::vector<LptTable> lpt_tables;
@@ -319,9 +319,10 @@ constexpr int64_t kSmallDbSubjects = 64 * 1000;
 // of a strong-scaled database — have too few blocks to hide the widest ones:
 // the scan time becomes the widest block's latency (width x passes / 2 for
 // a wave pair) while a long subject on the wavefront kernel takes only
-// (length + 64) steps.  The threshold then shrinks as sqrt(n / kFillSubjects),
-// measured on C2's 1/2, 1/4 and 1/8 shares (profiles/r02_strong/
-// threshold_sweep_*: best 1,536-2,048 / 1,024 / 600-704).
+// (length + 64) steps.  The threshold then shrinks as (n / kFillSubjects)^0.4,
+// measured on C2's 1/2, 1/4 and 1/8 shares with the merged longest-first
+// launch (profiles/r02_strong/: 1/8 best near 900; two concurrent launches
+// preferred 1,536-2,048 / 1,024 / 600-704).
 constexpr double kFillSubjects = 570000.0;
 
 int32_t default_long_threshold(const sw_db* db) {
@@ -329,7 +330,7 @@ int32_t default_long_threshold(const sw_db* db) {
     const double mean = static_cast<double>(db->residues) / static_cast<double>(db->n);
     if (db->n < kSmallDbSubjects && mean >= 256) return 64;
     const double fill = db->n < kSmallDbSubjects ? 1.0 : std::min(1.0, static_cast<double>(db->n) / kFillSubjects);
-    const double t = 5.7 * mean * std::sqrt(fill);
+    const double t = 5.7 * mean * std::pow(fill, 0.4);
     return static_cast<int32_t>(std::min(8192.0, std::max(fill < 1.0 ? 512.0 : 1024.0, t)));
 }
 
@@ -756,6 +757,20 @@ int32_t pair_blocks(const sw_db* db) {
 constexpr double kTickUs = 7.4;
 double intra_step_us(int ri) { return 0.157 * (ri * 28.8 + 80.0) / (6 * 28.8 + 80.0); }
 
+// The widest group blocks of the merged launch run by quads: those at least
+// kQuadFrac x the long threshold wide, whose pair latency would otherwise
+// exceed the long subjects' (SW_QUAD_WIDTH=w: at least w columns; 0: none).
+constexpr double kQuadFrac = 0.67;
+
+int32_t lpt_quad_blocks(const sw_db* db, int32_t npair) {
+    int64_t wmin = static_cast<int64_t>(kQuadFrac * db->long_threshold);
+    if (const char* e = std::getenv("SW_QUAD_WIDTH")) wmin = std::atoll(e);
+    if (wmin <= 0) return 0;
+    int32_t n = 0;
+    while (n < npair && static_cast<int64_t>(db->h_blk_groups[n]) * swk::kGroupCols >= wmin) ++n;
+    return n;
+}
+
 // Ticks of a single-wave block (x2s_block: chained passes when ncols >= 32).
 double single_ticks(int64_t ncols, int passes) {
     if (ncols <= 0) return 0;
@@ -773,28 +788,30 @@ double group_ticks_host(int64_t ncols, int passes, int G) {
 }
 
 // The work table of sw_scan_lpt for this scan shape (built once, cached).
-int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int group, const int32_t** order,
+int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad, const int32_t** order,
               int* n) {
     for (const auto& t : db->lpt_tables)
-        if (t.qpad == qpad && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == group) {
+        if (t.qpad == qpad && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad) {
             *order = t.d_order;
             *n = t.n;
             return SW_OK;
         }
     const int passes = qpad / 64;
-    const int NG = swk::kWavesPerWG / group;
     const int64_t nb = db->nblocks;
-    const int64_t pwg = (npair + NG - 1) / NG;
+    const int64_t pwg = nquad + (npair - nquad + 1) / 2;
     const int64_t swg = (nb - npair + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
     const int64_t iwg = (((db->nlong + 1) / 2) + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
     const int nch = qpad_intra / (swk::kLanes * ri);
     std::vector<std::pair<double, int32_t>> w;
     w.reserve(static_cast<size_t>(pwg + swg + iwg));
     auto width = [&](int64_t b) { return static_cast<int64_t>(db->h_blk_groups[b]) * swk::kGroupCols; };
-    for (int64_t g = 0; g < pwg; ++g) {
+    for (int64_t g = 0; g < nquad; ++g) w.emplace_back(group_ticks_host(width(g), passes, 4) * kTickUs, g);
+    for (int64_t g = nquad; g < pwg; ++g) {
         double c = 0;
-        for (int q = 0; q < NG; ++q)
-            if (g * NG + q < npair) c = std::max(c, group_ticks_host(width(g * NG + q), passes, group));
+        for (int q = 0; q < 2; ++q) {
+            const int64_t b = nquad + (g - nquad) * 2 + q;
+            if (b < npair) c = std::max(c, group_ticks_host(width(b), passes, 2));
+        }
         w.emplace_back(c * kTickUs, static_cast<int32_t>(g));
     }
     for (int64_t g = 0; g < swg; ++g)  // widest first: the workgroup's first block bounds it
@@ -808,7 +825,7 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     });
     std::vector<int32_t> ord(w.size());
     for (size_t k = 0; k < w.size(); ++k) ord[k] = w[k].second;
-    sw_db::LptTable t{qpad, qpad_intra, ri, npair, group, static_cast<int32_t>(ord.size()), nullptr};
+    sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, static_cast<int32_t>(ord.size()), nullptr};
     HIPCHECK(hipMalloc(reinterpret_cast<void**>(&t.d_order), ord.size() * sizeof(int32_t)));
     HIPCHECK(hipMemcpy(t.d_order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     db->device_bytes += ord.size() * sizeof(int32_t);
@@ -991,7 +1008,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     if (rescue && db->nblocks && !db->d_rescue) {
         // lists A and B, then the fp16 pass's largest flagged block
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rescue), (2 * (db->nblocks + 1) + 2) * sizeof(int32_t)));
-        db->device_bytes += (db->nblocks + 1) * sizeof(int32_t);
+        db->device_bytes += (2 * (db->nblocks + 1) + 2) * sizeof(int32_t);
     }
     const bool multi_inter = qpad_inter > R || qpad_rescue > swk::rescue_rows(affine) ||
                              qpad_coop > swk::inter_coop_rows() || qpad_list > (affine ? 64 : 96);
@@ -1025,7 +1042,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     const bool lpt_want = lpt_env ? lpt_env[0] == '1' : static_cast<double>(db->n) < kFillSubjects;
     const bool lpt = lpt_want && db->nlong && db->nblocks && intra_x2 && !intra_i16_first &&
                      f16 && rescue && npair && pair_merged && !ncoop && i16_span == 0 &&
-                     swk::lpt_supported(pair_group(db), ri2);
+                     swk::lpt_supported(ri2);
     db->last_lpt = lpt;
     // fork: the side stream starts when the main stream reaches ev[0]
     HIPCHECK(hipEventRecord(h->ev[0], h->stream));
@@ -1134,8 +1151,11 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         a.scores = scores_dev;
         if (std::getenv("SW_TRACE_FILE")) {
             if (!db->h_trace)
-                HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&db->h_trace), 32 * db->nblocks,
+            {
+                HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&db->h_trace), 32 * (db->nblocks + db->nlong + 8),
                                        hipHostMallocMapped));
+                std::memset(db->h_trace, 0, 32 * (db->nblocks + db->nlong + 8));
+            }
             HIPCHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.trace), db->h_trace, 0));
         }
         int32_t* listA = db->d_rescue;                    // [count, ids...]
@@ -1209,8 +1229,10 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             a.blk_first = npair;
             const int32_t* order = nullptr;
             int nwg = 0;
-            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, pair_group(db), &order, &nwg))) return rc;
-            HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, order, nwg, affine, pair_group(db), ri2, h->stream));
+            const int32_t nquad = lpt_quad_blocks(db, npair);
+            a.blk_quad = nquad;
+            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, &order, &nwg))) return rc;
+            HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, order, nwg, affine, ri2, h->stream));
             HIPCHECK(hipEventRecord(h->ev[7], h->stream));
             if ((rc = launch_long(true))) return rc;
             HIPCHECK(hipEventRecord(h->ev[1], h->stream));
@@ -1228,9 +1250,11 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         if (lpt) h->last_kernel += "+lpt";
         if (!lpt) HIPCHECK(hipEventRecord(h->ev[7], h->stream));
         ++h->launches;
+        if (ncoop || (npair && !pair_merged) || nr) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
         if (f16 && rescue && !db->icount_pending) {
             // the fp16 pass's flagged count and largest flagged block, read
-            // by a later scan (no synchronisation here)
+            // by a later scan (no synchronisation here), after every fp16
+            // launch that appends to list A has joined the main stream
             if (!db->h_icount) {
                 HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&db->h_icount), 2 * sizeof(int32_t),
                                        hipHostMallocDefault));
@@ -1244,7 +1268,6 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             db->icount_qlen = qlen;
             db->icount_nr = nr;
         }
-        if (ncoop || (npair && !pair_merged) || nr) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
         if (f16) {
             // fp16 chain, stage 2: the int16 packed kernel re-scores the
             // blocks the fp16 kernel flagged (scores near 2048) and flags
@@ -1645,7 +1668,7 @@ int sw_db_free(sw_db* db) {
     if (db->h_trace) {  // the last scan's block timeline (tail analysis builds)
         if (const char* path = std::getenv("SW_TRACE_FILE"))
             if (FILE* f = std::fopen(path, "wb")) {
-                std::fwrite(db->h_trace, 32, static_cast<size_t>(db->nblocks), f);
+                std::fwrite(db->h_trace, 32, static_cast<size_t>(db->nblocks + db->nlong + 8), f);
                 std::fclose(f);
             }
         (void)hipHostFree(db->h_trace);

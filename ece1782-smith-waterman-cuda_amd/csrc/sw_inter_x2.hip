@@ -801,8 +801,7 @@ __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>&
 // scan (sw_capi.cpp pair_blocks / pair_group).
 constexpr int kPairLag = 3;
 
-template <int G>
-__device__ __forceinline__ int group_ticks(uint32_t ncols, int passes, int SG) {
+__device__ __forceinline__ int group_ticks(uint32_t ncols, int passes, int SG, int G) {
     if (ncols == 0 || passes <= 0) return 0;
     const int S = static_cast<int>(ncols) / SG + 1;
     const int per = max(S, G * kPairLag);
@@ -811,28 +810,26 @@ __device__ __forceinline__ int group_ticks(uint32_t ncols, int passes, int SG) {
     return t;
 }
 
-// MERGED: one launch for the whole scan — workgroups [0, nwg_groups) run the
-// P = a.blk_first widest blocks by G-wave groups (4 / G blocks per
-// workgroup), the rest run blocks [P, nblocks) one per wave (x2s_block), so
-// the dispatcher hands out work widest-first across both forms (the LDS of
-// the group form, 53 KB for pairs and 61 KB for quads, still leaves 2
-// workgroups per CU, the register-bound occupancy of both).
 // The LDS of one workgroup of the group form: the waves' profile images, the
-// rings between consecutive waves of a group, the partial maxima.
-template <int R, int SG, int G>
+// rings between consecutive waves of a group (3 for a quad, 2 for two
+// pairs), the partial maxima.  53 KB for pairs, 61 KB for quads: both still
+// leave 2 workgroups per CU, the register-bound occupancy.
+template <int R, int SG, int GMAX>
 struct X2pSmem {
-    static constexpr int NG = kWavesPerWG / G;
     X2Lds<R> lds[kWavesPerWG];
-    int4 ring[NG * (G - 1)][kRingSlots * (SG / 4) * kLanes];
+    int4 ring[kWavesPerWG - kWavesPerWG / GMAX][kRingSlots * (SG / 4) * kLanes];
     uint32_t part[kWavesPerWG][kLanes];
 };
 
-// One workgroup's work (wgi = its index in the launch's numbering).
-template <int R, int SG, bool AFFINE, bool F16, bool MERGED, int G>
-__device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, X2pSmem<R, SG, G>& sm) {
+// One workgroup's work (wgi = its index in the launch's numbering):
+// workgroups [0, Q) run the Q blocks [blk_base, quad_end) by quads (GMAX = 4
+// only), the next ones blocks [quad_end, npair) by pairs (two per
+// workgroup), and with MERGED the rest blocks [npair, nblocks) one per wave
+// (x2s_block): the dispatcher hands out work widest-first across the forms.
+template <int R, int SG, bool AFFINE, bool F16, bool MERGED, int GMAX>
+__device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, int quad_end, X2pSmem<R, SG, GMAX>& sm) {
     static_assert(R % 16 == 0 && SG % 4 == 0, "shape");
-    static_assert(G == 2 || G == 4, "groups of 2 or 4 waves");
-    constexpr int NG = kWavesPerWG / G;  // groups (blocks) per workgroup
+    static_assert(GMAX == 2 || GMAX == 4, "groups of 2 or 4 waves");
     X2Lds<R>* lds = sm.lds;
     auto& ring = sm.ring;
     auto& part = sm.part;
@@ -841,21 +838,26 @@ __device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, X2pSmem<R, S
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int npair = MERGED ? a.blk_first : a.nblocks;  // blocks [blk_base, npair) by groups
-    const int pwg = (npair - a.blk_base + NG - 1) / NG;    // their workgroups
+    const int qend = GMAX == 4 ? quad_end : a.blk_base;   // blocks [blk_base, qend) by quads
+    const int qwg = qend - a.blk_base;                     // quad workgroups
+    const int pwg = qwg + (npair - qend + 1) / 2;          // ... and pair workgroups
     if (MERGED && wgi >= pwg) {
         const int blk = npair + (wgi - pwg) * kWavesPerWG + wave;
         if (blk < a.nblocks) x2s_block<R, SG, AFFINE, F16>(a, blk, lds[wave], lane);
         return;  // workgroup-uniform branch: no barrier below is skipped by part of it
     }
+    const bool quad = wgi < qwg;                           // workgroup-uniform
+    const int G = quad ? 4 : 2, NG = kWavesPerWG / G;
+    const int first = quad ? a.blk_base + wgi : qend + (wgi - qwg) * 2;
     const int gi = wave / G, w = wave % G;
     const int passes = (a.qpad + 2 * R - 1) / (2 * R);
     // the workgroup's clock runs to the longest of its blocks
     int tmax = 0;
     for (int q = 0; q < NG; ++q) {
-        const int b = a.blk_base + wgi * NG + q;
-        if (b < npair) tmax = max(tmax, group_ticks<G>(a.blk_groups[b] * kGroupCols, passes, SG));
+        const int b = first + q;
+        if (b < npair) tmax = max(tmax, group_ticks(a.blk_groups[b] * kGroupCols, passes, SG, G));
     }
-    const int blk = a.blk_base + wgi * NG + gi;
+    const int blk = first + gi;
     Best<F16> best;
     best.init();
     int tick = 0;
@@ -883,21 +885,21 @@ __device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, X2pSmem<R, S
     __syncthreads();
     if (blk < npair && w == 0) {
         V b = best.value(a);
-#pragma unroll
         for (int u = 1; u < G; ++u) {
             const V o = P::from(part[wave + u][lane]);
             if constexpr (F16) b = __builtin_elementwise_maximum(b, o);
             else b = max2(b, o);
         }
         x2s_finish<F16>(a, blk, lane, b);
-        trace_block(a, blk, t0, lane, 1);
+        trace_block(a, blk, t0, lane, quad ? 4 : 1);
     }
 }
 
+// G = 2: every group block by pairs; G = 4: every group block by quads.
 template <int R, int SG, bool AFFINE, bool F16, bool MERGED, int G>
 __global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
     __shared__ __attribute__((aligned(16))) X2pSmem<R, SG, G> sm;
-    x2p_wg<R, SG, AFFINE, F16, MERGED, G>(a, blockIdx.x, sm);
+    x2p_wg<R, SG, AFFINE, F16, MERGED, G>(a, blockIdx.x, MERGED ? a.blk_first : a.nblocks, sm);
 }
 
 // ---------------------------------------------------------------------------
@@ -916,43 +918,39 @@ __global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
 // so the dispatcher starts the longest work first and fills the end with
 // the shortest (LPT).  LDS: the two kinds' buffers overlap (a workgroup is
 // one kind), so the occupancy stays the inter kernel's 2 workgroups per CU.
-template <int R, int SG, bool AFFINE, int G, int RI>
+template <int R, int SG, bool AFFINE, int RI>
 __global__ __launch_bounds__(256, 2) void sw_scan_lpt(InterArgs a, IntraArgs ia, const int32_t* __restrict__ order) {
     using Elem = typename ix2::IntraImg<RI, true>::Elem;
-    constexpr size_t kInter = sizeof(X2pSmem<R, SG, G>);
+    constexpr size_t kInter = sizeof(X2pSmem<R, SG, 4>);
     constexpr size_t kIntra = sizeof(Elem) * ix2::img_elems<RI, true>();
     __shared__ __attribute__((aligned(16))) char smem[kInter > kIntra ? kInter : kIntra];
     const int item = order[blockIdx.x];
+    const uint64_t t0 = trace_now();
     if (item >= 0)
-        x2p_wg<R, SG, AFFINE, true, true, G>(a, item, *reinterpret_cast<X2pSmem<R, SG, G>*>(smem));
+        x2p_wg<R, SG, AFFINE, true, true, 4>(a, item, a.blk_quad, *reinterpret_cast<X2pSmem<R, SG, 4>*>(smem));
     else
         ix2::intra_x2_wg<RI, true, false>(ia, -1 - item, reinterpret_cast<Elem*>(smem));
+    // per-workgroup timeline (trace builds): after the per-block entries
+    if (threadIdx.x == 0) trace_block(a, a.nblocks + blockIdx.x, t0, 0, item >= 0 ? 2 : 3);
 }
 
-template <int G, int RI>
+template <int RI>
 static void launch_lpt_t(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine,
                          hipStream_t s) {
-    if (affine) hipLaunchKernelGGL((sw_scan_lpt<32, 8, true, G, RI>), dim3(n), dim3(kWavesPerWG * kLanes), 0, s, a, ia,
+    if (affine) hipLaunchKernelGGL((sw_scan_lpt<32, 8, true, RI>), dim3(n), dim3(kWavesPerWG * kLanes), 0, s, a, ia,
                                    order);
-    else hipLaunchKernelGGL((sw_scan_lpt<32, 8, false, G, RI>), dim3(n), dim3(kWavesPerWG * kLanes), 0, s, a, ia,
-                            order);
+    else hipLaunchKernelGGL((sw_scan_lpt<32, 8, false, RI>), dim3(n), dim3(kWavesPerWG * kLanes), 0, s, a, ia, order);
 }
 
-bool lpt_supported(int group, int ri) { return (group == 2 || group == 4) && (ri == 4 || ri == 6 || ri == 8); }
+bool lpt_supported(int ri) { return ri == 4 || ri == 6 || ri == 8; }
 
-int lpt_inter_wgs(const InterArgs& a, int group) {
-    const int NG = kWavesPerWG / group;
-    return (a.blk_first - a.blk_base + NG - 1) / NG + (a.nblocks - a.blk_first + kWavesPerWG - 1) / kWavesPerWG;
-}
-
-hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine,
-                           int group, int ri, hipStream_t s) {
+hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri,
+                           hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    if (!lpt_supported(group, ri)) return hipErrorInvalidValue;
-#define SW_LPT(G_, RI_) \
-    if (group == G_ && ri == RI_) launch_lpt_t<G_, RI_>(a, ia, order, n, affine, s);
-    SW_LPT(2, 4) SW_LPT(2, 6) SW_LPT(2, 8) SW_LPT(4, 4) SW_LPT(4, 6) SW_LPT(4, 8)
-#undef SW_LPT
+    if (ri == 4) launch_lpt_t<4>(a, ia, order, n, affine, s);
+    else if (ri == 6) launch_lpt_t<6>(a, ia, order, n, affine, s);
+    else if (ri == 8) launch_lpt_t<8>(a, ia, order, n, affine, s);
+    else return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -81,6 +81,8 @@ struct InterArgs {
     // sw_inter_x2p: its pair blocks are [blk_base, blk_first) (merged) or
     // [blk_base, nblocks); blocks below blk_base run elsewhere
     int32_t blk_base;
+    // sw_scan_lpt: blocks [blk_base, blk_quad) run by wave quads
+    int32_t blk_quad;
     // fp16 kernels: the largest flagged block id (atomicMax; nullable), read
     // back by the host to route the widest blocks to int16 next time
     int32_t* rescue_max;
@@ -160,14 +162,14 @@ hipError_t launch_inter_x2s_list(const InterArgs& a, bool affine, hipStream_t s)
 // otherwise blocks [blk_base, nblocks) by groups only.
 hipError_t launch_inter_x2p(const InterArgs& a, bool affine, bool f16, bool merged, int group, hipStream_t s);
 // One launch for the whole fp16 scan, longest work first (sw_scan_lpt):
-// order[0..n) names each workgroup's work, >= 0 an inter workgroup of the
-// merged group launch (lpt_inter_wgs of them; a as for launch_inter_x2p
-// merged), < 0 intra workgroup -1 - order[k] (ia as for launch_intra_x2: 4
-// subject pairs per workgroup).  Group 2 or 4, intra rows per lane 4, 6, 8.
-bool lpt_supported(int group, int ri);
-int lpt_inter_wgs(const InterArgs& a, int group);
-hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine,
-                           int group, int ri, hipStream_t s);
+// order[0..n) names each workgroup's work, >= 0 an inter workgroup (a as for
+// launch_inter_x2p merged, with blocks [blk_base, blk_quad) by quads, then
+// [blk_quad, blk_first) by pairs), < 0 intra workgroup -1 - order[k] (ia as
+// for launch_intra_x2: 4 subject pairs per workgroup).  Intra rows per lane
+// 4, 6 or 8.
+bool lpt_supported(int ri);
+hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri,
+                           hipStream_t s);
 // true if the chosen inter kernel has a wave-pair form (two-strips 32x8).
 bool inter_has_pair(bool affine, int x2_ok);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.

@@ -165,7 +165,7 @@ SW_API int sw_db_subjects(const sw_db* db, int64_t* lengths, int32_t* ids);
  * wave per subject) instead of the inter-sequence kernels (one subject per
  * lane).  0 = library default: 5.7 x the mean length clamped to
  * [1024, 8192]; from 64,000 to 570,000 subjects (a rank's share of a strong-
- * scaled database) scaled by sqrt(n / 570,000), floor 512; 64 for databases
+ * scaled database) scaled by (n / 570,000)^0.4, floor 512; 64 for databases
  * under 64,000 subjects with a mean length >= 256 (too few 64-subject blocks
  * to fill the GPU).  May be changed between scans (re-packs the database). */
 SW_API int sw_db_set_long_threshold(sw_db* db, int32_t threshold);

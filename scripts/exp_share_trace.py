@@ -30,6 +30,8 @@ st = db.stats()
 tm = h.timing()
 db.close()
 t = np.fromfile(path, dtype=np.uint64).reshape(-1, 4)
+tall = t
+t = t[:st["n_blocks"]]
 t0, t1 = t[:, 0].astype(np.int64), t[:, 1].astype(np.int64)
 ok = t1 > 0
 T0 = t0[ok].min()
@@ -58,3 +60,26 @@ crit = np.argsort(-e)[:6]
 out["last_to_end"] = [[int(blk[i]), int(kind[i]), int(width[i]), round(float(s[i]), 1), round(float(e[i]), 1)]
                       for i in crit]
 print(json.dumps(out))
+
+# merged launch (sw_scan_lpt): per-workgroup records after the per-block ones
+nb = st["n_blocks"]
+w = tall[nb:]
+okw = w[:, 1] > 0
+if okw.any():
+    ws = (w[okw, 0].astype(np.int64) - T0) / 100.0
+    we = (w[okw, 1].astype(np.int64) - T0) / 100.0
+    wk = w[okw, 3] >> 32
+    lpt = {"workgroups": int(okw.sum())}
+    for kd, name in ((2, "inter"), (3, "intra")):
+        sel = wk == kd
+        if sel.any():
+            d = we[sel] - ws[sel]
+            lpt[name] = {"n": int(sel.sum()), "start_us_max": round(float(ws[sel].max()), 1),
+                         "end_us_max": round(float(we[sel].max()), 1),
+                         "dur_us_min_med_max": [round(float(d.min()), 1), round(float(np.median(d)), 1),
+                                                round(float(d.max()), 1)]}
+    grid = np.linspace(0, float(we.max()), 21)
+    lpt["wgs_inflight_every_5pct"] = [int(((ws <= x) & (we > x)).sum()) for x in grid]
+    last = np.argsort(-we)[:6]
+    lpt["last_to_end"] = [[int(wk[i]), round(float(ws[i]), 1), round(float(we[i]), 1)] for i in last]
+    print(json.dumps({"lpt": lpt}))

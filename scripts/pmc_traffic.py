@@ -11,8 +11,12 @@ usage: pmc_traffic.py FETCH_DIR WRITE_DIR WORKLOAD_KEY OUT_JSON ROCPROF_NAME_SUB
 (LABEL = the library's kernel name, sw_last_kernel(), which bench.py matches)
 """
 import csv
+import datetime
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def per_dispatch(d, counter, kernel):
@@ -37,7 +41,10 @@ def main():
            "hbm_bytes_per_launch": round(fetch + write),
            "dispatches": {"fetch_pass": len(f), "write_pass": len(w)},
            "raw_kib_mean": {"FETCH_SIZE": sum(f) / len(f), "WRITE_SIZE": sum(w) / len(w)},
-           "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane streaming reads); WRITE_SIZE as reported"}
+           "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane streaming reads); WRITE_SIZE as reported",
+           # bench.py reports the bytes only for a build with these kernel sources
+           "kernel_src_sha16": __import__("bench").kernel_source_hash(),
+           "measured": datetime.date.today().isoformat()}
     with open(out, "w") as fo:
         json.dump(res, fo, indent=1)
     print(json.dumps(res))

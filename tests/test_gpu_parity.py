@@ -561,3 +561,35 @@ def test_random_scoring_and_shapes(sw, oracle, handle, case):
         got = db.scan(q, m, go, ge)
         assert np.array_equal(got, want), (case, go, ge, len(q), handle.last_kernel(),
                                            handle.last_intra_kernel(), np.nonzero(got != want)[0][:10])
+
+
+@pytest.mark.parametrize("quad_width", ["0", "200", "16"])
+@pytest.mark.parametrize("scoring", [(1, 12, 1), (0, 2, 2)])
+def test_merged_lpt_launch(sw, oracle, handle, monkeypatch, quad_width, scoring):
+    """sw_scan_lpt (the inter blocks by quads / pairs / single waves and the
+    long subjects' fp16 pass in one launch, longest work first): queries for
+    the three intra shapes it supports (4, 6, 8 rows per lane), quads for none,
+    the widest or every group block, planted near-copies in both kernels'
+    halves (rescue chains after the merged launch), against the oracle and
+    the two-launch form."""
+    mid, go, ge = scoring
+    monkeypatch.setenv("SW_LPT", "1")
+    monkeypatch.setenv("SW_QUAD_WIDTH", quad_width)
+    monkeypatch.setenv("SW_PAIR_WIDTH", "64")
+    r, o = sw.synth.database(2500, shard=23)
+    q0 = sw.synth.query(500, shard=8)
+    extra = [q0, q0[:300], np.concatenate([q0, q0])]  # a long near-copy goes to the intra half
+    r2 = np.concatenate([r] + extra)
+    o2 = np.concatenate([o, o[-1] + np.cumsum([len(x) for x in extra])])
+    db = sw.Database(handle, r2, o2, long_threshold=700)
+    m = sw.capi.builtin_matrix(mid)
+    for qlen in (200, 375, 500):
+        q = q0[:qlen]
+        got = db.scan(q, m, go, ge)
+        assert handle.last_kernel().endswith("+lpt"), handle.last_kernel()
+        want = oracle.scan(q, r2, o2, mat=m, gap_open=go, gap_extend=ge)
+        assert np.array_equal(got, want), (qlen, np.nonzero(got != want)[0][:10])
+        monkeypatch.setenv("SW_LPT", "0")
+        assert np.array_equal(db.scan(q, m, go, ge), got)
+        assert not handle.last_kernel().endswith("+lpt")
+        monkeypatch.setenv("SW_LPT", "1")
