@@ -1032,14 +1032,14 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     }
     // One merged launch for the fp16 scan, longest work first (sw_scan_lpt):
     // the inter groups + single waves and the long subjects' fp16 pass, when
-    // the scan takes exactly that shape, on databases that do not fill the
-    // GPU many times over (n < kFillSubjects: a rank's share of a strong-
-    // scaled database).  Measured (profiles/r02_strong/lpt/): C2's 1/8 share
-    // 1.92 -> 1.45 ms, 1/4 2.57 -> 2.29, 1/2 equal; the whole C2 database
-    // 7.55 -> 7.70 ms, so it keeps two concurrent launches.  SW_LPT=0 / 1
-    // forces either form.
+    // the scan takes exactly that shape, on databases far from filling the
+    // GPU (n < 0.35 kFillSubjects: a rank's share of a strong-scaled
+    // database at N >= 4).  Measured (profiles/r02_strong/lpt/, r02_round/):
+    // C2's 1/8 share 1.92 -> 1.45 ms, 1/4 2.57 -> 2.29, 1/2 4.15 -> 4.29;
+    // the whole C2 database 7.55 -> 7.70 ms, so those keep two concurrent
+    // launches.  SW_LPT=0 / 1 forces either form.
     const char* lpt_env = std::getenv("SW_LPT");
-    const bool lpt_want = lpt_env ? lpt_env[0] == '1' : static_cast<double>(db->n) < kFillSubjects;
+    const bool lpt_want = lpt_env ? lpt_env[0] == '1' : static_cast<double>(db->n) < 0.35 * kFillSubjects;
     const bool lpt = lpt_want && db->nlong && db->nblocks && intra_x2 && !intra_i16_first &&
                      f16 && rescue && npair && pair_merged && !ncoop && i16_span == 0 &&
                      swk::lpt_supported(ri2);
