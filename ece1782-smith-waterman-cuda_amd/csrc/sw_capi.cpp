@@ -266,7 +266,7 @@ struct sw_db {
     std::vector<int32_t> h_llen;         // long subjects' lengths, longest first
     // sw_scan_lpt work tables (longest first), per scan shape
     struct LptTable {
-        int32_t qpad, qpad_intra, ri, npair, group /* quad blocks */, n;
+        int32_t qpad, qpad_intra, ri, npair, group /* quad blocks */, npipe, qpad_pipe, n;
         int32_t* d_order;
     };
     std::vector<LptTable> lpt_tables;
@@ -788,10 +788,32 @@ double group_ticks_host(int64_t ncols, int passes, int G) {
 }
 
 // The work table of sw_scan_lpt for this scan shape (built once, cached).
-int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad, const int32_t** order,
-              int* n) {
+// The longest subject pairs can run pipelined over a whole workgroup (ix2
+// PIPE): pairs whose longer subject has at least kPipeFrac x the long
+// threshold residues, when the query spans 2..4 chunks of 64 x
+// lpt_pipe_rows() rows (SW_PIPE_LEN=n: at least n residues; 0: none).
+// Measured slower on C2's 1/8 share (profiles/r02_strong/pipe/: 1.37 ms
+// without, 1.56 with pairs >= 2 x the threshold, 1.57 with only pairs >=
+// 4,000 residues), so it is off unless SW_PIPE_LEN asks for it.
+constexpr double kPipeFrac = 0.0;
+
+int32_t lpt_pipe_pairs(const sw_db* db, int32_t qlen) {
+    const int64_t ch = static_cast<int64_t>(swk::kLanes) * swk::lpt_pipe_rows();
+    const int64_t nch = (qlen + ch - 1) / ch;
+    if (nch < 2 || nch > swk::kWavesPerWG) return 0;
+    int64_t lmin = static_cast<int64_t>(kPipeFrac * db->long_threshold);
+    if (const char* e = std::getenv("SW_PIPE_LEN")) lmin = std::atoll(e);
+    if (lmin <= 0) return 0;
+    int64_t k = 0;  // subjects (longest first) at least lmin long, in whole pairs
+    while (k < db->nlong && db->h_llen[static_cast<size_t>(k)] >= lmin) ++k;
+    return static_cast<int32_t>((k + 1) / 2);
+}
+
+int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad, int32_t npipe,
+              int32_t qpad_pipe, const int32_t** order, int* n) {
     for (const auto& t : db->lpt_tables)
-        if (t.qpad == qpad && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad) {
+        if (t.qpad == qpad && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad &&
+            t.npipe == npipe && t.qpad_pipe == qpad_pipe) {
             *order = t.d_order;
             *n = t.n;
             return SW_OK;
@@ -800,7 +822,10 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     const int64_t nb = db->nblocks;
     const int64_t pwg = nquad + (npair - nquad + 1) / 2;
     const int64_t swg = (nb - npair + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
-    const int64_t iwg = (((db->nlong + 1) / 2) + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
+    const int64_t npairs = (db->nlong + 1) / 2;
+    const int64_t iwg = (npairs - npipe + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
+    const int rp = swk::lpt_pipe_rows();
+    const int pch = qpad_pipe / (swk::kLanes * rp);
     const int nch = qpad_intra / (swk::kLanes * ri);
     std::vector<std::pair<double, int32_t>> w;
     w.reserve(static_cast<size_t>(pwg + swg + iwg));
@@ -818,14 +843,18 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
         w.emplace_back(single_ticks(width(npair + g * swk::kWavesPerWG), passes) * kTickUs,
                        static_cast<int32_t>(pwg + g));
     for (int64_t g = 0; g < iwg; ++g)
-        w.emplace_back((db->h_llen[static_cast<size_t>(8 * g)] + swk::kLanes - 1) * nch * intra_step_us(ri),
+        w.emplace_back((db->h_llen[static_cast<size_t>(2 * npipe + 8 * g)] + swk::kLanes - 1) * nch * intra_step_us(ri),
                        static_cast<int32_t>(-1 - g));
+    for (int64_t q = 0; q < npipe; ++q)
+        w.emplace_back((db->h_llen[static_cast<size_t>(2 * q)] + swk::kLanes - 1 + 128.0 * (pch - 1)) *
+                           intra_step_us(rp),
+                       static_cast<int32_t>(-swk::lpt_pipe_item() - q));
     std::stable_sort(w.begin(), w.end(), [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) {
         return x.first > y.first;
     });
     std::vector<int32_t> ord(w.size());
     for (size_t k = 0; k < w.size(); ++k) ord[k] = w[k].second;
-    sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, static_cast<int32_t>(ord.size()), nullptr};
+    sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, npipe, qpad_pipe, static_cast<int32_t>(ord.size()), nullptr};
     HIPCHECK(hipMalloc(reinterpret_cast<void**>(&t.d_order), ord.size() * sizeof(int32_t)));
     HIPCHECK(hipMemcpy(t.d_order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     db->device_bytes += ord.size() * sizeof(int32_t);
@@ -967,6 +996,9 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     }
     i16_span = static_cast<int32_t>(std::min<int64_t>(std::max(i16_span, 0), db->nblocks));
     const int32_t qpad_intra2 = ri2 ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri2)) : 0;
+    // the merged launch's pipelined pairs (see lpt_pipe_pairs)
+    const int32_t qpad_pipe =
+        intra_x2 ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * swk::lpt_pipe_rows())) : 0;
     // Empty query: every score is 0 (the reference's kernel leaves maxScore 0).
     if (qlen == 0) {
         db->last_ncoop = 0;
@@ -1002,7 +1034,8 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     db->last_npair = npair;
     db->last_pair_merged = npair && pair_merged;
     const int32_t qpad_coop = ncoop ? static_cast<int32_t>(round_up(qlen, swk::inter_coop_rows())) : 0;
-    if ((rc = build_profiles(h, query, qlen, mat, go, affine, std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2}),
+    if ((rc = build_profiles(h, query, qlen, mat, go, affine,
+                             std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2, qpad_pipe}),
                              x2 || intra_x2, ri, qpad_intra, &P)))
         return rc;
     if (rescue && db->nblocks && !db->d_rescue) {
@@ -1230,9 +1263,15 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             const int32_t* order = nullptr;
             int nwg = 0;
             const int32_t nquad = lpt_quad_blocks(db, npair);
+            const int32_t npipe = lpt_pipe_pairs(db, qlen);
             a.blk_quad = nquad;
-            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, &order, &nwg))) return rc;
-            HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, order, nwg, affine, ri2, h->stream));
+            swk::IntraArgs ip = lpt_intra;  // the pipelined longest pairs
+            ip.qpad = qpad_pipe;
+            ip.pair_base = 0;
+            lpt_intra.pair_base = npipe;
+            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, npipe, qpad_pipe, &order, &nwg)))
+                return rc;
+            HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, ip, order, nwg, affine, ri2, h->stream));
             HIPCHECK(hipEventRecord(h->ev[7], h->stream));
             if ((rc = launch_long(true))) return rc;
             HIPCHECK(hipEventRecord(h->ev[1], h->stream));
