@@ -940,9 +940,9 @@ __global__ __launch_bounds__(256, 2) void sw_scan_lpt(InterArgs a, IntraArgs ia,
     if (item >= 0)
         x2p_wg<R, SG, AFFINE, true, true, 4>(a, item, a.blk_quad, *reinterpret_cast<X2pSmem<R, SG, 4>*>(smem));
     else if (item > -kLptPipe)
-        ix2::intra_x2_wg<RI, true, false>(ia, -1 - item, reinterpret_cast<Elem*>(smem));
+        ix2::intra_x2_wg<RI, true, false, false, !AFFINE>(ia, -1 - item, reinterpret_cast<Elem*>(smem));
     else
-        ix2::intra_x2_wg<kLptPipeRI, true, false, true>(ip, -kLptPipe - item, reinterpret_cast<PElem*>(smem),
+        ix2::intra_x2_wg<kLptPipeRI, true, false, true, !AFFINE>(ip, -kLptPipe - item, reinterpret_cast<PElem*>(smem),
                                                         reinterpret_cast<uint32_t*>(smem + kPipeImg));
     // per-workgroup timeline (trace builds): after the per-block entries
     if (threadIdx.x == 0) trace_block(a, a.nblocks + blockIdx.x, t0, 0, item >= 0 ? 2 : 3);

@@ -162,7 +162,12 @@ constexpr int kPipeLdsWords = 2 * kWavesPerWG * kPipeRing + kWavesPerWG * kLanes
 // One workgroup's work (wgi = its index in the launch: subject pairs
 // pair_base + 4 wgi .. + 3, one per wave; PIPE: pair pair_base + wgi);
 // img: the workgroup's LDS image (PIPE: one per wave).
-template <int RI, bool F16, bool LIST, bool PIPE = false>
+// LIN (linear gaps, open == extend = g): the biased cell needs no E or F —
+// the left and up terms H - g ARE the stored neighbours (the bias grows by g
+// per row and per step), so h~ = max(max3(H~_left, H~_up, H~_diag + S + 2g),
+// floor): 2 packed ops per cell pair after the diagonal sum instead of the
+// Farrar form's 6 (the two-strips kernel's linear cell, sw_inter_x2.hip).
+template <int RI, bool F16, bool LIST, bool PIPE = false, bool LIN = false>
 __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typename IntraImg<RI, F16>::Elem* img,
                                             uint32_t* pipe_lds = nullptr) {
     static_assert(RI % 2 == 0 && RI <= 16, "rows per lane");
@@ -241,11 +246,11 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
         if (!hasA && !hasB) continue;  // wave-uniform (PIPE: workgroup-uniform); the barriers above are shared
 
         // state of step -1 (column -1 - lane: H = 0), before step 0's rebase
-        V H[RI], E[RI];
+        V H[RI], E[LIN ? 1 : RI];
 #pragma unroll
         for (int r = 0; r < RI; ++r) {
             H[r] = step(r + NB - 1);
-            E[r] = C::from(0u);
+            if constexpr (!LIN) E[r] = C::from(0u);
         }
         // bottom row (H, F) of this lane one step back, and H of the row above
         // at the previous column (row 0's diagonal): zeros of step -1
@@ -318,7 +323,7 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
                 for (int b = 0; b < NB; ++b) {
                     const int m = m0 + b;
                     const uint32_t sbh = __builtin_amdgcn_readlane(in_bh, m);
-                    const uint32_t sbf = __builtin_amdgcn_readlane(in_bf, m);
+                    const uint32_t sbf = LIN ? 0u : __builtin_amdgcn_readlane(in_bf, m);
                     Elem wa[NQ], wb[NQ];
                     if constexpr (kPrefetch) {
                         rc = rc_n;
@@ -341,13 +346,13 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
                     // hand-off: the row above's bottom (H, F) from one step back
                     const V adj = step(RI - 1 + (b == 0 ? NB : 0));
                     const uint32_t up0 = C::bits(C::from(shr1u(sbh, hl)) - adj);
-                    V f = C::from(shr1u(sbf, fl)) - adj;
+                    V f = LIN ? C::from(0u) : C::from(shr1u(sbf, fl)) - adj;
                     if (b == 0) {  // rebase: the bias period restarts
                         const V reb = step(NB);
 #pragma unroll
                         for (int r = 0; r < RI; ++r) {
                             H[r] = H[r] - reb;
-                            E[r] = E[r] - reb;
+                            if constexpr (!LIN) E[r] = E[r] - reb;
                         }
                         up_prev = C::bits(C::from(up_prev) - reb);
                     }
@@ -361,13 +366,21 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
                         const V sc = C::from(__builtin_amdgcn_perm(ub, ua, (r & 1) ? 0x07060302u : 0x05040100u));
                         T[r] = (r == 0 ? C::from(up_prev) : H[r - 1]) + sc;
                     }
+                    // LIN: row 0's up term is the row above's bottom H (up0)
+                    V up = C::from(up0);
                     up_prev = up0;
 #pragma unroll
                     for (int r = 0; r < RI; ++r) {
-                        const V h = C::max3(E[r], f, T[r]);
-                        const V mm = h - gog;
-                        E[r] = C::max2(E[r], mm);
-                        f = C::max3(f, mm, step(r + 1 + b));
+                        V h;
+                        if constexpr (LIN) {
+                            h = C::max2(C::max3(H[r], up, T[r]), step(r + b));
+                            up = h;
+                        } else {
+                            h = C::max3(E[r], f, T[r]);
+                            const V mm = h - gog;
+                            E[r] = C::max2(E[r], mm);
+                            f = C::max3(f, mm, step(r + 1 + b));
+                        }
                         V& ac = acc[r + b];
                         if (b & 1) {
                             if (r + 1 < RI) ac = C::max3(ac, h, H[r + 1]);  // H[r + 1]: cell (r + 1, step - 1)
@@ -378,25 +391,25 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
                         H[r] = h;
                     }
                     hl = C::bits(H[RI - 1]);
-                    fl = C::bits(f);
+                    if constexpr (!LIN) fl = C::bits(f);
                     if (!last) {
                         // lane 63 finished column k - 63: collect it for the next pass
                         const int oc = k0 + m - (kLanes - 1);
                         if (oc >= 0 && oc < L) {
                             const int slot = oc & (kLanes - 1);
                             const uint32_t vh = __builtin_amdgcn_readlane(hl, kLanes - 1);
-                            const uint32_t vf = __builtin_amdgcn_readlane(fl, kLanes - 1);
+                            const uint32_t vf = LIN ? 0u : __builtin_amdgcn_readlane(fl, kLanes - 1);
                             out_h = lane == slot ? vh : out_h;
-                            out_f = lane == slot ? vf : out_f;
+                            if constexpr (!LIN) out_f = lane == slot ? vf : out_f;
                             if (slot == kLanes - 1 || oc == L - 1) {
                                 const int col = (oc & ~(kLanes - 1)) + lane;
                                 if (col <= oc) {
                                     if constexpr (PIPE) {
                                         ring_out_h[col & (kPipeRing - 1)] = out_h;
-                                        ring_out_f[col & (kPipeRing - 1)] = out_f;
+                                        if constexpr (!LIN) ring_out_f[col & (kPipeRing - 1)] = out_f;
                                     } else {
                                         bnd_h[col] = out_h;
-                                        bnd_f[col] = out_f;
+                                        if constexpr (!LIN) bnd_f[col] = out_f;
                                     }
                                 }
                             }

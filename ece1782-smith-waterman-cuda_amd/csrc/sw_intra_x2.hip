@@ -7,10 +7,10 @@
 
 namespace swk {
 
-template <int RI, bool F16, bool LIST>
+template <int RI, bool F16, bool LIST, bool LIN>
 __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
     __shared__ typename ix2::IntraImg<RI, F16>::Elem img[ix2::img_elems<RI, F16>()];
-    ix2::intra_x2_wg<RI, F16, LIST>(a, blockIdx.x, img);
+    ix2::intra_x2_wg<RI, F16, LIST, false, LIN>(a, blockIdx.x, img);
 }
 
 int intra_x2_rows_for(int qlen, int longest) {
@@ -34,25 +34,37 @@ int intra_x2_rows_for(int qlen, int longest) {
     return best_ri;
 }
 
-template <bool F16, bool LIST>
+template <bool F16, bool LIST, bool LIN>
 static hipError_t launch_intra_x2_t(const IntraArgs& a, int ri, hipStream_t s) {
     const int npairs = (a.nsubj + 1) / 2;
     const dim3 grid((npairs + kWavesPerWG - 1) / kWavesPerWG), block(kWavesPerWG * kLanes);
     switch (ri) {
-        case 4: hipLaunchKernelGGL((sw_intra_x2<4, F16, LIST>), grid, block, 0, s, a); break;
-        case 6: hipLaunchKernelGGL((sw_intra_x2<6, F16, LIST>), grid, block, 0, s, a); break;
-        case 8: hipLaunchKernelGGL((sw_intra_x2<8, F16, LIST>), grid, block, 0, s, a); break;
-        case 10: hipLaunchKernelGGL((sw_intra_x2<10, F16, LIST>), grid, block, 0, s, a); break;
-        case 12: hipLaunchKernelGGL((sw_intra_x2<12, F16, LIST>), grid, block, 0, s, a); break;
-        case 16: hipLaunchKernelGGL((sw_intra_x2<16, F16, LIST>), grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((sw_intra_x2<4, F16, LIST, LIN>), grid, block, 0, s, a); break;
+        case 6: hipLaunchKernelGGL((sw_intra_x2<6, F16, LIST, LIN>), grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((sw_intra_x2<8, F16, LIST, LIN>), grid, block, 0, s, a); break;
+        case 10: hipLaunchKernelGGL((sw_intra_x2<10, F16, LIST, LIN>), grid, block, 0, s, a); break;
+        case 12: hipLaunchKernelGGL((sw_intra_x2<12, F16, LIST, LIN>), grid, block, 0, s, a); break;
+        case 16: hipLaunchKernelGGL((sw_intra_x2<16, F16, LIST, LIN>), grid, block, 0, s, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
+// Linear gaps (open == extend) take the biased linear cell (ix2 LIN);
+// SW_INTRA_LIN=0 keeps the Farrar form for them (A/B).
+bool intra_linear(const IntraArgs& a) {
+    const char* e = std::getenv("SW_INTRA_LIN");
+    return a.gap_open == a.gap_extend && !(e && e[0] == '0');
+}
+
+template <bool F16, bool LIST>
+static hipError_t launch_intra_x2_g(const IntraArgs& a, int ri, hipStream_t s) {
+    return intra_linear(a) ? launch_intra_x2_t<F16, LIST, true>(a, ri, s) : launch_intra_x2_t<F16, LIST, false>(a, ri, s);
+}
+
 hipError_t launch_intra_x2(const IntraArgs& a, int ri, hipStream_t s) {
     if (a.nsubj <= 0 || a.qpad <= 0) return hipSuccess;
-    return launch_intra_x2_t<true, false>(a, ri, s);
+    return launch_intra_x2_g<true, false>(a, ri, s);
 }
 
 // The int16 form over the device-side list of subjects the fp16 pass flagged
@@ -60,12 +72,12 @@ hipError_t launch_intra_x2(const IntraArgs& a, int ri, hipStream_t s) {
 // a.rescue_list for the int32 sw_intra.
 hipError_t launch_intra_x2_list16(const IntraArgs& a, int ri, hipStream_t s) {
     if (a.nsubj <= 0 || a.qpad <= 0) return hipSuccess;
-    return launch_intra_x2_t<false, true>(a, ri, s);
+    return launch_intra_x2_g<false, true>(a, ri, s);
 }
 
 hipError_t launch_intra_x2_int16(const IntraArgs& a, int ri, hipStream_t s) {
     if (a.nsubj <= 0 || a.qpad <= 0) return hipSuccess;
-    return launch_intra_x2_t<false, false>(a, ri, s);
+    return launch_intra_x2_g<false, false>(a, ri, s);
 }
 
 }  // namespace swk

@@ -439,7 +439,7 @@ def test_intra_two_subjects_per_wave(sw, oracle, handle, monkeypatch, packed, ri
     db = sw.Database(handle, r, o, long_threshold=64)
     assert db.stats()["n_long"] == len(subs)
     for qlen, mid, go, ge in [(40, 1, 12, 1), (375, 1, 12, 1), (600, 1, 12, 1), (700, 1, 11, 2), (1100, 0, 2, 2),
-                              (1500, 0, 2, 2), (2100, 1, 12, 1), (260, 0, 8, 8)]:
+                              (1500, 0, 2, 2), (2100, 1, 12, 1), (260, 0, 8, 8), (40, 0, 2, 2), (600, 1, 3, 3)]:
         q = q0[:qlen]
         m = sw.capi.builtin_matrix(mid)
         got = db.scan(q, m, go, ge)
