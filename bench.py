@@ -670,6 +670,7 @@ def main():
             wave_gcups = float(qtot) / nq * intra_res / (intra_ms * 1e-3) / 1e9 if intra_ms > 0 else 0.0
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
         traffic, traffic_note = None, "no rocprofv3 --pmc measurement of this workload and build"
+        valu_hw = None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
@@ -677,6 +678,19 @@ def main():
                     and tj.get("workload_key") == workload_key(args, qtot) and tj.get("kernel") == roof_kernel):
                 if tj.get("kernel_src_sha16") == kernel_source_hash():
                     traffic = tj.get("hbm_bytes_per_launch")
+                    if tj.get("sq_insts_valu_per_launch") and tj.get("profiled_ns_per_launch") and kernel_ms > 0:
+                        # hardware-anchored VALU fraction of the dominant
+                        # launch: its SQ_INSTS_VALU (wave instructions) at the
+                        # measured packed-op cost, over every SIMD's cycles at
+                        # the clock GRBM_GUI_ACTIVE shows under this load
+                        insts = tj["sq_insts_valu_per_launch"]
+                        clk = tj["grbm_gui_active_per_launch"] / tj["profiled_ns_per_launch"]  # GHz
+                        cells_launch = float(qtot) / nq * wave_res
+                        valu_hw = {"sq_insts_valu_per_launch": insts,
+                                   "valu_insts_per_128_cells": round(insts / (cells_launch / 128), 3),
+                                   "clock_ghz_under_load": round(clk, 3), "cycles_per_valu_inst": 4.25,
+                                   "issue_frac": round(insts * 4.25 / (SIMDS * clk * 1e9 * kernel_ms * 1e-3), 4),
+                                   "source": "stored rocprofv3 --pmc SQ pass (pmc_traffic.json), same kernel sources"}
                     traffic_note = ("stored rocprofv3 --pmc measurement (FETCH_SIZE x2 + WRITE_SIZE) of this "
                                     "workload, taken on a build with the same kernel sources (%s, %s)"
                                     % (tj.get("kernel_src_sha16"), tj.get("measured", "?")))
@@ -730,6 +744,7 @@ def main():
                          "kernel": roof_kernel,
                          "alg_bytes_per_launch": int(alg_bytes), "kernel_ms": round(kernel_ms, 4)},
             "valu_roofline": valu_roofline(roof_kernel, cells_all / world, kt["total_ms"] / nsc * nq, wave_gcups),
+            "valu_hw": valu_hw,
             "kernels": {"inter": kernel, "intra": intra_kernel},
             "top_hit": {"id": int(top_ids[0]), "score": int(top_scores[0])},
             "host": {"cores_used": args.cpu_threads or eff, "affinity_cpus": aff, "cgroup_quota_cpus": quota},

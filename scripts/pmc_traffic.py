@@ -7,8 +7,10 @@ section), on gfx950 FETCH_SIZE counts half the bytes of a wide (16 B/lane)
 streaming read, which is how sw_inter loads its packed residue groups, so it
 is doubled; WRITE_SIZE is taken as reported.
 
-usage: pmc_traffic.py FETCH_DIR WRITE_DIR WORKLOAD_KEY OUT_JSON ROCPROF_NAME_SUBSTR LABEL
-(LABEL = the library's kernel name, sw_last_kernel(), which bench.py matches)
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR WORKLOAD_KEY OUT_JSON ROCPROF_NAME_SUBSTR LABEL [SQ_DIR]
+(LABEL = the library's kernel name, sw_last_kernel(), which bench.py matches;
+SQ_DIR: a pass with SQ_INSTS_VALU and GRBM_GUI_ACTIVE for the VALU issue
+fraction of the same kernel)
 """
 import csv
 import datetime
@@ -30,8 +32,18 @@ def per_dispatch(d, counter, kernel):
     return vals
 
 
+def durations(d, kernel):
+    out = []
+    with open(d + "/run_counter_collection.csv") as f:
+        for row in csv.DictReader(f):
+            if kernel in row["Kernel_Name"] and row["Counter_Name"] == "SQ_INSTS_VALU":
+                out.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    return out
+
+
 def main():
     fdir, wdir, key, out, kernel, label = sys.argv[1:7]
+    sqdir = sys.argv[7] if len(sys.argv) > 7 else None
     f = per_dispatch(fdir, "FETCH_SIZE", kernel)
     w = per_dispatch(wdir, "WRITE_SIZE", kernel)
     fetch = sum(f) / len(f) * 1024 * 2
@@ -45,6 +57,13 @@ def main():
            # bench.py reports the bytes only for a build with these kernel sources
            "kernel_src_sha16": __import__("bench").kernel_source_hash(),
            "measured": datetime.date.today().isoformat()}
+    if sqdir:
+        v = per_dispatch(sqdir, "SQ_INSTS_VALU", kernel)
+        g = per_dispatch(sqdir, "GRBM_GUI_ACTIVE", kernel)
+        dn = durations(sqdir, kernel)
+        res["sq_insts_valu_per_launch"] = round(sum(v) / len(v))
+        res["grbm_gui_active_per_launch"] = round(sum(g) / len(g))
+        res["profiled_ns_per_launch"] = round(sum(dn) / len(dn)) if dn else None
     with open(out, "w") as fo:
         json.dump(res, fo, indent=1)
     print(json.dumps(res))
