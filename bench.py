@@ -684,7 +684,8 @@ def main():
                         # measured packed-op cost, over every SIMD's cycles at
                         # the clock GRBM_GUI_ACTIVE shows under this load
                         insts = tj["sq_insts_valu_per_launch"]
-                        clk = tj["grbm_gui_active_per_launch"] / tj["profiled_ns_per_launch"]  # GHz
+                        # GRBM_GUI_ACTIVE is summed over the 8 XCDs by rocprofv3
+                        clk = tj["grbm_gui_active_per_launch"] / 8 / tj["profiled_ns_per_launch"]  # GHz
                         cells_launch = float(qtot) / nq * wave_res
                         valu_hw = {"sq_insts_valu_per_launch": insts,
                                    "valu_insts_per_128_cells": round(insts / (cells_launch / 128), 3),

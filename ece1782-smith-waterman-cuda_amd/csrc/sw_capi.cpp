@@ -268,6 +268,7 @@ struct sw_db {
     struct LptTable {
         int32_t qpad, qpad_intra, ri, npair, group /* quad blocks */, npipe, qpad_pipe, n;
         int32_t* d_order;
+        std::vector<float> cost;  // estimated duration of each entry, longest first
     };
     std::vector<LptTable> lpt_tables;
     bool last_pair_merged = false;
@@ -809,13 +810,22 @@ int32_t lpt_pipe_pairs(const sw_db* db, int32_t qlen) {
     return static_cast<int32_t>((k + 1) / 2);
 }
 
+// Workgroups whose estimated duration is at least kPrioFrac x the longest
+// raise their wave priority (SW_LPT_PRIO=f overrides the fraction; 0: off).
+constexpr double kPrioFrac = 0.0;
+
 int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad, int32_t npipe,
-              int32_t qpad_pipe, const int32_t** order, int* n) {
+              int32_t qpad_pipe, const int32_t** order, int* n, int* nprio) {
+    double pf = kPrioFrac;
+    if (const char* e = std::getenv("SW_LPT_PRIO")) pf = std::atof(e);
     for (const auto& t : db->lpt_tables)
         if (t.qpad == qpad && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad &&
             t.npipe == npipe && t.qpad_pipe == qpad_pipe) {
             *order = t.d_order;
             *n = t.n;
+            *nprio = 0;
+            if (pf > 0)
+                while (*nprio < t.n && t.cost[static_cast<size_t>(*nprio)] >= pf * t.cost[0]) ++*nprio;
             return SW_OK;
         }
     const int passes = qpad / 64;
@@ -853,8 +863,13 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
         return x.first > y.first;
     });
     std::vector<int32_t> ord(w.size());
-    for (size_t k = 0; k < w.size(); ++k) ord[k] = w[k].second;
-    sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, npipe, qpad_pipe, static_cast<int32_t>(ord.size()), nullptr};
+    std::vector<float> cost(w.size());
+    for (size_t k = 0; k < w.size(); ++k) {
+        ord[k] = w[k].second;
+        cost[k] = static_cast<float>(w[k].first);
+    }
+    sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, npipe, qpad_pipe, static_cast<int32_t>(ord.size()), nullptr,
+                      cost};
     HIPCHECK(hipMalloc(reinterpret_cast<void**>(&t.d_order), ord.size() * sizeof(int32_t)));
     HIPCHECK(hipMemcpy(t.d_order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     db->device_bytes += ord.size() * sizeof(int32_t);
@@ -865,6 +880,9 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     db->lpt_tables.push_back(t);
     *order = t.d_order;
     *n = t.n;
+    *nprio = 0;
+    if (pf > 0)
+        while (*nprio < t.n && cost[static_cast<size_t>(*nprio)] >= pf * cost[0]) ++*nprio;
     return SW_OK;
 }
 
@@ -1269,8 +1287,11 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             ip.qpad = qpad_pipe;
             ip.pair_base = 0;
             lpt_intra.pair_base = npipe;
-            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, npipe, qpad_pipe, &order, &nwg)))
+            int nprio = 0;
+            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, npipe, qpad_pipe, &order, &nwg,
+                                &nprio)))
                 return rc;
+            a.lpt_prio = nprio;
             HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, ip, order, nwg, affine, ri2, h->stream));
             HIPCHECK(hipEventRecord(h->ev[7], h->stream));
             if ((rc = launch_long(true))) return rc;

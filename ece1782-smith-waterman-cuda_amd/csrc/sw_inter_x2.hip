@@ -937,6 +937,9 @@ __global__ __launch_bounds__(256, 2) void sw_scan_lpt(InterArgs a, IntraArgs ia,
     __shared__ __attribute__((aligned(16))) char smem[kMax];
     const int item = order[blockIdx.x];
     const uint64_t t0 = trace_now();
+    // the longest work (the launch's critical path) wins the SIMDs' issue
+    // arbitration against the shorter work sharing them
+    if (static_cast<int>(blockIdx.x) < a.lpt_prio) __builtin_amdgcn_s_setprio(2);
     if (item >= 0)
         x2p_wg<R, SG, AFFINE, true, true, 4>(a, item, a.blk_quad, *reinterpret_cast<X2pSmem<R, SG, 4>*>(smem));
     else if (item > -kLptPipe)

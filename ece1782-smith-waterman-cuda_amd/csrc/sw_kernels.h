@@ -83,6 +83,9 @@ struct InterArgs {
     int32_t blk_base;
     // sw_scan_lpt: blocks [blk_base, blk_quad) run by wave quads
     int32_t blk_quad;
+    // sw_scan_lpt: workgroups [0, lpt_prio) of the (longest-first) order
+    // raise their wave priority (the critical path of a small database)
+    int32_t lpt_prio;
     // fp16 kernels: the largest flagged block id (atomicMax; nullable), read
     // back by the host to route the widest blocks to int16 next time
     int32_t* rescue_max;
