@@ -451,7 +451,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--verify-seconds", type=float, default=15.0,
+    ap.add_argument("--verify-seconds", type=float, default=25.0,
                     help="oracle budget per rank for the parity leg (whole share if it fits)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-gpu", action="store_true", help="c1: skip the GPU comparison")

@@ -855,8 +855,10 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     for (int64_t g = 0; g < iwg; ++g)
         w.emplace_back((db->h_llen[static_cast<size_t>(2 * npipe + 8 * g)] + swk::kLanes - 1) * nch * intra_step_us(ri),
                        static_cast<int32_t>(-1 - g));
+    double pipe_cost = 1.0;  // SW_PIPE_COST: scale of the pipelined pairs' estimate (ordering A/B)
+    if (const char* e = std::getenv("SW_PIPE_COST")) pipe_cost = std::atof(e);
     for (int64_t q = 0; q < npipe; ++q)
-        w.emplace_back((db->h_llen[static_cast<size_t>(2 * q)] + swk::kLanes - 1 + 128.0 * (pch - 1)) *
+        w.emplace_back(pipe_cost * (db->h_llen[static_cast<size_t>(2 * q)] + swk::kLanes - 1 + 128.0 * (pch - 1)) *
                            intra_step_us(rp),
                        static_cast<int32_t>(-swk::lpt_pipe_item() - q));
     std::stable_sort(w.begin(), w.end(), [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) {
