@@ -455,6 +455,10 @@ def main():
                     help="oracle budget per rank for the parity leg (whole share if it fits)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-gpu", action="store_true", help="c1: skip the GPU comparison")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="run each step's top-K exchange on the scan's stream instead of overlapping the next scan")
+    ap.add_argument("--exchange-priority", type=int, default=0,
+                    help="HIP stream priority of the exchange stream (negative = higher)")
     # the latest rocprofv3 --pmc measurement of the C2 launch (FETCH_SIZE x2 +
     # WRITE_SIZE, scripts/pmc_traffic.py); kept at the root because profiles/
     # does not travel to the GPU box
@@ -532,7 +536,9 @@ def main():
     log("rank %d: share %d/%d: %d subjects, %d residues, generated + packed + resident in %.1fs: %s"
         % (rank, shard_rank, shard_world, n, residues, time.perf_counter() - t0, st))
 
-    scores = torch.zeros((nq, max(n, 1)), dtype=torch.int32, device=dev)
+    # two score buffers: the top-K exchange of step i (on its own stream)
+    # overlaps the scan of step i + 1
+    scores_buf = [torch.zeros((nq, max(n, 1)), dtype=torch.int32, device=dev) for _ in range(2)]
     K = args.topk
     top = torch.empty((nq, K), dtype=torch.int64, device=dev)
     gathered = torch.empty((world, nq, K), dtype=torch.int64, device=dev)
@@ -542,28 +548,48 @@ def main():
     mat = sw.capi.builtin_matrix(MATRICES[args.matrix])
     scoring = (mat, args.gap_open, args.gap_extend)
 
+    # The exchange (device top-K, RCCL all-gather, merge) runs on a second
+    # stream with its own library handle, so it overlaps the next step's scan
+    # (HIP events order the two; --no-overlap runs everything on one stream).
+    xstream = stream if args.no_overlap else torch.cuda.Stream(dev, priority=args.exchange_priority)
+    xhandle = handle
+    if not args.no_overlap:
+        xhandle = sw.Handle(gpu)
+        xhandle.set_stream(xstream.cuda_stream)
+    scanned = [torch.cuda.Event(), torch.cuda.Event()]
+    ranked = [torch.cuda.Event(), torch.cuda.Event()]
+    counter = [0]
+
     def step():
+        b = counter[0] % 2
+        counter[0] += 1
+        scores = scores_buf[b]
+        if counter[0] > 2:
+            stream.wait_event(ranked[b])  # step i-2's top-K has read this buffer
         if nq == 1:
             db.scan_device(queries[0], scores.data_ptr(), *scoring)
         else:
             db.scan_batch_device(queries, scores.data_ptr(), *scoring)
-        # device top-K per query: int64 keys (score << 32 | 2^31-1-global id), best first
-        for k in range(nq):
-            if gid_dev is not None:
-                handle.topk_device_ids(scores[k].data_ptr(), n, gid_dev.data_ptr(), K, top[k].data_ptr())
-            else:
-                handle.topk_device(scores[k].data_ptr(), n, K, top[k].data_ptr(), id_base=id_base)
-        if world == 1:
-            return
-        if args.backend == "nccl":
-            tdist.all_gather_into_tensor(gathered, top)  # RCCL over xGMI: nq x K x 8 B per rank
-        else:
-            parts = [torch.empty((nq, K), dtype=torch.int64) for _ in range(world)]
-            tdist.all_gather(parts, top.cpu())
-            gathered.copy_(torch.stack(parts))
-        for k in range(nq):
-            merged = gathered[:, k, :].contiguous()
-            handle.topk_keys_device(merged.data_ptr(), world * K, K, final[k].data_ptr())
+        scanned[b].record(stream)
+        xstream.wait_event(scanned[b])
+        with torch.cuda.stream(xstream):
+            # device top-K per query: int64 keys (score << 32 | 2^31-1-global id), best first
+            for k in range(nq):
+                if gid_dev is not None:
+                    xhandle.topk_device_ids(scores[k].data_ptr(), n, gid_dev.data_ptr(), K, top[k].data_ptr())
+                else:
+                    xhandle.topk_device(scores[k].data_ptr(), n, K, top[k].data_ptr(), id_base=id_base)
+            if world > 1:
+                if args.backend == "nccl":
+                    tdist.all_gather_into_tensor(gathered, top)  # RCCL over xGMI: nq x K x 8 B per rank
+                else:
+                    parts = [torch.empty((nq, K), dtype=torch.int64) for _ in range(world)]
+                    tdist.all_gather(parts, top.cpu())
+                    gathered.copy_(torch.stack(parts))
+                for k in range(nq):
+                    merged = gathered[:, k, :].contiguous()
+                    xhandle.topk_keys_device(merged.data_ptr(), world * K, K, final[k].data_ptr())
+            ranked[b].record(xstream)
 
     cells_rank = float(qtot) * residues
 
@@ -581,11 +607,13 @@ def main():
         t_start = time.perf_counter()
         for _ in range(args.steps):
             step()
+        t_enq = time.perf_counter() - t_start  # host time to enqueue the K steps
         torch.cuda.synchronize()
         if world > 1:
             tdist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t_start
+        log("rank %d: %d steps in %.3f ms, host enqueue %.3f ms" % (rank, args.steps, elapsed * 1e3, t_enq * 1e3))
         kt = handle.timing_total()
         if world > 1:
             t = torch.tensor([elapsed, cells_rank], dtype=torch.float64,
@@ -600,8 +628,8 @@ def main():
     st = db.stats()  # the coop split of the timed scans
     final_keys = (final if world > 1 else top).cpu().numpy()
     top_ids, top_scores = sw.capi.decode_keys(final_keys[0])
-    # the measured run's scores and keys, for the parity leg
-    gs = scores.cpu().numpy()[:, :n]
+    # the measured run's scores and keys (its last step's buffer), for the parity leg
+    gs = scores_buf[(counter[0] - 1) % 2].cpu().numpy()[:, :n]
     dev_top = top.cpu().numpy()
 
     ref = None
@@ -768,6 +796,8 @@ def main():
         tdist.barrier()
         tdist.destroy_process_group()
     db.close()
+    if xhandle is not handle:
+        xhandle.close()
     handle.close()
 
 

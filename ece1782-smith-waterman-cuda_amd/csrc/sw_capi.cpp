@@ -47,6 +47,17 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
+// record event k of the current scan's set on stream s
+#define MARK(k, s)                                  \
+    do {                                            \
+        HIPCHECK(hipEventRecord(h->ev[k], (s)));    \
+        *h->ev_rec |= 1u << (k);                    \
+    } while (0)
+
+hipError_t ensure_stream(hipStream_t& s) {
+    return s ? hipSuccess : hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+}
+
 #define HIPCHECK(expr)                                                                  \
     do {                                                                                \
         hipError_t e_ = (expr);                                                         \
@@ -163,6 +174,9 @@ struct ScanEvents {
     // each inter kernel on its own stream: 4/5 the cooperative kernel
     // (side2), 6/7 the per-wave kernel (main)
     hipEvent_t ev[8] = {};
+    unsigned rec = 0;  // bit k: ev[k] was recorded by this scan (read_events
+                       // falls back for the others: each record is a packet
+                       // the command processor spends microseconds on)
     int launches = 0;
 };
 
@@ -176,6 +190,7 @@ struct sw_handle {
     std::vector<ScanEvents> evpool;
     size_t nscans = 0;
     hipEvent_t* ev = nullptr;  // event set of the current scan
+    unsigned* ev_rec = nullptr;
     // The intra kernel runs on a side stream, concurrently with the inter
     // kernel (fork/join through ev[0] and ev[1]).
     hipStream_t side = nullptr;
@@ -195,10 +210,18 @@ struct sw_handle {
         size_t hcap = 0;
         hipEvent_t copied = nullptr;  // the staging buffer may be rewritten after this
         bool pending = false;
+        hipEvent_t used = nullptr;    // the last scan reading the device copy has finished
+                                      // (that scan's end event, owned by evpool)
+        bool used_pending = false;
     };
     static constexpr int kProfSlots = 4;
     ProfSlot prof[kProfSlots];
     int prof_next = 0;
+    ProfSlot* prof_cur = nullptr;     // the slot of the scan being enqueued
+    // profiles are copied on their own stream, so the H2D copy of the next
+    // scan's profile overlaps the running scan instead of sitting between
+    // two scans on the main stream
+    hipStream_t copy = nullptr;
     int32_t* d_scores = nullptr;  // for the synchronous sw_scan
     size_t scores_cap = 0;
     int64_t* d_topk_work = nullptr;  // device top-K workspace
@@ -238,6 +261,10 @@ struct sw_db {
     int32_t* h_lcount = nullptr;
     hipEvent_t lcount_ev = nullptr;
     bool lcount_pending = false;
+    uint64_t lcount_qhash = 0;
+    bool lcount_seen = false;  // the last observation read back (see icount_seen)
+    uint64_t lseen_key = 0, lseen_qhash = 0;
+    int32_t lseen_qlen = 0;
     uint64_t lcount_key = 0;
     int32_t lcount_qlen = 0;
     std::vector<std::pair<uint64_t, int32_t>> i16_first;
@@ -250,6 +277,12 @@ struct sw_db {
     uint64_t icount_key = 0;
     int32_t icount_qlen = 0;
     int32_t icount_nr = 0;
+    uint64_t icount_qhash = 0;
+    // the last observation read back: a scan repeating it (same query,
+    // scoring and split) does not read it back again
+    bool icount_seen = false;
+    uint64_t seen_key = 0, seen_qhash = 0;
+    int32_t seen_qlen = 0, seen_nr = 0;
     struct SpanObs {
         uint64_t key;
         int32_t qlen;
@@ -348,8 +381,10 @@ void free_dev(sw_db* db) {
     for (auto& t : db->lpt_tables) (void)hipFree(t.d_order);
     db->lpt_tables.clear();
     db->lcount_pending = false;
+    db->lcount_seen = false;
     db->i16_first.clear();  // the long partition may change
     db->icount_pending = false;
+    db->icount_seen = false;
     db->i16_span.clear();   // ... and the block layout
     db->device_bytes = 0;
     db->built = false;
@@ -660,6 +695,7 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     if (P->total > S.dcap) {
         if (S.d) {
             HIPCHECK(hipStreamSynchronize(h->stream));  // scans in flight may still read it
+            if (h->copy) HIPCHECK(hipStreamSynchronize(h->copy));
             HIPCHECK(hipFree(S.d));
         }
         S.dcap = std::max<size_t>(P->total, 1 << 16);
@@ -691,9 +727,15 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
                     for (int r = 0; r < rip; ++r) d[r] = static_cast<int8_t>(r < ri ? value(c, ch * CH + t * ri + r) : 0);
                 }
     }
-    HIPCHECK(hipMemcpyAsync(S.d, hp, P->total, hipMemcpyHostToDevice, h->stream));
-    HIPCHECK(hipEventRecord(S.copied, h->stream));
+    // the device copy is rewritten once the scan that last read it is done;
+    // the scan waits for the copy
+    HIPCHECK(ensure_stream(h->copy));
+    if (S.used_pending) HIPCHECK(hipStreamWaitEvent(h->copy, S.used, 0));
+    HIPCHECK(hipMemcpyAsync(S.d, hp, P->total, hipMemcpyHostToDevice, h->copy));
+    HIPCHECK(hipEventRecord(S.copied, h->copy));
+    HIPCHECK(hipStreamWaitEvent(h->stream, S.copied, 0));
     S.pending = true;
+    h->prof_cur = &S;
     return SW_OK;
 }
 
@@ -896,6 +938,8 @@ int next_events(sw_handle* h) {
         h->evpool.push_back(se);
     }
     h->ev = h->evpool[h->nscans].ev;
+    h->ev_rec = &h->evpool[h->nscans].rec;
+    *h->ev_rec = 0;
     h->evpool[h->nscans].launches = 0;
     ++h->nscans;
     return SW_OK;
@@ -956,8 +1000,14 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     uint64_t skey = 1469598103934665603ull;  // FNV-1a of the scoring
     for (int k = 0; k < 625; ++k) skey = (skey ^ static_cast<uint8_t>(mat[k])) * 1099511628211ull;
     skey = ((skey ^ static_cast<uint32_t>(go)) * 1099511628211ull ^ static_cast<uint32_t>(ge)) * 1099511628211ull;
+    uint64_t qhash = 1469598103934665603ull;  // FNV-1a of the query (which
+    for (int32_t k = 0; k < qlen; ++k) qhash = (qhash ^ query[k]) * 1099511628211ull;  // readbacks repeat)
     if (db->lcount_pending && hipEventQuery(db->lcount_ev) == hipSuccess) {
         db->lcount_pending = false;
+        db->lcount_seen = true;
+        db->lseen_key = db->lcount_key;
+        db->lseen_qhash = db->lcount_qhash;
+        db->lseen_qlen = db->lcount_qlen;
         if (2 * static_cast<int64_t>(*db->h_lcount) > db->nlong) {
             bool seen = false;
             for (auto& e : db->i16_first)
@@ -986,6 +1036,11 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // beside the fp16 launch.  SW_INTER_I16_SPAN=n forces n blocks (0: off).
     if (db->icount_pending && hipEventQuery(db->icount_ev) == hipSuccess) {
         db->icount_pending = false;
+        db->icount_seen = true;
+        db->seen_key = db->icount_key;
+        db->seen_qhash = db->icount_qhash;
+        db->seen_qlen = db->icount_qlen;
+        db->seen_nr = db->icount_nr;
         const int32_t cnt = db->h_icount[0], span = db->h_icount[1] + 1;
         // most of [nr, span) flagged: not a few high-scoring hits far out
         if (cnt > 0 && span > db->icount_nr && 2 * static_cast<int64_t>(cnt) >= span - db->icount_nr) {
@@ -1025,10 +1080,10 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         db->last_npair = 0;
         h->last_kernel = "none";
         h->last_intra = "none";
-        HIPCHECK(hipEventRecord(h->ev[0], h->stream));
+        MARK(0, h->stream);
         if (db->max_id >= 0)
             HIPCHECK(hipMemsetAsync(scores_dev, 0, static_cast<size_t>(db->max_id + 1) * 4, h->stream));
-        for (int k = 1; k < 8; ++k) HIPCHECK(hipEventRecord(h->ev[k], h->stream));
+        for (int k = 1; k < 8; ++k) MARK(k, h->stream);
         h->timed = true;
         return SW_OK;
     }
@@ -1098,7 +1153,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                      swk::lpt_supported(ri2);
     db->last_lpt = lpt;
     // fork: the side stream starts when the main stream reaches ev[0]
-    HIPCHECK(hipEventRecord(h->ev[0], h->stream));
+    MARK(0, h->stream);
     h->last_intra = "none";
     // the long subjects' stream: a side stream, concurrent with the inter
     // kernels (SW_INTRA_SERIAL=1: the main stream, before them — to measure
@@ -1106,11 +1161,15 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // the main stream after it (only the rescue stages are left to run)
     const char* iser = std::getenv("SW_INTRA_SERIAL");
     hipStream_t is = (lpt || (iser && iser[0] == '1')) ? h->stream : h->side;
+    if (db->nlong && is != h->stream) {
+        HIPCHECK(ensure_stream(h->side));
+        is = h->side;
+    }
     swk::IntraArgs lpt_intra{};
     // the long subjects' kernels: all of them, or (lpt_done) those after the
     // fp16 pass the merged launch ran
     auto launch_long = [&](bool lpt_done) -> int {
-        if (!lpt_done) HIPCHECK(hipStreamWaitEvent(is, h->ev[0], 0));
+        if (!lpt_done && is != h->stream) HIPCHECK(hipStreamWaitEvent(is, h->ev[0], 0));
         swk::IntraArgs ia{};
         ia.residues = db->d_lres;
         ia.subj_off = db->d_loff;
@@ -1156,12 +1215,15 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                                            hipHostMallocDefault));
                     HIPCHECK(hipEventCreateWithFlags(&db->lcount_ev, hipEventDisableTiming));
                 }
-                if (!db->lcount_pending) {
+                const bool lseen = db->lcount_seen && db->lseen_key == skey && db->lseen_qhash == qhash &&
+                                   db->lseen_qlen == qlen;
+                if (!db->lcount_pending && !lseen) {
                     HIPCHECK(hipMemcpyAsync(db->h_lcount, list1, sizeof(int32_t), hipMemcpyDeviceToHost, is));
                     HIPCHECK(hipEventRecord(db->lcount_ev, is));
                     db->lcount_pending = true;
                     db->lcount_key = skey;
                     db->lcount_qlen = qlen;
+                    db->lcount_qhash = qhash;
                 }
                 // the int16 form re-scores the fp16 pass's list (scores near
                 // 2048: high-scoring pairs, or linear scoring with cheap gaps)
@@ -1186,7 +1248,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         return SW_OK;
     };
     if (db->nlong && (rc = launch_long(false))) return rc;
-    if (!lpt) HIPCHECK(hipEventRecord(h->ev[1], db->nlong ? is : h->stream));
+    if (!lpt) MARK(1, db->nlong ? is : h->stream);
     if (db->nblocks) {
         swk::InterArgs a{};
         a.residues = db->d_res;
@@ -1233,10 +1295,11 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             swk::InterArgs c = a;
             c.qpad = qpad_coop;
             c.prof = P.dev + P.off8;  // the coop kernel reads the int8 profile
+            HIPCHECK(ensure_stream(h->side2));
             HIPCHECK(hipStreamWaitEvent(h->side2, h->ev[0], 0));
-            HIPCHECK(hipEventRecord(h->ev[4], h->side2));
+            MARK(4, h->side2);
             HIPCHECK(swk::launch_inter_coop(c, ncoop, affine, h->side2));
-            HIPCHECK(hipEventRecord(h->ev[5], h->side2));
+            MARK(5, h->side2);
             HIPCHECK(hipEventRecord(h->coop_done, h->side2));
             ++h->launches;
             a.blk_first = ncoop;
@@ -1245,11 +1308,12 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             // (after the list counters above are reset: they share listA)
             swk::InterArgs c = a;
             c.nblocks = npair;
+            HIPCHECK(ensure_stream(h->side2));
             HIPCHECK(hipEventRecord(h->fork2, h->stream));
             HIPCHECK(hipStreamWaitEvent(h->side2, h->fork2, 0));
-            HIPCHECK(hipEventRecord(h->ev[4], h->side2));
+            MARK(4, h->side2);
             HIPCHECK(swk::launch_inter_x2p(c, affine, f16, false, pair_group(db), h->side2));
-            HIPCHECK(hipEventRecord(h->ev[5], h->side2));
+            MARK(5, h->side2);
             HIPCHECK(hipEventRecord(h->coop_done, h->side2));
             ++h->launches;
             a.blk_first = npair;
@@ -1262,18 +1326,16 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             c.rescue_list = listB + 1;
             c.rescue_count = listB;
             c.rescue_max = nullptr;
+            HIPCHECK(ensure_stream(h->side2));
             HIPCHECK(hipEventRecord(h->fork2, h->stream));
             HIPCHECK(hipStreamWaitEvent(h->side2, h->fork2, 0));
-            HIPCHECK(hipEventRecord(h->ev[4], h->side2));
+            MARK(4, h->side2);
             HIPCHECK(swk::launch_inter_x2p(c, affine, false, false, 2, h->side2));
-            HIPCHECK(hipEventRecord(h->ev[5], h->side2));
+            MARK(5, h->side2);
             HIPCHECK(hipEventRecord(h->coop_done, h->side2));
             ++h->launches;
-        } else {
-            HIPCHECK(hipEventRecord(h->ev[4], h->stream));
-            HIPCHECK(hipEventRecord(h->ev[5], h->stream));
         }
-        HIPCHECK(hipEventRecord(h->ev[6], h->stream));
+        MARK(6, h->stream);
         if (lpt) {
             // one launch: the inter groups + single waves and the long
             // subjects' fp16 pass, longest work first; then the long
@@ -1295,9 +1357,8 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                 return rc;
             a.lpt_prio = nprio;
             HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, ip, order, nwg, affine, ri2, h->stream));
-            HIPCHECK(hipEventRecord(h->ev[7], h->stream));
+            MARK(7, h->stream);
             if ((rc = launch_long(true))) return rc;
-            HIPCHECK(hipEventRecord(h->ev[1], h->stream));
         } else if (npair && pair_merged) {
             // one launch: pairs for blocks [nr, npair), one wave per block after
             a.blk_base = nr;
@@ -1310,10 +1371,12 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         if (npair) h->last_kernel.replace(0, std::strlen("sw_inter_x2s"), "sw_inter_x2p");  // + wave pairs
         if (nr) h->last_kernel += "+int16[0," + std::to_string(nr) + ")";
         if (lpt) h->last_kernel += "+lpt";
-        if (!lpt) HIPCHECK(hipEventRecord(h->ev[7], h->stream));
+        if (!lpt) MARK(7, h->stream);
         ++h->launches;
         if (ncoop || (npair && !pair_merged) || nr) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
-        if (f16 && rescue && !db->icount_pending) {
+        const bool seen = db->icount_seen && db->seen_key == skey && db->seen_qhash == qhash &&
+                          db->seen_qlen == qlen && db->seen_nr == nr;
+        if (f16 && rescue && !db->icount_pending && !seen) {
             // the fp16 pass's flagged count and largest flagged block, read
             // by a later scan (no synchronisation here), after every fp16
             // launch that appends to list A has joined the main stream
@@ -1329,6 +1392,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             db->icount_key = skey;
             db->icount_qlen = qlen;
             db->icount_nr = nr;
+            db->icount_qhash = qhash;
         }
         if (f16) {
             // fp16 chain, stage 2: the int16 packed kernel re-scores the
@@ -1359,11 +1423,16 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         }
     }
     if (!db->nblocks)
-        for (int k = 4; k < 8; ++k) HIPCHECK(hipEventRecord(h->ev[k], h->stream));
-    HIPCHECK(hipEventRecord(h->ev[2], h->stream));
-    // join
-    if (db->nlong) HIPCHECK(hipStreamWaitEvent(h->stream, h->ev[1], 0));
-    HIPCHECK(hipEventRecord(h->ev[3], h->stream));
+        for (int k = 6; k < 8; ++k) MARK(k, h->stream);
+    // (the merged launch has no separate inter end, nor a side stream to join)
+    if (!lpt) MARK(2, h->stream);
+    if (db->nlong && !lpt) HIPCHECK(hipStreamWaitEvent(h->stream, h->ev[1], 0));
+    MARK(3, h->stream);
+    if (h->prof_cur) {  // the profile slot's device copy may be rewritten after this scan
+        h->prof_cur->used = h->ev[3];
+        h->prof_cur->used_pending = true;
+        h->prof_cur = nullptr;
+    }
     h->evpool[h->nscans - 1].launches = h->launches;
     h->timed = true;
     if (std::getenv("SW_RESCUE_STATS")) {  // diagnostics: what the guard bands flagged (synchronises)
@@ -1479,8 +1548,9 @@ int sw_create(int32_t device, sw_handle** out) {
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete h; return fail(SW_E_HIP, hipGetErrorString(e)); }
     h->own_stream = true;
-    e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side2, hipStreamNonBlocking);
+    // side, side2 and copy are created on first use: HIP maps streams onto a
+    // few hardware queues (GPU_MAX_HW_QUEUES), and two streams sharing one
+    // run in order, so a handle that never needs them should not hold them
     for (auto& S : h->prof)
         if (e == hipSuccess) e = hipEventCreateWithFlags(&S.copied, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->coop_done, hipEventDisableTiming);
@@ -1499,6 +1569,7 @@ int sw_destroy(sw_handle* h) {
             if (ev) (void)hipEventDestroy(ev);
     if (h->side) (void)hipStreamSynchronize(h->side);
     if (h->side2) (void)hipStreamSynchronize(h->side2);
+    if (h->copy) (void)hipStreamSynchronize(h->copy);
     for (auto& S : h->prof) {
         if (S.d) (void)hipFree(S.d);
         if (S.h) (void)hipHostFree(S.h);
@@ -1508,6 +1579,7 @@ int sw_destroy(sw_handle* h) {
     if (h->d_topk_work) (void)hipFree(h->d_topk_work);
     if (h->side) (void)hipStreamDestroy(h->side);
     if (h->side2) (void)hipStreamDestroy(h->side2);
+    if (h->copy) (void)hipStreamDestroy(h->copy);
     if (h->coop_done) (void)hipEventDestroy(h->coop_done);
     if (h->fork2) (void)hipEventDestroy(h->fork2);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
@@ -1726,7 +1798,7 @@ int sw_db_free(sw_db* db) {
     if (!db) return SW_OK;
     (void)hipSetDevice(db->h->device);
     (void)hipStreamSynchronize(db->h->stream);
-    (void)hipStreamSynchronize(db->h->side);
+    if (db->h->side) (void)hipStreamSynchronize(db->h->side);
     if (db->h_trace) {  // the last scan's block timeline (tail analysis builds)
         if (const char* path = std::getenv("SW_TRACE_FILE"))
             if (FILE* f = std::fopen(path, "wb")) {
@@ -1772,7 +1844,7 @@ int sw_db_set_long_threshold(sw_db* db, int32_t threshold) {
     if (t == db->long_threshold && db->built) return SW_OK;
     HIPCHECK(hipSetDevice(db->h->device));
     HIPCHECK(hipStreamSynchronize(db->h->stream));
-    HIPCHECK(hipStreamSynchronize(db->h->side));
+    if (db->h->side) HIPCHECK(hipStreamSynchronize(db->h->side));
     free_dev(db);
     db->long_threshold = t;
     return build_db(db);
@@ -1853,13 +1925,17 @@ int read_events(const ScanEvents& se, sw_timing* t) {
     HIPCHECK(hipEventSynchronize(se.ev[3]));
     // intra runs on the side stream from the fork (ev0) to ev1; inter on the
     // main stream from ev0 to ev2; they overlap.
+    // (events a scan did not record: the intra and inter spans fall back to
+    // the whole scan, the cooperative kernel's to 0)
+    auto has = [&](int k) { return (se.rec >> k & 1u) != 0; };
     float t01 = 0, t02 = 0, t03 = 0;
-    HIPCHECK(hipEventElapsedTime(&t01, se.ev[0], se.ev[1]));
-    HIPCHECK(hipEventElapsedTime(&t02, se.ev[0], se.ev[2]));
     HIPCHECK(hipEventElapsedTime(&t03, se.ev[0], se.ev[3]));
+    t01 = t02 = t03;
+    if (has(1)) HIPCHECK(hipEventElapsedTime(&t01, se.ev[0], se.ev[1]));
+    if (has(2)) HIPCHECK(hipEventElapsedTime(&t02, se.ev[0], se.ev[2]));
     float t45 = 0, t67 = 0;
-    HIPCHECK(hipEventElapsedTime(&t45, se.ev[4], se.ev[5]));
-    HIPCHECK(hipEventElapsedTime(&t67, se.ev[6], se.ev[7]));
+    if (has(4) && has(5)) HIPCHECK(hipEventElapsedTime(&t45, se.ev[4], se.ev[5]));
+    if (has(6) && has(7)) HIPCHECK(hipEventElapsedTime(&t67, se.ev[6], se.ev[7]));
     t->intra_ms += t01;
     t->inter_ms += t02;
     t->total_ms += t03;
