@@ -181,6 +181,7 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
     constexpr int NACC = RI + NB - 1;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
+    const bool is_last_lane = lane == kLanes - 1;
     const int p = a.pair_base + (PIPE ? wgi : wgi * kWavesPerWG + wave);  // subject pair
     int sa = 2 * p, sb = 2 * p + 1;
     bool hasA = sa < a.nsubj, hasB = sb < a.nsubj;
@@ -257,7 +258,7 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
         uint32_t hl = C::step(a, RI + NB - 2), fl = C::step(a, RI + NB - 1);
         uint32_t up_prev = C::step(a, NB - 2);
         uint32_t rc = kPadPair;        // codes (A | B << 8) of this lane's current column
-        uint32_t in_res = kPadPair, in_bh = 0, in_bf = 0, out_h = 0, out_f = 0;
+        uint32_t in_res = kPadPair, in_bh = 0, in_bf = 0;
         const int nsteps = L + kLanes - 1;
         // LDS byte address of this lane's element of code 0
         const uint32_t lrow = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(cimg + lane));
@@ -281,7 +282,10 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
             return ca | (cb << 8);
         };
         uint32_t in_res_nb = codes_at(lane);  // codes of the next block of 64 steps
-        Elem wa_n[NQ], wb_n[NQ];               // prefetched words of the next step
+        // profile words, double-buffered by step parity (NB is even, so a
+        // bias period starts on buffer 0): step b reads W[b & 1] and
+        // prefetches the next step's into the other, no register copies
+        Elem W[2][2][NQ];
         uint32_t rc_n = 0;
 
         // blocks of 64 steps; PIPE: every wave joins one barrier per block of
@@ -314,7 +318,7 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
             }
             if (kPrefetch && k0 == 0) {
                 rc_n = shr1u(__builtin_amdgcn_readlane(in_res, 0), rc);
-                read_words(rc_n, wa_n, wb_n);
+                read_words(rc_n, W[0][0], W[0][1]);
             }
             // whole bias periods (steps past nsteps run pad columns: harmless)
             const int mend = min(kLanes, nsteps - k0);
@@ -324,21 +328,18 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
                     const int m = m0 + b;
                     const uint32_t sbh = __builtin_amdgcn_readlane(in_bh, m);
                     const uint32_t sbf = LIN ? 0u : __builtin_amdgcn_readlane(in_bf, m);
-                    Elem wa[NQ], wb[NQ];
+                    static_assert(NB % 2 == 0, "buffer parity");
+                    Elem(&wa)[NQ] = W[b & 1][0];
+                    Elem(&wb)[NQ] = W[b & 1][1];
                     if constexpr (kPrefetch) {
                         rc = rc_n;
-#pragma unroll
-                        for (int qq = 0; qq < NQ; ++qq) {
-                            wa[qq] = wa_n[qq];
-                            wb[qq] = wb_n[qq];
-                        }
                         // the next step's codes: lane 0 takes the next column
                         // (the next block's first at the block's last step)
                         const bool wrap = (b == NB - 1) && (m0 + NB == kLanes);
                         const uint32_t sres_n = wrap ? __builtin_amdgcn_readlane(in_res_nb, 0)
                                                      : __builtin_amdgcn_readlane(in_res, (m + 1) & (kLanes - 1));
                         rc_n = shr1u(sres_n, rc);
-                        read_words(rc_n, wa_n, wb_n);
+                        read_words(rc_n, W[(b + 1) & 1][0], W[(b + 1) & 1][1]);
                     } else {
                         rc = shr1u(__builtin_amdgcn_readlane(in_res, m), rc);
                         read_words(rc, wa, wb);
@@ -393,25 +394,16 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
                     hl = C::bits(H[RI - 1]);
                     if constexpr (!LIN) fl = C::bits(f);
                     if (!last) {
-                        // lane 63 finished column k - 63: collect it for the next pass
+                        // lane 63 finished column k - 63: it stores it for the
+                        // next pass itself (no per-step collection across lanes)
                         const int oc = k0 + m - (kLanes - 1);
-                        if (oc >= 0 && oc < L) {
-                            const int slot = oc & (kLanes - 1);
-                            const uint32_t vh = __builtin_amdgcn_readlane(hl, kLanes - 1);
-                            const uint32_t vf = LIN ? 0u : __builtin_amdgcn_readlane(fl, kLanes - 1);
-                            out_h = lane == slot ? vh : out_h;
-                            if constexpr (!LIN) out_f = lane == slot ? vf : out_f;
-                            if (slot == kLanes - 1 || oc == L - 1) {
-                                const int col = (oc & ~(kLanes - 1)) + lane;
-                                if (col <= oc) {
-                                    if constexpr (PIPE) {
-                                        ring_out_h[col & (kPipeRing - 1)] = out_h;
-                                        if constexpr (!LIN) ring_out_f[col & (kPipeRing - 1)] = out_f;
-                                    } else {
-                                        bnd_h[col] = out_h;
-                                        if constexpr (!LIN) bnd_f[col] = out_f;
-                                    }
-                                }
+                        if (oc >= 0 && oc < L && is_last_lane) {
+                            if constexpr (PIPE) {
+                                ring_out_h[oc & (kPipeRing - 1)] = hl;
+                                if constexpr (!LIN) ring_out_f[oc & (kPipeRing - 1)] = fl;
+                            } else {
+                                bnd_h[oc] = hl;
+                                if constexpr (!LIN) bnd_f[oc] = fl;
                             }
                         }
                     }
