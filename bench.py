@@ -94,7 +94,8 @@ VALU_MODEL = {
 # packed cell ops incl. E's max, 0.53 v_pk_maximum3_f16 for the anti-diagonal
 # maxima, 0.25 for the rebase every 8 steps) for 2 x 64 cells, plus ~80
 # cycles of conveyor work (3 DPP moves, 3 readlanes, 2 hand-off adjusts, the
-# lane-63 collection; hipcc -S of sw_intra_x2.hip)
+# profile addresses, lane 63's boundary store; hipcc -S of sw_intra_x2.hip;
+# SQ_INSTS_VALU on C5 at RI = 16: 130 per lane-step, profiles/r02_sq/)
 for _ri in (4, 8, 12, 16):
     VALU_MODEL["sw_intra_x2<%d>" % _ri] = (_ri * (6.78 * 4.25) + 80.0) / (128 * _ri)
 MATRICES = {"blosum50": 0, "blosum62": 1}
@@ -106,7 +107,7 @@ C3_QUERIES = ["P02232", "P05013", "P14942", "P07327", "P01008", "P03435", "P4235
 # sources whose change can change the dominant kernel's HBM traffic: a stored
 # rocprofv3 --pmc measurement (pmc_traffic.json) is only reported for the
 # build it was taken on
-KERNEL_SOURCES = ["sw_inter_x2.hip", "sw_intra_x2.hip", "sw_kernels.hip", "sw_kernels.h", "sw_capi.cpp"]
+KERNEL_SOURCES = ["sw_inter_x2.hip", "sw_intra_x2.hip", "sw_intra_x2.h", "sw_kernels.hip", "sw_kernels.h", "sw_capi.cpp"]
 
 
 def log(*a):
