@@ -800,6 +800,26 @@ __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>&
 // blocks exist to fill the GPU and the widest block's latency bounds the
 // scan (sw_capi.cpp pair_blocks / pair_group).
 constexpr int kPairLag = 3;
+// Profile rows per LDS chunk in the group launches (the wave groups' passes
+// and the merged launch's single-wave blocks): 8, not the per-wave kernel's
+// 16.  These kernels hold 2 waves per SIMD (LDS and the ring buffers) and
+// the 16-row double buffer left them 148 B of register spills in the pass
+// loop; at 8 rows they spill nothing (C2 10,219 -> 10,320 GCUPS, C3
+// 10,323 -> 10,510, the 1/8 share 1.302 -> 1.309 ms per step).  -D
+// overrides for experiments; 3 waves per SIMD (SW_GROUP_WAVES_PER_EU=3)
+// does not fit: 168 registers spill 400-800 B.
+#ifndef SW_PAIR_CR
+#define SW_PAIR_CR 8
+#endif
+constexpr int kPairCR = SW_PAIR_CR;
+#ifndef SW_SINGLE_CR
+#define SW_SINGLE_CR 8
+#endif
+constexpr int kSingleCR = SW_SINGLE_CR;
+#ifndef SW_GROUP_WAVES_PER_EU
+#define SW_GROUP_WAVES_PER_EU 2
+#endif
+constexpr int kGroupWavesPerEU = SW_GROUP_WAVES_PER_EU;
 
 __device__ __forceinline__ int group_ticks(uint32_t ncols, int passes, int SG, int G) {
     if (ncols == 0 || passes <= 0) return 0;
@@ -843,7 +863,7 @@ __device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, int quad_end
     const int pwg = qwg + (npair - qend + 1) / 2;          // ... and pair workgroups
     if (MERGED && wgi >= pwg) {
         const int blk = npair + (wgi - pwg) * kWavesPerWG + wave;
-        if (blk < a.nblocks) x2s_block<R, SG, AFFINE, F16>(a, blk, lds[wave], lane);
+        if (blk < a.nblocks) x2s_block<R, SG, AFFINE, F16, kSingleCR>(a, blk, lds[wave], lane);
         return;  // workgroup-uniform branch: no barrier below is skipped by part of it
     }
     const bool quad = wgi < qwg;                           // workgroup-uniform
@@ -874,7 +894,7 @@ __device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, int quad_end
                 __syncthreads();
                 ++tick;
             }
-            x2s_pass<R, SG, AFFINE, F16, true>(a, lds[wave], ncols, base, lane, p * 2 * R, best, rin, rout, &tick);
+            x2s_pass<R, SG, AFFINE, F16, true, kPairCR>(a, lds[wave], ncols, base, lane, p * 2 * R, best, rin, rout, &tick);
         }
     }
     while (tick < tmax) {
@@ -897,7 +917,7 @@ __device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, int quad_end
 
 // G = 2: every group block by pairs; G = 4: every group block by quads.
 template <int R, int SG, bool AFFINE, bool F16, bool MERGED, int G>
-__global__ __launch_bounds__(256, 2) void sw_inter_x2p(InterArgs a) {
+__global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_inter_x2p(InterArgs a) {
     __shared__ __attribute__((aligned(16))) X2pSmem<R, SG, G> sm;
     x2p_wg<R, SG, AFFINE, F16, MERGED, G>(a, blockIdx.x, MERGED ? a.blk_first : a.nblocks, sm);
 }
@@ -925,7 +945,7 @@ constexpr int kLptPipe = 1 << 20;
 constexpr int kLptPipeRI = 2;
 
 template <int R, int SG, bool AFFINE, int RI>
-__global__ __launch_bounds__(256, 2) void sw_scan_lpt(InterArgs a, IntraArgs ia, IntraArgs ip,
+__global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(InterArgs a, IntraArgs ia, IntraArgs ip,
                                                       const int32_t* __restrict__ order) {
     using Elem = typename ix2::IntraImg<RI, true>::Elem;
     using PElem = typename ix2::IntraImg<kLptPipeRI, true>::Elem;
