@@ -458,7 +458,10 @@ def main():
     ap.add_argument("--no-gpu", action="store_true", help="c1: skip the GPU comparison")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run each step's top-K exchange on the scan's stream instead of overlapping the next scan")
-    ap.add_argument("--exchange-priority", type=int, default=0,
+    # high priority: HIP gives such streams their own hardware queues, so the
+    # exchange never shares one (in order) with the scan's main, long-subject
+    # or int16 side streams (GPU_MAX_HW_QUEUES = 4 normal-priority queues)
+    ap.add_argument("--exchange-priority", type=int, default=-1,
                     help="HIP stream priority of the exchange stream (negative = higher)")
     # the latest rocprofv3 --pmc measurement of the C2 launch (FETCH_SIZE x2 +
     # WRITE_SIZE, scripts/pmc_traffic.py); kept at the root because profiles/

@@ -210,18 +210,10 @@ struct sw_handle {
         size_t hcap = 0;
         hipEvent_t copied = nullptr;  // the staging buffer may be rewritten after this
         bool pending = false;
-        hipEvent_t used = nullptr;    // the last scan reading the device copy has finished
-                                      // (that scan's end event, owned by evpool)
-        bool used_pending = false;
     };
     static constexpr int kProfSlots = 4;
     ProfSlot prof[kProfSlots];
     int prof_next = 0;
-    ProfSlot* prof_cur = nullptr;     // the slot of the scan being enqueued
-    // profiles are copied on their own stream, so the H2D copy of the next
-    // scan's profile overlaps the running scan instead of sitting between
-    // two scans on the main stream
-    hipStream_t copy = nullptr;
     int32_t* d_scores = nullptr;  // for the synchronous sw_scan
     size_t scores_cap = 0;
     int64_t* d_topk_work = nullptr;  // device top-K workspace
@@ -695,7 +687,6 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     if (P->total > S.dcap) {
         if (S.d) {
             HIPCHECK(hipStreamSynchronize(h->stream));  // scans in flight may still read it
-            if (h->copy) HIPCHECK(hipStreamSynchronize(h->copy));
             HIPCHECK(hipFree(S.d));
         }
         S.dcap = std::max<size_t>(P->total, 1 << 16);
@@ -727,15 +718,13 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
                     for (int r = 0; r < rip; ++r) d[r] = static_cast<int8_t>(r < ri ? value(c, ch * CH + t * ri + r) : 0);
                 }
     }
-    // the device copy is rewritten once the scan that last read it is done;
-    // the scan waits for the copy
-    HIPCHECK(ensure_stream(h->copy));
-    if (S.used_pending) HIPCHECK(hipStreamWaitEvent(h->copy, S.used, 0));
-    HIPCHECK(hipMemcpyAsync(S.d, hp, P->total, hipMemcpyHostToDevice, h->copy));
-    HIPCHECK(hipEventRecord(S.copied, h->copy));
-    HIPCHECK(hipStreamWaitEvent(h->stream, S.copied, 0));
+    // on the scan's stream: after the scans before it (the slot's last
+    // reader among them), before this one.  (A copy stream of its own, to
+    // overlap the copy with the running scan, measured no faster and costs
+    // a hardware queue: see sw_create.)
+    HIPCHECK(hipMemcpyAsync(S.d, hp, P->total, hipMemcpyHostToDevice, h->stream));
+    HIPCHECK(hipEventRecord(S.copied, h->stream));
     S.pending = true;
-    h->prof_cur = &S;
     return SW_OK;
 }
 
@@ -1428,11 +1417,6 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     if (!lpt) MARK(2, h->stream);
     if (db->nlong && !lpt) HIPCHECK(hipStreamWaitEvent(h->stream, h->ev[1], 0));
     MARK(3, h->stream);
-    if (h->prof_cur) {  // the profile slot's device copy may be rewritten after this scan
-        h->prof_cur->used = h->ev[3];
-        h->prof_cur->used_pending = true;
-        h->prof_cur = nullptr;
-    }
     h->evpool[h->nscans - 1].launches = h->launches;
     h->timed = true;
     if (std::getenv("SW_RESCUE_STATS")) {  // diagnostics: what the guard bands flagged (synchronises)
@@ -1548,9 +1532,15 @@ int sw_create(int32_t device, sw_handle** out) {
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete h; return fail(SW_E_HIP, hipGetErrorString(e)); }
     h->own_stream = true;
-    // side, side2 and copy are created on first use: HIP maps streams onto a
-    // few hardware queues (GPU_MAX_HW_QUEUES), and two streams sharing one
-    // run in order, so a handle that never needs them should not hold them
+    // side and side2 are created with the handle, right after its own
+    // stream: HIP maps normal-priority streams onto GPU_MAX_HW_QUEUES (4)
+    // hardware queues, least-used first, and two streams sharing a queue run
+    // in order.  Created here they take the queues beside the own stream.
+    // Created on first use instead, side2 shared the caller's queue
+    // and the int16 launch beside the fp16 one ran after it (C3 under the
+    // reference scoring 12,840 -> 8,900 GCUPS).
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side2, hipStreamNonBlocking);
     for (auto& S : h->prof)
         if (e == hipSuccess) e = hipEventCreateWithFlags(&S.copied, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->coop_done, hipEventDisableTiming);
@@ -1569,7 +1559,6 @@ int sw_destroy(sw_handle* h) {
             if (ev) (void)hipEventDestroy(ev);
     if (h->side) (void)hipStreamSynchronize(h->side);
     if (h->side2) (void)hipStreamSynchronize(h->side2);
-    if (h->copy) (void)hipStreamSynchronize(h->copy);
     for (auto& S : h->prof) {
         if (S.d) (void)hipFree(S.d);
         if (S.h) (void)hipHostFree(S.h);
@@ -1579,7 +1568,6 @@ int sw_destroy(sw_handle* h) {
     if (h->d_topk_work) (void)hipFree(h->d_topk_work);
     if (h->side) (void)hipStreamDestroy(h->side);
     if (h->side2) (void)hipStreamDestroy(h->side2);
-    if (h->copy) (void)hipStreamDestroy(h->copy);
     if (h->coop_done) (void)hipEventDestroy(h->coop_done);
     if (h->fork2) (void)hipEventDestroy(h->fork2);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
