@@ -1,5 +1,7 @@
 # Round 2: bisect the C3 reference-scoring slowdown (12,941 -> 8,900 GCUPS)
-# over two earlier builds (git worktrees under .bisect/, built here).
+# over earlier builds: for each commit C in $BISECT, first (on the CPU side)
+#   git worktree add .bisect/C C && make -C .bisect/C/ece1782-smith-waterman-cuda_amd/csrc
+# (.bisect/ is excluded from git; the built trees travel with gpurun).
 set -o pipefail
 export TMPDIR=/tmp
 O=$PWD/gpurun_out/${RUN:-r02z}
