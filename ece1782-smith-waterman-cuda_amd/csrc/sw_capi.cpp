@@ -54,9 +54,6 @@ int fail(int code, const std::string& msg) {
         *h->ev_rec |= 1u << (k);                    \
     } while (0)
 
-hipError_t ensure_stream(hipStream_t& s) {
-    return s ? hipSuccess : hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-}
 
 #define HIPCHECK(expr)                                                                  \
     do {                                                                                \
@@ -1150,10 +1147,6 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // the main stream after it (only the rescue stages are left to run)
     const char* iser = std::getenv("SW_INTRA_SERIAL");
     hipStream_t is = (lpt || (iser && iser[0] == '1')) ? h->stream : h->side;
-    if (db->nlong && is != h->stream) {
-        HIPCHECK(ensure_stream(h->side));
-        is = h->side;
-    }
     swk::IntraArgs lpt_intra{};
     // the long subjects' kernels: all of them, or (lpt_done) those after the
     // fp16 pass the merged launch ran
@@ -1284,7 +1277,6 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             swk::InterArgs c = a;
             c.qpad = qpad_coop;
             c.prof = P.dev + P.off8;  // the coop kernel reads the int8 profile
-            HIPCHECK(ensure_stream(h->side2));
             HIPCHECK(hipStreamWaitEvent(h->side2, h->ev[0], 0));
             MARK(4, h->side2);
             HIPCHECK(swk::launch_inter_coop(c, ncoop, affine, h->side2));
@@ -1297,7 +1289,6 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             // (after the list counters above are reset: they share listA)
             swk::InterArgs c = a;
             c.nblocks = npair;
-            HIPCHECK(ensure_stream(h->side2));
             HIPCHECK(hipEventRecord(h->fork2, h->stream));
             HIPCHECK(hipStreamWaitEvent(h->side2, h->fork2, 0));
             MARK(4, h->side2);
@@ -1315,7 +1306,6 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             c.rescue_list = listB + 1;
             c.rescue_count = listB;
             c.rescue_max = nullptr;
-            HIPCHECK(ensure_stream(h->side2));
             HIPCHECK(hipEventRecord(h->fork2, h->stream));
             HIPCHECK(hipStreamWaitEvent(h->side2, h->fork2, 0));
             MARK(4, h->side2);
