@@ -435,7 +435,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"],
                     help="c2 = the headline (BASELINE configs[1]); c1 / c3 / c4 / c5 = configs[0] / [2] / [3] / [4]")
     ap.add_argument("--steps", type=int, default=None, help="default 100 (c2, c5) / 3 (c3, c4)")
-    ap.add_argument("--warmup", type=int, default=None, help="default 5 (c2, c5) / 1 (c3, c4)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 20 (c2, c5) / 1 (c3, c4)")
     ap.add_argument("--db-seqs", type=int, default=None,
                     help="subjects of the WHOLE database (default 570000; c1: 1000; c4: 50M; c5: 10000)")
     ap.add_argument("--shard-of", type=int, default=0,
@@ -476,7 +476,10 @@ def main():
     if args.steps is None:
         args.steps = 3 if args.config in ("c3", "c4") else 100
     if args.warmup is None:
-        args.warmup = 1 if args.config in ("c3", "c4") else 5
+        # 20 short steps (a 1/8 share's step is ~1.3 ms): the first ~0.1 s of
+        # back-to-back scans on a GPU that was idle ran up to 5 % slower
+        # (scripts/gpu_r02_thr.sh, the first of two identical runs)
+        args.warmup = 1 if args.config in ("c3", "c4") else 20
     if args.db_seqs is None:
         args.db_seqs = {"c5": 10000, "c4": C4_TOTAL}.get(args.config, 570000)
 
