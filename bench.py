@@ -264,22 +264,31 @@ def verify(sw, dist, world, rank, queries, sampler, n, gids, gpu_scores, dev_top
     of the per-rank CPU top-K of the GPU scores."""
     nq = len(queries)
     qtot = sum(len(q) for q in queries)
-    ok_topk = all(np.array_equal(dev_top[k], sw.dist.local_topk(gpu_scores[k], gids, K)) for k in range(nq))
+    # the device top-K is always K long, padded with INT64_MIN past a short share
+    ok_topk = all(np.array_equal(dev_top[k], _pad_keys(sw.dist.local_topk(gpu_scores[k], gids, K), K))
+                  for k in range(nq))
     # the rank's top-K hits (local indices) are always re-scored
     pos = {int(g): i for i, g in enumerate(gids)} if len(gids) else {}
     hit_local = set()
     for k in range(nq):
         ids, _ = sw.capi.decode_keys(dev_top[k])
         hit_local.update(pos[int(g)] for g in ids if g >= 0)
-    # estimate the oracle's rate from a small calibration sample
+    # estimate the oracle's rate from a calibration sample grown until it
+    # takes >= 0.5 s (thread start-up dominates tiny samples and made the
+    # estimate ~2x low: whole shares that fit the budget were only sampled)
     rng = np.random.default_rng(1782 + rank)
     perm = rng.permutation(n)
     m0 = min(n, 256)
-    cal = np.sort(perm[:m0])
-    sr, so = sampler(cal)
-    t = time.perf_counter()
-    oracle_scan(queries, sr, so, scoring, threads)
-    rate = qtot * int(so[-1]) / max(time.perf_counter() - t, 1e-4)
+    while True:
+        cal = np.sort(perm[:m0])
+        sr, so = sampler(cal)
+        t = time.perf_counter()
+        oracle_scan(queries, sr, so, scoring, threads)
+        dt_cal = time.perf_counter() - t
+        if dt_cal >= 0.5 or m0 >= n:
+            break
+        m0 = min(n, m0 * 4)
+    rate = qtot * int(so[-1]) / max(dt_cal, 1e-4)
     res_total = None
     try:
         _, offs = sampler.full
@@ -429,6 +438,50 @@ def make_workload(sw, args, world, rank):
     return qs, names, r_res, r_offs, gids, desc, (res, offs)
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` started without a torchrun environment: start N
+    ranks as ONE child process (`python -m torch.distributed.run`, one rank per
+    GPU, rendezvous on 127.0.0.1), relay rank 0's single JSON line and return
+    the child's exit code.  Runs before anything in this process touches HIP
+    (torch is not even imported here) and never replaces this process."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    log("starting %d ranks: %s" % (n, " ".join(cmd)))
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, cwd=REPO)
+    lines = []
+    for line in proc.stdout:
+        s = line.strip()
+        if s.startswith("{") and '"metric"' in s:
+            lines.append(s)
+        elif s:
+            print(s, file=sys.stderr, flush=True)
+    rc = proc.wait()
+    if rc == 0 and len(lines) != 1:
+        log("expected one JSON line from rank 0, got %d" % len(lines))
+        rc = 1
+    if lines:
+        print(lines[-1], flush=True)
+    return rc
+
+
+def check_world(gpus, env):
+    """Return the WORLD_SIZE to run with, or raise SystemExit when it
+    disagrees with --gpus (a silent one-rank measurement would be reported as
+    an N-GPU number)."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d: refusing to measure a different number of ranks "
+                         "than asked (start without WORLD_SIZE to let bench.py launch the ranks)" % (gpus, world))
+    return world
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -473,6 +526,12 @@ def main():
     args = ap.parse_args()
     if args.config == "c1":
         return c1_main(args)
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if args.shard_of:
+            raise SystemExit("--shard-of is a one-process rehearsal")
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     if args.steps is None:
         args.steps = 3 if args.config in ("c3", "c4") else 100
     if args.warmup is None:
@@ -486,12 +545,10 @@ def main():
     import torch
     import torch.distributed as tdist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = check_world(args.gpus, os.environ)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    if world != args.gpus:
-        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     # the database is split over shard_world ranks; this process scans share
     # shard_rank (= its rank, or the rehearsed one with --shard-of)
     shard_world, shard_rank = (args.shard_of, args.shard_rank) if args.shard_of else (world, rank)

@@ -175,6 +175,7 @@ struct ScanEvents {
                        // falls back for the others: each record is a packet
                        // the command processor spends microseconds on)
     int launches = 0;
+    bool merged = false;  // one merged launch (sw_scan_lpt): ev6..ev7 is the whole scan's fp16 pass
 };
 
 struct sw_handle {
@@ -280,6 +281,7 @@ struct sw_db {
     std::vector<SpanObs> i16_span;
     int32_t last_i16_span = 0;
     uint64_t* h_trace = nullptr;         // SW_TRACE_FILE: host-mapped block timeline
+    size_t trace_entries = 0;            // ... its entries: per block, then per merged-launch workgroup
     std::vector<uint32_t> h_blk_groups;  // block widths (16-column groups), widest first
     std::vector<int64_t> h_blk_res;      // unpadded residues per block
     int32_t last_ncoop = 0;              // blocks the last scan gave the coop kernel
@@ -288,7 +290,7 @@ struct sw_db {
     std::vector<int32_t> h_llen;         // long subjects' lengths, longest first
     // sw_scan_lpt work tables (longest first), per scan shape
     struct LptTable {
-        int32_t qpad, qpad_intra, ri, npair, group /* quad blocks */, npipe, qpad_pipe, n;
+        int32_t qpad, qpad_intra, ri, npair, group /* quad blocks */, n;
         int32_t* d_order;
         std::vector<float> cost;  // estimated duration of each entry, longest first
     };
@@ -369,6 +371,9 @@ void free_dev(sw_db* db) {
     db->d_lrescue = nullptr;
     for (auto& t : db->lpt_tables) (void)hipFree(t.d_order);
     db->lpt_tables.clear();
+    if (db->h_trace) (void)hipHostFree(db->h_trace);  // sized for this block layout
+    db->h_trace = nullptr;
+    db->trace_entries = 0;
     db->lcount_pending = false;
     db->lcount_seen = false;
     db->i16_first.clear();  // the long partition may change
@@ -817,43 +822,12 @@ double group_ticks_host(int64_t ncols, int passes, int G) {
 }
 
 // The work table of sw_scan_lpt for this scan shape (built once, cached).
-// The longest subject pairs can run pipelined over a whole workgroup (ix2
-// PIPE): pairs whose longer subject has at least kPipeFrac x the long
-// threshold residues, when the query spans 2..4 chunks of 64 x
-// lpt_pipe_rows() rows (SW_PIPE_LEN=n: at least n residues; 0: none).
-// Measured slower on C2's 1/8 share (profiles/r02_strong/pipe/: 1.37 ms
-// without, 1.56 with pairs >= 2 x the threshold, 1.57 with only pairs >=
-// 4,000 residues), so it is off unless SW_PIPE_LEN asks for it.
-constexpr double kPipeFrac = 0.0;
-
-int32_t lpt_pipe_pairs(const sw_db* db, int32_t qlen) {
-    const int64_t ch = static_cast<int64_t>(swk::kLanes) * swk::lpt_pipe_rows();
-    const int64_t nch = (qlen + ch - 1) / ch;
-    if (nch < 2 || nch > swk::kWavesPerWG) return 0;
-    int64_t lmin = static_cast<int64_t>(kPipeFrac * db->long_threshold);
-    if (const char* e = std::getenv("SW_PIPE_LEN")) lmin = std::atoll(e);
-    if (lmin <= 0) return 0;
-    int64_t k = 0;  // subjects (longest first) at least lmin long, in whole pairs
-    while (k < db->nlong && db->h_llen[static_cast<size_t>(k)] >= lmin) ++k;
-    return static_cast<int32_t>((k + 1) / 2);
-}
-
-// Workgroups whose estimated duration is at least kPrioFrac x the longest
-// raise their wave priority (SW_LPT_PRIO=f overrides the fraction; 0: off).
-constexpr double kPrioFrac = 0.0;
-
-int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad, int32_t npipe,
-              int32_t qpad_pipe, const int32_t** order, int* n, int* nprio) {
-    double pf = kPrioFrac;
-    if (const char* e = std::getenv("SW_LPT_PRIO")) pf = std::atof(e);
+int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad,
+              const int32_t** order, int* n) {
     for (const auto& t : db->lpt_tables)
-        if (t.qpad == qpad && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad &&
-            t.npipe == npipe && t.qpad_pipe == qpad_pipe) {
+        if (t.qpad == qpad && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad) {
             *order = t.d_order;
             *n = t.n;
-            *nprio = 0;
-            if (pf > 0)
-                while (*nprio < t.n && t.cost[static_cast<size_t>(*nprio)] >= pf * t.cost[0]) ++*nprio;
             return SW_OK;
         }
     const int passes = qpad / 64;
@@ -861,9 +835,7 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     const int64_t pwg = nquad + (npair - nquad + 1) / 2;
     const int64_t swg = (nb - npair + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
     const int64_t npairs = (db->nlong + 1) / 2;
-    const int64_t iwg = (npairs - npipe + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
-    const int rp = swk::lpt_pipe_rows();
-    const int pch = qpad_pipe / (swk::kLanes * rp);
+    const int64_t iwg = (npairs + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
     const int nch = qpad_intra / (swk::kLanes * ri);
     std::vector<std::pair<double, int32_t>> w;
     w.reserve(static_cast<size_t>(pwg + swg + iwg));
@@ -881,14 +853,8 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
         w.emplace_back(single_ticks(width(npair + g * swk::kWavesPerWG), passes) * kTickUs,
                        static_cast<int32_t>(pwg + g));
     for (int64_t g = 0; g < iwg; ++g)
-        w.emplace_back((db->h_llen[static_cast<size_t>(2 * npipe + 8 * g)] + swk::kLanes - 1) * nch * intra_step_us(ri),
+        w.emplace_back((db->h_llen[static_cast<size_t>(8 * g)] + swk::kLanes - 1) * nch * intra_step_us(ri),
                        static_cast<int32_t>(-1 - g));
-    double pipe_cost = 1.0;  // SW_PIPE_COST: scale of the pipelined pairs' estimate (ordering A/B)
-    if (const char* e = std::getenv("SW_PIPE_COST")) pipe_cost = std::atof(e);
-    for (int64_t q = 0; q < npipe; ++q)
-        w.emplace_back(pipe_cost * (db->h_llen[static_cast<size_t>(2 * q)] + swk::kLanes - 1 + 128.0 * (pch - 1)) *
-                           intra_step_us(rp),
-                       static_cast<int32_t>(-swk::lpt_pipe_item() - q));
     std::stable_sort(w.begin(), w.end(), [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) {
         return x.first > y.first;
     });
@@ -898,8 +864,7 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
         ord[k] = w[k].second;
         cost[k] = static_cast<float>(w[k].first);
     }
-    sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, npipe, qpad_pipe, static_cast<int32_t>(ord.size()), nullptr,
-                      cost};
+    sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, static_cast<int32_t>(ord.size()), nullptr, cost};
     HIPCHECK(hipMalloc(reinterpret_cast<void**>(&t.d_order), ord.size() * sizeof(int32_t)));
     HIPCHECK(hipMemcpy(t.d_order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     db->device_bytes += ord.size() * sizeof(int32_t);
@@ -910,9 +875,6 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     db->lpt_tables.push_back(t);
     *order = t.d_order;
     *n = t.n;
-    *nprio = 0;
-    if (pf > 0)
-        while (*nprio < t.n && cost[static_cast<size_t>(*nprio)] >= pf * cost[0]) ++*nprio;
     return SW_OK;
 }
 
@@ -927,6 +889,7 @@ int next_events(sw_handle* h) {
     h->ev_rec = &h->evpool[h->nscans].rec;
     *h->ev_rec = 0;
     h->evpool[h->nscans].launches = 0;
+    h->evpool[h->nscans].merged = false;
     ++h->nscans;
     return SW_OK;
 }
@@ -1057,9 +1020,6 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     }
     i16_span = static_cast<int32_t>(std::min<int64_t>(std::max(i16_span, 0), db->nblocks));
     const int32_t qpad_intra2 = ri2 ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri2)) : 0;
-    // the merged launch's pipelined pairs (see lpt_pipe_pairs)
-    const int32_t qpad_pipe =
-        intra_x2 ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * swk::lpt_pipe_rows())) : 0;
     // Empty query: every score is 0 (the reference's kernel leaves maxScore 0).
     if (qlen == 0) {
         db->last_ncoop = 0;
@@ -1086,17 +1046,14 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // two-strips scans: the widest blocks by wave pairs (at least two passes)
     const int32_t npair =
         (db->nblocks && swk::inter_has_pair(affine, x2_ok) && qpad_inter > R) ? pair_blocks(db) : 0;
-    // pairs and single waves in one launch (default) or two concurrent ones
-    const char* pm = std::getenv("SW_PAIR_MERGED");
-    const bool pair_merged = !(pm && pm[0] == '0');
     const int32_t ncoop =
         (!npair && db->nblocks) ? coop_blocks(db, swk::inter_coop_divisor(affine, x2_ok)) : 0;
     db->last_ncoop = ncoop;
     db->last_npair = npair;
-    db->last_pair_merged = npair && pair_merged;
+    db->last_pair_merged = npair != 0;
     const int32_t qpad_coop = ncoop ? static_cast<int32_t>(round_up(qlen, swk::inter_coop_rows())) : 0;
     if ((rc = build_profiles(h, query, qlen, mat, go, affine,
-                             std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2, qpad_pipe}),
+                             std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2}),
                              x2 || intra_x2, ri, qpad_intra, &P)))
         return rc;
     if (rescue && db->nblocks && !db->d_rescue) {
@@ -1135,18 +1092,17 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     const char* lpt_env = std::getenv("SW_LPT");
     const bool lpt_want = lpt_env ? lpt_env[0] == '1' : static_cast<double>(db->n) < 0.35 * kFillSubjects;
     const bool lpt = lpt_want && db->nlong && db->nblocks && intra_x2 && !intra_i16_first &&
-                     f16 && rescue && npair && pair_merged && !ncoop && i16_span == 0 &&
+                     f16 && rescue && npair && !ncoop && i16_span == 0 &&
                      swk::lpt_supported(ri2);
     db->last_lpt = lpt;
+    h->evpool[h->nscans - 1].merged = lpt;
     // fork: the side stream starts when the main stream reaches ev[0]
     MARK(0, h->stream);
     h->last_intra = "none";
     // the long subjects' stream: a side stream, concurrent with the inter
-    // kernels (SW_INTRA_SERIAL=1: the main stream, before them — to measure
-    // what the concurrency costs the inter kernel); with the merged launch,
-    // the main stream after it (only the rescue stages are left to run)
-    const char* iser = std::getenv("SW_INTRA_SERIAL");
-    hipStream_t is = (lpt || (iser && iser[0] == '1')) ? h->stream : h->side;
+    // kernels; with the merged launch, the main stream after it (only the
+    // rescue stages are left to run)
+    hipStream_t is = lpt ? h->stream : h->side;
     swk::IntraArgs lpt_intra{};
     // the long subjects' kernels: all of them, or (lpt_done) those after the
     // fp16 pass the merged launch ran
@@ -1247,11 +1203,13 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         a.bnd_f = db->d_bnd_f;
         a.scores = scores_dev;
         if (std::getenv("SW_TRACE_FILE")) {
-            if (!db->h_trace)
-            {
-                HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&db->h_trace), 32 * (db->nblocks + db->nlong + 8),
+            if (!db->h_trace) {
+                // one entry per block, then one per workgroup of a merged
+                // launch (at most nblocks inter + nlong / 8 intra workgroups)
+                db->trace_entries = static_cast<size_t>(2 * db->nblocks + db->nlong + 8);
+                HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&db->h_trace), 32 * db->trace_entries,
                                        hipHostMallocMapped));
-                std::memset(db->h_trace, 0, 32 * (db->nblocks + db->nlong + 8));
+                std::memset(db->h_trace, 0, 32 * db->trace_entries);
             }
             HIPCHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.trace), db->h_trace, 0));
         }
@@ -1259,7 +1217,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         int32_t* listB = db->d_rescue ? db->d_rescue + db->nblocks + 1 : nullptr;
         int32_t* maxA = db->d_rescue ? db->d_rescue + 2 * (db->nblocks + 1) : nullptr;
         // the widest blocks the int16 kernel takes first (see i16_span)
-        const int32_t nr = (f16 && rescue && npair && pair_merged && !ncoop) ? i16_span : 0;
+        const int32_t nr = (f16 && rescue && npair && !ncoop) ? i16_span : 0;
         db->last_i16_span = nr;
         if (rescue) {
             a.rescue_count = listA;
@@ -1284,19 +1242,6 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             HIPCHECK(hipEventRecord(h->coop_done, h->side2));
             ++h->launches;
             a.blk_first = ncoop;
-        } else if (npair && !pair_merged) {
-            // the widest blocks by wave pairs, beside the per-wave kernel
-            // (after the list counters above are reset: they share listA)
-            swk::InterArgs c = a;
-            c.nblocks = npair;
-            HIPCHECK(hipEventRecord(h->fork2, h->stream));
-            HIPCHECK(hipStreamWaitEvent(h->side2, h->fork2, 0));
-            MARK(4, h->side2);
-            HIPCHECK(swk::launch_inter_x2p(c, affine, f16, false, pair_group(db), h->side2));
-            MARK(5, h->side2);
-            HIPCHECK(hipEventRecord(h->coop_done, h->side2));
-            ++h->launches;
-            a.blk_first = npair;
         } else if (nr) {
             // blocks [0, nr) in int16 by wave pairs beside the fp16 launch;
             // their near-32767 ones go to list B (the int32 stage)
@@ -1324,21 +1269,12 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             const int32_t* order = nullptr;
             int nwg = 0;
             const int32_t nquad = lpt_quad_blocks(db, npair);
-            const int32_t npipe = lpt_pipe_pairs(db, qlen);
             a.blk_quad = nquad;
-            swk::IntraArgs ip = lpt_intra;  // the pipelined longest pairs
-            ip.qpad = qpad_pipe;
-            ip.pair_base = 0;
-            lpt_intra.pair_base = npipe;
-            int nprio = 0;
-            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, npipe, qpad_pipe, &order, &nwg,
-                                &nprio)))
-                return rc;
-            a.lpt_prio = nprio;
-            HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, ip, order, nwg, affine, ri2, h->stream));
+            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, &order, &nwg))) return rc;
+            HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, order, nwg, affine, ri2, h->stream));
             MARK(7, h->stream);
             if ((rc = launch_long(true))) return rc;
-        } else if (npair && pair_merged) {
+        } else if (npair) {
             // one launch: pairs for blocks [nr, npair), one wave per block after
             a.blk_base = nr;
             a.blk_first = std::max(npair, nr);
@@ -1352,7 +1288,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         if (lpt) h->last_kernel += "+lpt";
         if (!lpt) MARK(7, h->stream);
         ++h->launches;
-        if (ncoop || (npair && !pair_merged) || nr) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
+        if (ncoop || nr) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
         const bool seen = db->icount_seen && db->seen_key == skey && db->seen_qhash == qhash &&
                           db->seen_qlen == qlen && db->seen_nr == nr;
         if (f16 && rescue && !db->icount_pending && !seen) {
@@ -1780,10 +1716,9 @@ int sw_db_free(sw_db* db) {
     if (db->h_trace) {  // the last scan's block timeline (tail analysis builds)
         if (const char* path = std::getenv("SW_TRACE_FILE"))
             if (FILE* f = std::fopen(path, "wb")) {
-                std::fwrite(db->h_trace, 32, static_cast<size_t>(db->nblocks + db->nlong + 8), f);
+                std::fwrite(db->h_trace, 32, db->trace_entries, f);
                 std::fclose(f);
             }
-        (void)hipHostFree(db->h_trace);
     }
     if (db->h_lcount) (void)hipHostFree(db->h_lcount);
     if (db->lcount_ev) (void)hipEventDestroy(db->lcount_ev);
@@ -1914,6 +1849,10 @@ int read_events(const ScanEvents& se, sw_timing* t) {
     float t45 = 0, t67 = 0;
     if (has(4) && has(5)) HIPCHECK(hipEventElapsedTime(&t45, se.ev[4], se.ev[5]));
     if (has(6) && has(7)) HIPCHECK(hipEventElapsedTime(&t67, se.ev[6], se.ev[7]));
+    if (se.merged) {  // the merged launch: no separate intra span
+        t01 = 0;
+        t02 = t67;
+    }
     t->intra_ms += t01;
     t->inter_ms += t02;
     t->total_ms += t03;

@@ -17,10 +17,14 @@
 //
 // RCCL is loaded at run time (dlopen of librccl.so.1: the one already in the
 // process, e.g. PyTorch's, or /opt/rocm's), so the library has no link-time
-// RCCL dependency.  A group that names one device twice (tests on a one-GPU
-// box) cannot form an RCCL communicator; its exchange goes through the host
-// instead (same keys, same merge kernel) and sw_group_info says so.  A group
-// of one device runs the RCCL path with a one-rank communicator.
+// RCCL dependency, and only when the first sw_group_topk needs it: creating a
+// group and sw_group_scan (the drop-in's full result vector, no collective)
+// never touch RCCL.  A group that names one device twice (tests on a one-GPU
+// box) cannot form an RCCL communicator, and a process where librccl cannot
+// be loaded or ncclCommInitAll fails falls back the same way: the exchange
+// goes through the host (same keys, same merge kernel) and sw_group_info says
+// which path ran and why.  A group of one device runs the RCCL path with a
+// one-rank communicator.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -106,6 +110,8 @@ struct sw_group {
     std::vector<int32_t> devices;
     std::vector<sw_handle*> h;
     std::vector<ncclComm_t> comms;  // empty: host exchange
+    bool distinct = false;          // every device listed once: RCCL possible
+    bool comm_tried = false;        // communicators created (or failed) already
     // per device: K local keys, G x K gathered keys, capacity in keys
     std::vector<int64_t*> d_keys, d_all;
     int32_t kcap = 0;
@@ -142,6 +148,29 @@ int ensure_keys(sw_group* g, int32_t k) {
     return SW_OK;
 }
 
+// The exchange path, decided at the first top-K: one RCCL communicator per
+// device (ncclCommInitAll) when the devices are distinct and RCCL loads and
+// initialises, else the host exchange.
+void ensure_comms(sw_group* g) {
+    if (g->comm_tried) return;
+    g->comm_tried = true;
+    const int ndev = static_cast<int>(g->devices.size());
+    if (!g->distinct) return;
+    std::string why;
+    if (!rccl().load(&why)) {
+        g->exchange = "host (" + why + ")";
+        return;
+    }
+    g->comms.assign(ndev, nullptr);
+    const ncclResult_t r = rccl().init_all(g->comms.data(), ndev, g->devices.data());
+    if (r != ncclSuccess) {
+        g->comms.clear();
+        g->exchange = std::string("host (ncclCommInitAll failed: ") + rccl().error_string(r) + ")";
+        return;
+    }
+    g->exchange = "rccl allgather (" + std::to_string(ndev) + (ndev == 1 ? " rank)" : " ranks)");
+}
+
 }  // namespace
 
 extern "C" {
@@ -165,24 +194,9 @@ int sw_group_create(const int32_t* devices, int32_t ndev, sw_group** out) {
     }
     std::vector<int32_t> sorted(g->devices);
     std::sort(sorted.begin(), sorted.end());
-    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-    if (!distinct) {
-        g->exchange = "host (a device appears twice: no RCCL communicator)";
-    } else {
-        std::string why;
-        if (!rccl().load(&why)) {
-            sw_group_destroy(g);
-            return gfail(SW_E_UNSUPPORTED, why);
-        }
-        g->comms.assign(ndev, nullptr);
-        const ncclResult_t r = rccl().init_all(g->comms.data(), ndev, g->devices.data());
-        if (r != ncclSuccess) {
-            g->comms.clear();
-            sw_group_destroy(g);
-            return gfail(SW_E_HIP, std::string("ncclCommInitAll: ") + rccl().error_string(r));
-        }
-        g->exchange = "rccl allgather (" + std::to_string(ndev) + (ndev == 1 ? " rank)" : " ranks)");
-    }
+    g->distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    g->exchange = g->distinct ? "rccl allgather (communicators created by the first top-K)"
+                              : "host (a device appears twice: no RCCL communicator)";
     *out = g;
     return SW_OK;
 }
@@ -330,6 +344,7 @@ int sw_group_topk(sw_group* g, const sw_gdb* gd, const uint8_t* query, int32_t q
     });
     if (rc) return rc;
     // 2. exchange: every device receives all G x k keys
+    ensure_comms(g);
     if (!g->comms.empty()) {
         ncclResult_t r = rccl().group_start();
         for (int d = 0; d < G && r == ncclSuccess; ++d) {

@@ -938,59 +938,39 @@ __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_inter_x2p(InterArgs 
 // so the dispatcher starts the longest work first and fills the end with
 // the shortest (LPT).  LDS: the two kinds' buffers overlap (a workgroup is
 // one kind), so the occupancy stays the inter kernel's 2 workgroups per CU.
-// Items <= -kLptPipe: pipelined intra workgroups (one subject pair over the
-// four waves, kLptPipeRI rows per lane: ix2::intra_x2_wg<..., PIPE>), the
-// longest pairs (ip); -kLptPipe < item < 0: ordinary intra workgroups (ia).
-constexpr int kLptPipe = 1 << 20;
-constexpr int kLptPipeRI = 2;
-
 template <int R, int SG, bool AFFINE, int RI>
-__global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(InterArgs a, IntraArgs ia, IntraArgs ip,
-                                                      const int32_t* __restrict__ order) {
+__global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(InterArgs a, IntraArgs ia,
+                                                                     const int32_t* __restrict__ order) {
     using Elem = typename ix2::IntraImg<RI, true>::Elem;
-    using PElem = typename ix2::IntraImg<kLptPipeRI, true>::Elem;
     constexpr size_t kInter = sizeof(X2pSmem<R, SG, 4>);
     constexpr size_t kIntra = sizeof(Elem) * ix2::img_elems<RI, true>();
-    constexpr size_t kPipeImg = sizeof(PElem) * ix2::img_elems<kLptPipeRI, true>() * kWavesPerWG;
-    constexpr size_t kPipe = kPipeImg + 4 * ix2::kPipeLdsWords;
-    constexpr size_t kMax = kInter > kIntra ? (kInter > kPipe ? kInter : kPipe) : (kIntra > kPipe ? kIntra : kPipe);
-    __shared__ __attribute__((aligned(16))) char smem[kMax];
+    __shared__ __attribute__((aligned(16))) char smem[kInter > kIntra ? kInter : kIntra];
     const int item = order[blockIdx.x];
     const uint64_t t0 = trace_now();
-    // the longest work (the launch's critical path) wins the SIMDs' issue
-    // arbitration against the shorter work sharing them
-    if (static_cast<int>(blockIdx.x) < a.lpt_prio) __builtin_amdgcn_s_setprio(2);
     if (item >= 0)
         x2p_wg<R, SG, AFFINE, true, true, 4>(a, item, a.blk_quad, *reinterpret_cast<X2pSmem<R, SG, 4>*>(smem));
-    else if (item > -kLptPipe)
-        ix2::intra_x2_wg<RI, true, false, false, !AFFINE>(ia, -1 - item, reinterpret_cast<Elem*>(smem));
     else
-        ix2::intra_x2_wg<kLptPipeRI, true, false, true, !AFFINE>(ip, -kLptPipe - item, reinterpret_cast<PElem*>(smem),
-                                                        reinterpret_cast<uint32_t*>(smem + kPipeImg));
+        ix2::intra_x2_wg<RI, true, false, !AFFINE>(ia, -1 - item, reinterpret_cast<Elem*>(smem));
     // per-workgroup timeline (trace builds): after the per-block entries
     if (threadIdx.x == 0) trace_block(a, a.nblocks + blockIdx.x, t0, 0, item >= 0 ? 2 : 3);
 }
 
 template <int RI>
-static void launch_lpt_t(const InterArgs& a, const IntraArgs& ia, const IntraArgs& ip, const int32_t* order, int n,
-                         bool affine, hipStream_t s) {
+static void launch_lpt_t(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine,
+                         hipStream_t s) {
     if (affine) hipLaunchKernelGGL((sw_scan_lpt<32, 8, true, RI>), dim3(n), dim3(kWavesPerWG * kLanes), 0, s, a, ia,
-                                   ip, order);
-    else hipLaunchKernelGGL((sw_scan_lpt<32, 8, false, RI>), dim3(n), dim3(kWavesPerWG * kLanes), 0, s, a, ia, ip,
-                            order);
+                                   order);
+    else hipLaunchKernelGGL((sw_scan_lpt<32, 8, false, RI>), dim3(n), dim3(kWavesPerWG * kLanes), 0, s, a, ia, order);
 }
-
-int lpt_pipe_rows() { return kLptPipeRI; }
-int lpt_pipe_item() { return kLptPipe; }
 
 bool lpt_supported(int ri) { return ri == 4 || ri == 6 || ri == 8; }
 
-hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const IntraArgs& ip, const int32_t* order, int n,
-                           bool affine, int ri, hipStream_t s) {
+hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri,
+                           hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    if (ri == 4) launch_lpt_t<4>(a, ia, ip, order, n, affine, s);
-    else if (ri == 6) launch_lpt_t<6>(a, ia, ip, order, n, affine, s);
-    else if (ri == 8) launch_lpt_t<8>(a, ia, ip, order, n, affine, s);
+    if (ri == 4) launch_lpt_t<4>(a, ia, order, n, affine, s);
+    else if (ri == 6) launch_lpt_t<6>(a, ia, order, n, affine, s);
+    else if (ri == 8) launch_lpt_t<8>(a, ia, order, n, affine, s);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }

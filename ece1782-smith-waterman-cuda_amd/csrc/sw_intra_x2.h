@@ -147,29 +147,15 @@ constexpr bool kPrefetch = SW_IX2_PREFETCH != 0;
 template <int RI, bool F16>
 __host__ __device__ constexpr int img_elems() { return kCodes * IntraImg<RI, F16>::kPer * kLanes; }
 
-// PIPE (sw_scan_lpt, the longest subjects): the four waves of a workgroup
-// share ONE subject pair; wave w runs query chunk w (64 RI rows) and lags
-// wave w - 1 by kPipeLag blocks of 64 steps, receiving its bottom row (H, F)
-// through an LDS ring of kPipeRing columns instead of HBM, with one
-// workgroup barrier per block of 64 steps.  The pair's latency drops from
-// chunks x (L + 63) steps at the single-wave RI to (L + 63 + 128 (chunks-1))
-// steps at a small RI (fewer instructions per step): the longest subjects
-// of a small database stop bounding its scan.  pipe_lds: kPipeLdsWords.
-constexpr int kPipeLag = 2;     // blocks of 64 steps between consecutive chunks
-constexpr int kPipeRing = 256;  // columns per ring (>= kPipeLag + 1 blocks)
-constexpr int kPipeLdsWords = 2 * kWavesPerWG * kPipeRing + kWavesPerWG * kLanes;
-
 // One workgroup's work (wgi = its index in the launch: subject pairs
-// pair_base + 4 wgi .. + 3, one per wave; PIPE: pair pair_base + wgi);
-// img: the workgroup's LDS image (PIPE: one per wave).
+// 4 wgi .. 4 wgi + 3, one per wave); img: the workgroup's LDS image.
 // LIN (linear gaps, open == extend = g): the biased cell needs no E or F —
 // the left and up terms H - g ARE the stored neighbours (the bias grows by g
 // per row and per step), so h~ = max(max3(H~_left, H~_up, H~_diag + S + 2g),
 // floor): 2 packed ops per cell pair after the diagonal sum instead of the
 // Farrar form's 6 (the two-strips kernel's linear cell, sw_inter_x2.hip).
-template <int RI, bool F16, bool LIST, bool PIPE = false, bool LIN = false>
-__device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typename IntraImg<RI, F16>::Elem* img,
-                                            uint32_t* pipe_lds = nullptr) {
+template <int RI, bool F16, bool LIST, bool LIN = false>
+__device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typename IntraImg<RI, F16>::Elem* img) {
     static_assert(RI % 2 == 0 && RI <= 16, "rows per lane");
     constexpr int CH = kLanes * RI;  // query rows per chunk
     using C = IntraCell<F16>;
@@ -182,7 +168,7 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const bool is_last_lane = lane == kLanes - 1;
-    const int p = a.pair_base + (PIPE ? wgi : wgi * kWavesPerWG + wave);  // subject pair
+    const int p = wgi * kWavesPerWG + wave;  // subject pair
     int sa = 2 * p, sb = 2 * p + 1;
     bool hasA = sa < a.nsubj, hasB = sb < a.nsubj;
     if constexpr (LIST) {
@@ -220,31 +206,21 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
     for (int q = 0; q < NACC; ++q) acc[q] = C::from(0u);
     constexpr uint32_t kPadPair = kPadCode | (kPadCode << 8);
 
-    // PIPE: this wave's chunk, the rings from the previous wave / to the next
-    uint32_t* ring_in_h = PIPE && wave > 0 ? pipe_lds + (wave - 1) * kPipeRing : nullptr;
-    uint32_t* ring_in_f = PIPE && wave > 0 ? pipe_lds + (kWavesPerWG + wave - 1) * kPipeRing : nullptr;
-    uint32_t* ring_out_h = PIPE ? pipe_lds + wave * kPipeRing : nullptr;
-    uint32_t* ring_out_f = PIPE ? pipe_lds + (kWavesPerWG + wave) * kPipeRing : nullptr;
-    const int nloop = PIPE ? 1 : a.qpad / CH;
-    for (int ci = 0; ci < nloop; ++ci) {
-        const int c0 = (PIPE ? wave : ci) * CH;
-        const bool active = c0 < a.qpad;  // PIPE: waves past the last chunk only join the barriers
+    for (int c0 = 0; c0 < a.qpad; c0 += CH) {
         const bool first = (c0 == 0);
         const bool last = (c0 + CH >= a.qpad);
-        Elem* cimg = PIPE ? img + wave * img_elems<RI, F16>() : img;
-        if constexpr (!PIPE) __syncthreads();  // the previous chunk's LDS reads are done
+        __syncthreads();  // the previous chunk's LDS reads are done
         // stage rows [c0, c0 + CH) of codes 0..25 as fp16 S + 2 ge (the
-        // linear profile is biased by the gap, a.bias); PIPE: each wave its own
-        for (int t = PIPE ? lane : static_cast<int>(threadIdx.x); active && t < kCodes * NQ * kLanes;
-             t += PIPE ? kLanes : kWavesPerWG * kLanes) {
+        // linear profile is biased by the gap, a.bias)
+        for (int t = static_cast<int>(threadIdx.x); t < kCodes * NQ * kLanes; t += kWavesPerWG * kLanes) {
             const int code = t / (NQ * kLanes);
             const int u = t % (NQ * kLanes);
             const int qq = u / kLanes, ln = u % kLanes;
-            cimg[t] = Img::load(prof16 + static_cast<size_t>(code) * a.prof_stride + c0 + ln * RI + Img::kRows * qq,
-                                a.bias - 2 * a.gap_extend);
+            img[t] = Img::load(prof16 + static_cast<size_t>(code) * a.prof_stride + c0 + ln * RI + Img::kRows * qq,
+                               a.bias - 2 * a.gap_extend);
         }
         __syncthreads();
-        if (!hasA && !hasB) continue;  // wave-uniform (PIPE: workgroup-uniform); the barriers above are shared
+        if (!hasA && !hasB) continue;  // wave-uniform; the barriers above are shared
 
         // state of step -1 (column -1 - lane: H = 0), before step 0's rebase
         V H[RI], E[LIN ? 1 : RI];
@@ -261,7 +237,7 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
         uint32_t in_res = kPadPair, in_bh = 0, in_bf = 0;
         const int nsteps = L + kLanes - 1;
         // LDS byte address of this lane's element of code 0
-        const uint32_t lrow = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(cimg + lane));
+        const uint32_t lrow = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(img + lane));
 
         constexpr uint32_t kCodeBytes = NQ * kLanes * sizeof(Elem);
         // the profile words of code pair rcx (A | B << 8) for this lane
@@ -288,16 +264,9 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
         Elem W[2][2][NQ];
         uint32_t rc_n = 0;
 
-        // blocks of 64 steps; PIPE: every wave joins one barrier per block of
-        // the pipeline, wave w working on block it - kPipeLag w
+        // blocks of 64 steps
         const int nblk = (nsteps + kLanes - 1) / kLanes;
-        const int iters = PIPE ? nblk + kPipeLag * (kWavesPerWG - 1) : nblk;
-        for (int it = 0; it < iters; ++it) {
-            const int bk = PIPE ? it - kPipeLag * wave : it;
-            if (PIPE && !(active && bk >= 0 && bk < nblk)) {  // wave-uniform
-                __syncthreads();
-                continue;
-            }
+        for (int bk = 0; bk < nblk; ++bk) {
             const int k0 = bk * kLanes;
             // lane-0 conveyors for steps k0 .. k0+63 (column k = step); the
             // first chunk's row -1 is H = 0, F = 0 at the bias lane 0 reads
@@ -307,14 +276,8 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
                 in_res = in_res_nb;
                 in_res_nb = codes_at(col + kLanes);
                 const int bz = RI - 2 + (col % NB) + ((col % NB) == 0 ? NB : 0);
-                if constexpr (PIPE) {
-                    in_bh = (!first && col < L) ? ring_in_h[col & (kPipeRing - 1)] : C::pair_of(bz * a.gap_extend);
-                    in_bf = (!first && col < L) ? ring_in_f[col & (kPipeRing - 1)]
-                                                : C::pair_of((bz + 1) * a.gap_extend);
-                } else {
-                    in_bh = (!first && col < L) ? bnd_h[col] : C::pair_of(bz * a.gap_extend);
-                    in_bf = (!first && col < L) ? bnd_f[col] : C::pair_of((bz + 1) * a.gap_extend);
-                }
+                in_bh = (!first && col < L) ? bnd_h[col] : C::pair_of(bz * a.gap_extend);
+                in_bf = (!first && col < L) ? bnd_f[col] : C::pair_of((bz + 1) * a.gap_extend);
             }
             if (kPrefetch && k0 == 0) {
                 rc_n = shr1u(__builtin_amdgcn_readlane(in_res, 0), rc);
@@ -398,13 +361,8 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
                         // next pass itself (no per-step collection across lanes)
                         const int oc = k0 + m - (kLanes - 1);
                         if (oc >= 0 && oc < L && is_last_lane) {
-                            if constexpr (PIPE) {
-                                ring_out_h[oc & (kPipeRing - 1)] = hl;
-                                if constexpr (!LIN) ring_out_f[oc & (kPipeRing - 1)] = fl;
-                            } else {
-                                bnd_h[oc] = hl;
-                                if constexpr (!LIN) bnd_f[oc] = fl;
-                            }
+                            bnd_h[oc] = hl;
+                            if constexpr (!LIN) bnd_f[oc] = fl;
                         }
                     }
                     // pin the maxima at every step (left free, the compiler
@@ -413,7 +371,6 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
                     for (int q = 0; q < NACC; ++q) asm volatile("" : "+v"(acc[q]));
                 }
             }
-            if constexpr (PIPE) __syncthreads();  // the block's ring writes are visible to the next wave
         }
     }
     // the lane's maximum (unbiased), then the wave's
@@ -424,14 +381,6 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
     for (int off = 32; off > 0; off >>= 1) {
         const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(C::bits(best)), off));
         best = C::max2(best, C::from(o));
-    }
-    if constexpr (PIPE) {  // the chunks' maxima meet in wave 0
-        uint32_t* part = pipe_lds + 2 * kWavesPerWG * kPipeRing;
-        if (lane == 0) part[wave] = C::bits(best);
-        __syncthreads();
-        if (wave != 0) return;
-        for (int w = 1; w < kWavesPerWG; ++w)
-            if (w * CH < a.qpad) best = C::max2(best, C::from(part[w]));
     }
     if (lane == 0) {
         const int ba = C::lo(best);

@@ -10,7 +10,7 @@ namespace swk {
 template <int RI, bool F16, bool LIST, bool LIN>
 __global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
     __shared__ typename ix2::IntraImg<RI, F16>::Elem img[ix2::img_elems<RI, F16>()];
-    ix2::intra_x2_wg<RI, F16, LIST, false, LIN>(a, blockIdx.x, img);
+    ix2::intra_x2_wg<RI, F16, LIST, LIN>(a, blockIdx.x, img);
 }
 
 int intra_x2_rows_for(int qlen, int longest) {
@@ -50,12 +50,10 @@ static hipError_t launch_intra_x2_t(const IntraArgs& a, int ri, hipStream_t s) {
     return hipGetLastError();
 }
 
-// Linear gaps (open == extend) take the biased linear cell (ix2 LIN);
-// SW_INTRA_LIN=0 keeps the Farrar form for them (A/B).
-bool intra_linear(const IntraArgs& a) {
-    const char* e = std::getenv("SW_INTRA_LIN");
-    return a.gap_open == a.gap_extend && !(e && e[0] == '0');
-}
+// Linear gaps (open == extend) take the biased linear cell (ix2 LIN), as in
+// the merged launch (sw_scan_lpt); measured against the Farrar form in
+// profiles/r02_intra_lin/.
+bool intra_linear(const IntraArgs& a) { return a.gap_open == a.gap_extend; }
 
 template <bool F16, bool LIST>
 static hipError_t launch_intra_x2_g(const IntraArgs& a, int ri, hipStream_t s) {

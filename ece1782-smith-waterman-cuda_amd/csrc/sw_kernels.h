@@ -83,9 +83,6 @@ struct InterArgs {
     int32_t blk_base;
     // sw_scan_lpt: blocks [blk_base, blk_quad) run by wave quads
     int32_t blk_quad;
-    // sw_scan_lpt: workgroups [0, lpt_prio) of the (longest-first) order
-    // raise their wave priority (the critical path of a small database)
-    int32_t lpt_prio;
     // fp16 kernels: the largest flagged block id (atomicMax; nullable), read
     // back by the host to route the widest blocks to int16 next time
     int32_t* rescue_max;
@@ -122,9 +119,6 @@ struct IntraArgs {
     // sw_intra in list mode: only subjects subj_list[0 .. *list_count)
     const int32_t* subj_list = nullptr;
     const int32_t* list_count = nullptr;
-    // sw_intra_x2: subject pairs start at this one (sw_scan_lpt: the longest
-    // pairs run pipelined over whole workgroups, the rest after them)
-    int32_t pair_base = 0;
 };
 
 // Strip heights (query rows held in registers per lane) the kernels are
@@ -173,15 +167,9 @@ hipError_t launch_inter_x2p(const InterArgs& a, bool affine, bool f16, bool merg
 // [blk_quad, blk_first) by pairs), < 0 intra workgroup -1 - order[k] (ia as
 // for launch_intra_x2: 4 subject pairs per workgroup).  Intra rows per lane
 // 4, 6 or 8.
-// Items <= -lpt_pipe_item(): the longest subject pairs, one per workgroup,
-// their query chunks pipelined over its four waves (ip: lpt_pipe_rows() rows
-// per lane, qpad a multiple of 64 x that, at most 4 chunks; ia then starts
-// at ia.pair_base = the pipelined pairs).
 bool lpt_supported(int ri);
-int lpt_pipe_rows();
-int lpt_pipe_item();
-hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const IntraArgs& ip, const int32_t* order, int n,
-                           bool affine, int ri, hipStream_t s);
+hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri,
+                           hipStream_t s);
 // true if the chosen inter kernel has a wave-pair form (two-strips 32x8).
 bool inter_has_pair(bool affine, int x2_ok);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.

@@ -105,6 +105,9 @@ typedef struct sw_timing {
     float coop_ms;      /* cooperative wide-block kernel alone (events on its stream) */
     float wave_ms;      /* per-wave inter kernel alone (events on the handle's stream) */
 } sw_timing;
+/* A scan run as ONE merged longest-first launch (sw_last_kernel ends in
+ * "+lpt": inter blocks and the long subjects' fp16 pass in one grid) reports
+ * that launch as inter_ms and wave_ms and 0 as intra_ms. */
 
 typedef struct sw_handle sw_handle;
 typedef struct sw_db sw_db;
@@ -273,10 +276,12 @@ SW_API int sw_score_pair(sw_handle* h, const uint8_t* query, int32_t qlen,
 /* ---- several GPUs of one process -------------------------
  * Replaces the reference's single-GPU scan loop (main.cpp:54-56 ->
  * smith_waterman_cuda, SWSolver.cu:266-404) with one database sharded over
- * the devices of a group.  sw_group_create: one handle per listed device and,
- * for two or more DISTINCT devices, an RCCL communicator over them
- * (ncclCommInitAll; librccl is loaded at run time).  A device listed twice
- * is allowed (one-GPU tests): the top-K exchange then goes through the host.
+ * the devices of a group.  sw_group_create: one handle per listed device.
+ * The first sw_group_topk of a group of DISTINCT devices creates an RCCL
+ * communicator over them (ncclCommInitAll; librccl is loaded at run time,
+ * only then: sw_group_scan needs no collective and no RCCL).  A device listed
+ * twice is allowed (one-GPU tests), and RCCL that cannot be loaded or
+ * initialised is tolerated: the top-K exchange then goes through the host.
  * sw_group_db_create: LPT shards over subject lengths (longest first, each to
  * the lightest shard, lowest index on ties: residue-balanced and
  * deterministic), one resident sw_db per device, built in parallel.
@@ -289,7 +294,9 @@ typedef struct sw_group sw_group;
 typedef struct sw_gdb sw_gdb;
 SW_API int sw_group_create(const int32_t* devices, int32_t ndev, sw_group** out);
 SW_API int sw_group_destroy(sw_group* g);
-/* "rccl allgather (N ranks)" or "host (...)". */
+/* The top-K exchange path: "rccl allgather (N ranks)" once the communicators
+ * exist, "rccl allgather (communicators created by the first top-K)" before,
+ * or "host (<why>)". */
 SW_API const char* sw_group_info(const sw_group* g);
 /* The handle of device slot d (owned by the group). */
 SW_API int sw_group_handle(sw_group* g, int32_t d, sw_handle** out);

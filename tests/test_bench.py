@@ -12,6 +12,54 @@ CONTRACT = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
             "vs_baseline", "dtype", "data", "config")
 
 
+def test_bench_refuses_world_size_mismatch():
+    """--gpus N under a torchrun environment of another size exits non-zero
+    (before importing torch or touching a GPU) instead of measuring one rank."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"],
+                         capture_output=True, text=True, timeout=120, cwd=REPO, env=env)
+    assert out.returncode != 0
+    assert "WORLD_SIZE 1" in out.stderr and out.stdout.strip() == ""
+
+
+def test_bench_check_world():
+    sys.path.insert(0, REPO)
+    import bench
+    assert bench.check_world(4, {"WORLD_SIZE": "4"}) == 4
+    assert bench.check_world(1, {}) == 1
+    for gpus, env in ((8, {}), (2, {"WORLD_SIZE": "8"})):
+        try:
+            bench.check_world(gpus, env)
+        except SystemExit:
+            continue
+        raise AssertionError("no refusal for --gpus %d, env %s" % (gpus, env))
+
+
+def test_bench_launches_its_own_ranks(monkeypatch):
+    """Without WORLD_SIZE, --gpus N starts ONE torch.distributed.run child with
+    N ranks on 127.0.0.1 and relays exactly one JSON line and its exit code."""
+    sys.path.insert(0, REPO)
+    import bench
+    seen = {}
+
+    class FakeProc:
+        def __init__(self, cmd, **kw):
+            seen["cmd"] = cmd
+            self.stdout = iter(['[rank1] chatter\n', '{"metric": "m", "value": 1.0, "n_gpus": 2}\n'])
+
+        def wait(self):
+            return 0
+
+    monkeypatch.setattr(bench.subprocess, "Popen", FakeProc)
+    rc = bench.launch_ranks(2, ["--gpus", "2", "--backend", "gloo"])
+    assert rc == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "2"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "2", "--backend", "gloo"]
+
+
 def test_bench_c1_json_line():
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--config", "c1", "--no-gpu"],
                          capture_output=True, text=True, timeout=300, cwd=REPO)

@@ -4,8 +4,9 @@
   every id:score equal to the oracle's, one GPU and the sharded path
   (--gpus 2 over one device listed twice, SW_DEVICES=0,0) byte-identical;
 * sw_group_* through ctypes: a one-device group (one-rank RCCL
-  communicator: the ncclAllGather path) and a device listed twice (host
-  exchange): full scores == sw_scan's, top-K == the oracle's top-K."""
+  communicator: the ncclAllGather path), a device listed twice (host
+  exchange) and, on a multi-GPU box, every distinct device (RCCL over >= 2
+  ranks): full scores == sw_scan's, top-K == the oracle's top-K."""
 import os
 import subprocess
 import sys
@@ -49,13 +50,26 @@ def test_main_100k_records_equal_oracle(sw, oracle, fasta_100k):
     assert np.array_equal(pairs2, pairs)
 
 
-@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def _device_count():
+    import torch
+    return torch.cuda.device_count()
+
+
+# one device, one device listed twice / three times (host exchange), and every
+# distinct device of the box (2..8: ncclCommInitAll over >= 2 ranks, the
+# ncclAllGather path across devices) when it has more than one
+_DEVICE_SETS = [[0], [0, 0], [0, 0, 0]] + ([list(range(min(_device_count(), 8)))] if _device_count() >= 2 else [])
+
+
+@pytest.mark.parametrize("devices", _DEVICE_SETS, ids=lambda d: "dev" + "_".join(map(str, d)))
 def test_group_scan_and_topk(sw, oracle, handle, devices):
     res, offs = sw.synth.database(9000, shard=9)
     ids = np.random.default_rng(3).permutation(12000)[:9000].astype(np.int32)
     g = sw.Group(devices)
+    distinct = len(set(devices)) == len(devices)
     info = g.info()
-    assert info.startswith("rccl allgather (1 rank)" if len(devices) == 1 else "host")
+    # the communicators are created by the first top-K, not by the group
+    assert info.startswith("rccl allgather (communicators" if distinct else "host")
     gdb = g.database(res, offs, ids=ids)
     shards = [gdb.shard(k) for k in range(len(devices))]
     assert sum(s[0] for s in shards) == 9000 and sum(s[1] for s in shards) == int(offs[-1])
@@ -71,23 +85,34 @@ def test_group_scan_and_topk(sw, oracle, handle, devices):
     for k in (1, 100, 4096):
         keys = gdb.topk(q, k, m, 12, 1)
         assert np.array_equal(keys, sw.dist.local_topk(want, ids, k)), k
+    if distinct:
+        n = len(devices)
+        assert g.info() == "rccl allgather (%d rank%s)" % (n, "" if n == 1 else "s"), g.info()
     gdb.close()
     db.close()
     g.close()
 
 
-def test_group_single_rank_rccl_cli(fasta_100k):
-    """main --gpus 1 stays the single-handle path; --gpus 2 over two distinct
-    devices needs a second GPU (not on the test box): refused cleanly when
-    absent (no device), never silently served by one GPU."""
-    path, _, _ = fasta_100k
+def test_group_distinct_devices_cli(oracle, fasta_100k):
+    """main --gpus 2 over two DISTINCT devices: on a box with two or more GPUs
+    every id:score equals the oracle's (and the one-GPU output); on a one-GPU
+    box it is refused cleanly (no device), never silently served by one GPU."""
+    import dropin_scale
+    path, res, offs = fasta_100k
     env = dict(os.environ)
     env.pop("SW_DEVICES", None)
     lib = os.path.join(REPO, "ece1782-smith-waterman-cuda_amd", "lib", "main")
     qf = os.path.join(REPO, "tests", "golden", "queries", "P02232.fasta")
-    import torch
-    if torch.cuda.device_count() >= 2:
-        pytest.skip("two devices present: covered by the multi-GPU bench")
+    if _device_count() >= 2:
+        q = read_query("P02232")
+        q += "/" * (-len(q) % 8)  # SWSolver.cu:267-269
+        want = oracle.scan(oracle.encode(q), res, offs, mat=oracle.matrix(), gap_open=2, gap_extend=2, nthreads=16)
+        pairs, metrics, _ = dropin_scale.run_main("P02232", path, gpus=2, env=env)
+        assert metrics["gpus"] == 2
+        got = np.zeros(len(offs) - 1, dtype=np.int64)
+        got[pairs[:, 0]] = pairs[:, 1]
+        assert np.array_equal(got, want)
+        return
     out = subprocess.run([lib, "--query", qf, "--db", path, "--gpus", "2"], capture_output=True, text=True,
                          env=env, timeout=300)
     assert out.returncode != 0 and "device" in out.stderr

@@ -563,21 +563,18 @@ def test_random_scoring_and_shapes(sw, oracle, handle, case):
                                            handle.last_intra_kernel(), np.nonzero(got != want)[0][:10])
 
 
-@pytest.mark.parametrize("quad_width,pipe_len", [("0", "0"), ("200", "0"), ("16", "0"), ("200", "1"),
-                                                 ("0", "900")])
+@pytest.mark.parametrize("quad_width", ["0", "200", "16"])
 @pytest.mark.parametrize("scoring", [(1, 12, 1), (0, 2, 2)])
-def test_merged_lpt_launch(sw, oracle, handle, monkeypatch, quad_width, pipe_len, scoring):
+def test_merged_lpt_launch(sw, oracle, handle, monkeypatch, quad_width, scoring):
     """sw_scan_lpt (the inter blocks by quads / pairs / single waves and the
     long subjects' fp16 pass in one launch, longest work first): queries for
-    the three intra shapes it supports (4, 6, 8 rows per lane) and 2 / 3 / 4
-    chunks of the pipelined pairs, quads for none, the widest or every group
-    block, none / some / all long pairs pipelined over whole workgroups,
-    planted near-copies in both kernels' halves (rescue chains after the
-    merged launch), against the oracle and the two-launch form."""
+    the three intra shapes it supports (4, 6, 8 rows per lane), quads for
+    none, the widest or every group block, planted near-copies in both
+    kernels' halves (rescue chains after the merged launch), against the
+    oracle and the two-launch form."""
     mid, go, ge = scoring
     monkeypatch.setenv("SW_LPT", "1")
     monkeypatch.setenv("SW_QUAD_WIDTH", quad_width)
-    monkeypatch.setenv("SW_PIPE_LEN", pipe_len)
     monkeypatch.setenv("SW_PAIR_WIDTH", "64")
     r, o = sw.synth.database(2500, shard=23)
     q0 = sw.synth.query(500, shard=8)
