@@ -173,7 +173,8 @@ int main(int argc, char* argv[]) {
         cout << "{\"query_len\": " << querySequence.length() << ", \"subjects\": " << num_subjects
              << ", \"padded_residues\": " << length_sum << ", \"wall_s\": " << seconds_elapsed
              << ", \"parse_s\": " << parse_s << ", \"solve_s\": " << solve_s << ", \"flatten_s\": " << t.flatten_s
-             << ", \"upload_s\": " << t.upload_s << ", \"scan_s\": " << t.scan_s << ", \"gpus\": " << t.gpus
+             << ", \"init_s\": " << t.init_s << ", \"upload_s\": " << t.upload_s << ", \"scan_s\": " << t.scan_s
+             << ", \"gpus\": " << t.gpus
              << "}" << endl;
     }
     return 0;

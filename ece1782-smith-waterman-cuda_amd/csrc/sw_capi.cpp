@@ -140,9 +140,11 @@ int default_threads() {
     return static_cast<int>(std::min(16u, n));  // GPU boxes expose many more CPUs than our share
 }
 
+// f(i) for i in [0, n) on up to default_threads() threads, `grain` indices
+// per grab (at least one grab per thread).
 template <class F>
-void parallel_for(int64_t n, F&& f) {
-    const int nt = static_cast<int>(std::min<int64_t>(default_threads(), std::max<int64_t>(1, n / 64)));
+void parallel_for(int64_t n, F&& f, int64_t grain = 64) {
+    const int nt = static_cast<int>(std::min<int64_t>(default_threads(), std::max<int64_t>(1, n / grain)));
     if (nt <= 1) {
         for (int64_t i = 0; i < n; ++i) f(i);
         return;
@@ -152,13 +154,52 @@ void parallel_for(int64_t n, F&& f) {
     for (int t = 0; t < nt; ++t)
         th.emplace_back([&] {
             for (;;) {
-                const int64_t i0 = next.fetch_add(64);
+                const int64_t i0 = next.fetch_add(grain);
                 if (i0 >= n) break;
-                const int64_t i1 = std::min(n, i0 + 64);
+                const int64_t i1 = std::min(n, i0 + grain);
                 for (int64_t i = i0; i < i1; ++i) f(i);
             }
         });
     for (auto& t : th) t.join();
+}
+
+// A vector element type that resize() leaves uninitialised (the database's
+// host copy is filled by parallel copies right after).
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) {}
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        if constexpr (sizeof...(A) == 0) ::new (static_cast<void*>(p)) U;
+        else ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
+
+// Subject indices sorted by length, longest first, stable (file order
+// within a length): a counting sort when lengths are bounded, else
+// std::stable_sort.
+std::vector<int64_t> length_order(const std::vector<int64_t>& offs, int64_t n) {
+    std::vector<int64_t> order(n);
+    int64_t maxl = 0;
+    for (int64_t k = 0; k < n; ++k) maxl = std::max(maxl, offs[k + 1] - offs[k]);
+    if (maxl > (int64_t(1) << 22)) {
+        std::iota(order.begin(), order.end(), 0);
+        std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) {
+            return offs[x + 1] - offs[x] > offs[y + 1] - offs[y];
+        });
+        return order;
+    }
+    std::vector<int64_t> start(static_cast<size_t>(maxl) + 2, 0);
+    for (int64_t k = 0; k < n; ++k) ++start[static_cast<size_t>(maxl - (offs[k + 1] - offs[k]) + 1)];
+    for (size_t l = 1; l < start.size(); ++l) start[l] += start[l - 1];
+    for (int64_t k = 0; k < n; ++k) order[start[static_cast<size_t>(maxl - (offs[k + 1] - offs[k]))]++] = k;
+    return order;
 }
 
 }  // namespace
@@ -193,6 +234,17 @@ struct sw_handle {
     // kernel (fork/join through ev[0] and ev[1]).
     hipStream_t side = nullptr;
     hipStream_t side2 = nullptr;  // the cooperative wide-block kernel
+    // Deferred rescue tails (the queries of a batch but the last): a scan's
+    // re-scoring stages (int16 / int32 list kernels) run on `tail` after its
+    // fp16 passes, while the next query's fp16 passes start on the main and
+    // side streams.  Lists and boundary rows of the tail are its own
+    // (parity-indexed lists, sw_db::d_rbnd_*), so nothing is shared with the
+    // passes running beside it.
+    hipStream_t tail = nullptr;
+    hipEvent_t main_done = nullptr, side_done = nullptr;  // fp16 passes of the scan being deferred
+    hipEvent_t tail_done[2] = {};                         // per list parity
+    bool tail_pending[2] = {};
+    int parity = 0;                                       // list set of the next scan
     hipEvent_t coop_done = nullptr;
     hipEvent_t fork2 = nullptr;  // side2 starts after the rescue counters are reset
     // per-query workspace: profiles (inter: [32][stride]; intra: lane-slotted
@@ -208,7 +260,15 @@ struct sw_handle {
         size_t hcap = 0;
         hipEvent_t copied = nullptr;  // the staging buffer may be rewritten after this
         bool pending = false;
+        hipEvent_t tail_read = nullptr;  // a deferred rescue tail has read the device copy
+        bool tail_pending = false;
     };
+    // pinned staging of database uploads (build_db): the host packs one
+    // buffer while the other's copy runs
+    uint8_t* stage[2] = {};
+    size_t stage_cap = 0;
+    hipEvent_t stage_ev[2] = {};
+    bool stage_pending[2] = {};
     static constexpr int kProfSlots = 4;
     ProfSlot prof[kProfSlots];
     int prof_next = 0;
@@ -243,8 +303,16 @@ struct sw_db {
     // two rescue lists [count, block ids...] of nblocks + 1 ints each: the
     // 16-bit kernels' flagged blocks (list A), and the fp16 chain's second
     // stage's (list B)
+    // (two parities of these lists: consecutive scans of a batch alternate)
     int32_t* d_rescue = nullptr;
     int32_t* d_lrescue = nullptr;        // [count, subjects...] x 2: the intra rescue chain's lists
+    // boundary rows of deferred rescue tails (inter H, F; intra H, F), when
+    // device memory allows them (else the tails run in stream order)
+    int32_t* d_rbnd_h = nullptr;
+    int32_t* d_rbnd_f = nullptr;
+    int32_t* d_rlbnd_h = nullptr;
+    int32_t* d_rlbnd_f = nullptr;
+    bool rbnd_tried = false;
     // the intra chain's order (scan_impl): the fp16 pass's flagged count read
     // back after the scan (pinned, event-gated), and per scoring the shortest
     // query seen to flag over half of the long subjects
@@ -307,7 +375,7 @@ struct sw_db {
     int32_t* d_lbnd_h = nullptr;
     int32_t* d_lbnd_f = nullptr;
     // host copies kept to allow re-partitioning when the threshold changes
-    std::vector<uint8_t> h_residues;
+    std::vector<uint8_t, NoInitAlloc<uint8_t>> h_residues;
     std::vector<int64_t> h_offsets;
     std::vector<int32_t> h_ids;
     std::unordered_map<int32_t, int64_t> id_index;  // result id -> subject (built on first sw_align)
@@ -362,13 +430,15 @@ int32_t default_long_threshold(const sw_db* db) {
 void free_dev(sw_db* db) {
     void* ptrs[] = {db->d_res, db->d_blk_off, db->d_blk_groups, db->d_lane_ids, db->d_bnd_h, db->d_bnd_f,
                     db->d_rescue, db->d_lres, db->d_loff, db->d_llen, db->d_lid, db->d_lbnd_h, db->d_lbnd_f,
-                    db->d_lrescue};
+                    db->d_lrescue, db->d_rbnd_h, db->d_rbnd_f, db->d_rlbnd_h, db->d_rlbnd_f};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     db->d_res = nullptr; db->d_blk_off = nullptr; db->d_blk_groups = nullptr; db->d_lane_ids = nullptr;
     db->d_bnd_h = nullptr; db->d_bnd_f = nullptr; db->d_rescue = nullptr; db->d_lres = nullptr; db->d_loff = nullptr;
     db->d_llen = nullptr; db->d_lid = nullptr; db->d_lbnd_h = nullptr; db->d_lbnd_f = nullptr;
     db->d_lrescue = nullptr;
+    db->d_rbnd_h = db->d_rbnd_f = db->d_rlbnd_h = db->d_rlbnd_f = nullptr;
+    db->rbnd_tried = false;
     for (auto& t : db->lpt_tables) (void)hipFree(t.d_order);
     db->lpt_tables.clear();
     if (db->h_trace) (void)hipHostFree(db->h_trace);  // sized for this block layout
@@ -477,21 +547,63 @@ void subject_residues(const sw_db* db, int64_t k, uint8_t* out) {
         std::memcpy(out, db->h_residues.data() + db->h_offsets[k], L);
 }
 
+// Upload bytes produced unit by unit (unit u covers [bounds[u], bounds[u+1])
+// of `dev` and fill(u, dst) writes all of it, padding included) through the
+// handle's two pinned staging buffers: chunks of whole units are packed on
+// the host's cores into one buffer while the previous chunk's H2D copy runs
+// (the reference packs byte by byte into managed memory on one thread,
+// SWSolver.cu:309-359).
+constexpr size_t kStageBytes = size_t(32) << 20;
+
+template <class F>
+int staged_upload(sw_handle* h, uint8_t* dev, const std::vector<uint64_t>& bounds, F&& fill) {
+    const int64_t nu = static_cast<int64_t>(bounds.size()) - 1;
+    if (nu <= 0 || bounds.back() == bounds.front()) return SW_OK;
+    uint64_t maxu = 0;
+    for (int64_t u = 0; u < nu; ++u) maxu = std::max<uint64_t>(maxu, bounds[u + 1] - bounds[u]);
+    const size_t cap = std::max<size_t>(kStageBytes, maxu);
+    if (cap > h->stage_cap) {
+        for (int b = 0; b < 2; ++b) {
+            if (h->stage_pending[b]) HIPCHECK(hipEventSynchronize(h->stage_ev[b]));
+            h->stage_pending[b] = false;
+            if (h->stage[b]) HIPCHECK(hipHostFree(h->stage[b]));
+            h->stage[b] = nullptr;
+        }
+        h->stage_cap = 0;
+        for (int b = 0; b < 2; ++b)
+            HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h->stage[b]), cap, hipHostMallocDefault));
+        h->stage_cap = cap;
+    }
+    int b = 0;
+    for (int64_t u0 = 0; u0 < nu;) {
+        int64_t u1 = u0 + 1;
+        while (u1 < nu && bounds[u1 + 1] - bounds[u0] <= h->stage_cap) ++u1;
+        if (h->stage_pending[b]) HIPCHECK(hipEventSynchronize(h->stage_ev[b]));
+        uint8_t* buf = h->stage[b];
+        const uint64_t base = bounds[u0];
+        parallel_for(u1 - u0, [&](int64_t i) { fill(u0 + i, buf + (bounds[u0 + i] - base)); }, 1);
+        HIPCHECK(hipMemcpyAsync(dev + base, buf, bounds[u1] - base, hipMemcpyHostToDevice, h->stream));
+        HIPCHECK(hipEventRecord(h->stage_ev[b], h->stream));
+        h->stage_pending[b] = true;
+        b ^= 1;
+        u0 = u1;
+    }
+    return SW_OK;
+}
+
 // Pack: sort by length (descending, stable), route subjects longer than the
 // threshold to the intra kernel, deal the rest into 64-lane blocks of
 // 16-residue groups.  Lanes past a subject's end hold kPadCode.
 int build_db(sw_db* db) {
     hipStream_t s = db->h->stream;
     const int64_t n = db->n;
-    std::vector<int64_t> order(n);
-    std::iota(order.begin(), order.end(), 0);
+    const std::vector<int64_t> order = length_order(db->h_offsets, n);
     auto len = [&](int64_t k) { return db->h_offsets[k + 1] - db->h_offsets[k]; };
-    std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return len(x) > len(y); });
     int64_t nlong = 0;
     while (nlong < n && len(order[nlong]) > db->long_threshold) ++nlong;
 
-    // ---- intra (long) part: plain concatenation, 16-byte aligned starts
-    std::vector<uint64_t> loff(nlong);
+    // ---- intra (long) part: plain concatenation, 64-byte aligned starts
+    std::vector<uint64_t> loff(nlong + 1);
     std::vector<int32_t> llen(nlong), lid(nlong);
     uint64_t ltotal = 0;
     for (int64_t k = 0; k < nlong; ++k) {
@@ -501,17 +613,12 @@ int build_db(sw_db* db) {
         lid[k] = db->h_ids[src];
         ltotal += round_up(len(src), 64);
     }
-    std::vector<uint8_t> lres(db->synthetic ? 0 : ltotal, swk::kPadCode);
-    if (!db->synthetic)
-        parallel_for(nlong, [&](int64_t k) {
-            const int64_t src = order[k];
-            std::memcpy(lres.data() + loff[k], db->h_residues.data() + db->h_offsets[src], len(src));
-        });
+    loff[nlong] = ltotal;
 
     // ---- inter part
     const int64_t nshort = n - nlong;
     const int64_t nblocks = (nshort + swk::kLanes - 1) / swk::kLanes;
-    std::vector<uint64_t> blk_off(nblocks);
+    std::vector<uint64_t> blk_off(nblocks + 1);
     std::vector<uint32_t> blk_groups(nblocks);
     std::vector<int32_t> lane_ids(nblocks * swk::kLanes, -1);
     std::vector<int64_t> blk_res(nblocks, 0);  // unpadded residues per block
@@ -523,7 +630,7 @@ int build_db(sw_db* db) {
         blk_groups[b] = static_cast<uint32_t>(w / swk::kGroupCols);
         total += static_cast<uint64_t>(blk_groups[b]) * swk::kGroupBytes;
     }
-    std::vector<uint8_t> res(db->synthetic ? 0 : total, swk::kPadCode);
+    blk_off[nblocks] = total;
     std::vector<int32_t> lane_len(db->synthetic ? nblocks * swk::kLanes : 0, 0);
     parallel_for(nblocks, [&](int64_t b) {
         for (int l = 0; l < swk::kLanes; ++l) {
@@ -531,18 +638,31 @@ int build_db(sw_db* db) {
             if (k >= n) break;
             const int64_t src = order[k];
             lane_ids[b * swk::kLanes + l] = db->h_ids[src];
-            const int64_t L = len(src);
-            blk_res[b] += L;
-            if (db->synthetic) {
-                lane_len[b * swk::kLanes + l] = static_cast<int32_t>(L);
-                continue;
-            }
-            const uint8_t* p = db->h_residues.data() + db->h_offsets[src];
-            for (int64_t j = 0; j < L; ++j)
-                res[blk_off[b] + (j / swk::kGroupCols) * swk::kGroupBytes + l * swk::kGroupCols +
-                    (j % swk::kGroupCols)] = p[j];
+            blk_res[b] += len(src);
+            if (db->synthetic) lane_len[b * swk::kLanes + l] = static_cast<int32_t>(len(src));
         }
     });
+    // one block's bytes: [group][lane][16 codes], kPadCode past each subject
+    auto fill_block = [&](int64_t b, uint8_t* dst) {
+        std::memset(dst, swk::kPadCode, static_cast<size_t>(blk_groups[b]) * swk::kGroupBytes);
+        for (int l = 0; l < swk::kLanes; ++l) {
+            const int64_t k = nlong + b * swk::kLanes + l;
+            if (k >= n) break;
+            const int64_t src = order[k], L = len(src);
+            const uint8_t* p = db->h_residues.data() + db->h_offsets[src];
+            uint8_t* d = dst + l * swk::kGroupCols;
+            int64_t j = 0;
+            for (; j + swk::kGroupCols <= L; j += swk::kGroupCols, d += swk::kGroupBytes)
+                std::memcpy(d, p + j, swk::kGroupCols);
+            if (j < L) std::memcpy(d, p + j, static_cast<size_t>(L - j));
+        }
+    };
+    auto fill_long = [&](int64_t k, uint8_t* dst) {
+        const int64_t src = order[k];
+        std::memset(dst, swk::kPadCode, loff[k + 1] - loff[k]);
+        std::memcpy(dst, db->h_residues.data() + db->h_offsets[src], static_cast<size_t>(len(src)));
+    };
+    blk_off.pop_back();
 
     size_t acc = 0;
     int rc;
@@ -553,12 +673,23 @@ int build_db(sw_db* db) {
         if (ltotal) HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lres), ltotal));
         acc += total + ltotal;
     } else {
-        if ((rc = upload(&db->d_res, res, s, &acc))) return rc;
+        // residues through pinned staging, packed in parallel chunks
+        std::vector<uint64_t> bounds(blk_off);
+        bounds.push_back(total);
+        if (total) {
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_res), total));
+            if ((rc = staged_upload(db->h, db->d_res, bounds, fill_block))) return rc;
+        }
+        if (ltotal) {
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lres), ltotal));
+            if ((rc = staged_upload(db->h, db->d_lres, loff, fill_long))) return rc;
+        }
+        acc += total + ltotal;
     }
     if ((rc = upload(&db->d_blk_off, blk_off, s, &acc))) return rc;
     if ((rc = upload(&db->d_blk_groups, blk_groups, s, &acc))) return rc;
     if ((rc = upload(&db->d_lane_ids, lane_ids, s, &acc))) return rc;
-    if (!db->synthetic && (rc = upload(&db->d_lres, lres, s, &acc))) return rc;
+    loff.pop_back();
     if ((rc = upload(&db->d_loff, loff, s, &acc))) return rc;
     if ((rc = upload(&db->d_llen, llen, s, &acc))) return rc;
     if ((rc = upload(&db->d_lid, lid, s, &acc))) return rc;
@@ -627,6 +758,31 @@ int ensure_bnd(sw_db* db, bool affine, bool intra_f) {
     return SW_OK;
 }
 
+// The deferred tails' own boundary rows (same sizes as ensure_bnd's), tried
+// once per layout; false when device memory would drop below a quarter of
+// the card's (a 50M-subject database keeps its tails in stream order).
+bool ensure_rbnd(sw_db* db) {
+    if (db->d_rbnd_h || db->d_rlbnd_h) return true;
+    if (db->rbnd_tried) return false;
+    db->rbnd_tried = true;
+    const size_t need = db->res_bytes * 8 + db->lres_bytes * 8;
+    size_t freeb = 0, totalb = 0;
+    if (hipMemGetInfo(&freeb, &totalb) != hipSuccess || freeb < need + totalb / 4) return false;
+    void** p[4] = {reinterpret_cast<void**>(&db->d_rbnd_h), reinterpret_cast<void**>(&db->d_rbnd_f),
+                   reinterpret_cast<void**>(&db->d_rlbnd_h), reinterpret_cast<void**>(&db->d_rlbnd_f)};
+    const size_t sz[4] = {db->res_bytes * 4, db->res_bytes * 4, db->lres_bytes * 4, db->lres_bytes * 4};
+    for (int k = 0; k < 4; ++k)
+        if (sz[k] && hipMalloc(p[k], sz[k]) != hipSuccess) {
+            for (int j = 0; j < 4; ++j)
+                if (*p[j]) (void)hipFree(*p[j]);
+            for (int j = 0; j < 4; ++j) *p[j] = nullptr;
+            (void)hipGetLastError();
+            return false;
+        }
+    db->device_bytes += need;
+    return true;
+}
+
 int check_scoring(const sw_scoring* sc, const int8_t** mat, int* go, int* ge) {
     *mat = kBlosum50Ref;
     *go = 2;
@@ -656,6 +812,7 @@ struct Profiles {
     size_t off16 = 0;        // int16 inter profile (packed kernels)
     size_t intra_off = 0;    // lane-slotted intra profile
     size_t total = 0;
+    int slot = 0;            // the handle's profile slot holding them
 };
 
 int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* mat, int go, bool affine,
@@ -677,6 +834,7 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     const size_t intra_bytes = ri ? static_cast<size_t>(qpad_intra / (swk::kLanes * ri)) * swk::intra_chunk_bytes(ri) : 0;
     P->intra_off = take(intra_bytes);
     P->total = at;
+    P->slot = h->prof_next;
     sw_handle::ProfSlot& S = h->prof[h->prof_next];
     h->prof_next = (h->prof_next + 1) % sw_handle::kProfSlots;
     if (S.pending) HIPCHECK(hipEventSynchronize(S.copied));  // its last copy has consumed the staging buffer
@@ -724,6 +882,10 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     // reader among them), before this one.  (A copy stream of its own, to
     // overlap the copy with the running scan, measured no faster and costs
     // a hardware queue: see sw_create.)
+    if (S.tail_pending) {  // a deferred tail still reads the slot's last profiles
+        HIPCHECK(hipStreamWaitEvent(h->stream, S.tail_read, 0));
+        S.tail_pending = false;
+    }
     HIPCHECK(hipMemcpyAsync(S.d, hp, P->total, hipMemcpyHostToDevice, h->stream));
     HIPCHECK(hipEventRecord(S.copied, h->stream));
     S.pending = true;
@@ -894,8 +1056,11 @@ int next_events(sw_handle* h) {
     return SW_OK;
 }
 
+// defer: another scan follows on this handle before the caller waits (the
+// queries of a batch but the last): this scan's rescue tail may run on the
+// tail stream beside the next scan's fp16 passes (sw_handle::tail).
 int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen, const sw_scoring* sc,
-              int32_t* scores_dev) {
+              int32_t* scores_dev, bool defer = false) {
     sw_db* db = const_cast<sw_db*>(cdb);
     if (!h || !db || (!query && qlen > 0) || qlen < 0 || !scores_dev) return fail(SW_E_INVALID, "null argument");
     const int8_t* mat;
@@ -1056,29 +1221,45 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                              std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2}),
                              x2 || intra_x2, ri, qpad_intra, &P)))
         return rc;
+    const int64_t rstride = 2 * (db->nblocks + 1) + 2;  // lists A and B, the largest flagged block
+    const int64_t lstride = 2 * (db->nlong + 1);        // intra lists 1 and 2
     if (rescue && db->nblocks && !db->d_rescue) {
-        // lists A and B, then the fp16 pass's largest flagged block
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rescue), (2 * (db->nblocks + 1) + 2) * sizeof(int32_t)));
-        db->device_bytes += (2 * (db->nblocks + 1) + 2) * sizeof(int32_t);
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rescue), 2 * rstride * sizeof(int32_t)));
+        db->device_bytes += 2 * rstride * sizeof(int32_t);
     }
     const bool multi_inter = qpad_inter > R || qpad_rescue > swk::rescue_rows(affine) ||
                              qpad_coop > swk::inter_coop_rows() || qpad_list > (affine ? 64 : 96);
     const bool multi_intra = (ri && qpad_intra > swk::kLanes * ri) || (ri2 && qpad_intra2 > swk::kLanes * ri2);
     if ((multi_inter || multi_intra) && (rc = ensure_bnd(db, affine, intra_x2))) return rc;
     if (intra_x2 && !db->d_lrescue) {  // two lists: [count, subjects...] x 2
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lrescue), 2 * (db->nlong + 1) * sizeof(int32_t)));
-        db->device_bytes += 2 * (db->nlong + 1) * sizeof(int32_t);
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lrescue), 2 * lstride * sizeof(int32_t)));
+        db->device_bytes += 2 * lstride * sizeof(int32_t);
     }
+    // this scan's list set; a deferred tail of the scan before last used it
+    const int par = h->parity;
+    h->parity ^= 1;
+    if (h->tail_pending[par]) {
+        HIPCHECK(hipStreamWaitEvent(h->stream, h->tail_done[par], 0));
+        h->tail_pending[par] = false;
+    }
+    int32_t* const listA = db->d_rescue ? db->d_rescue + par * rstride : nullptr;  // [count, ids...]
+    int32_t* const listB = listA ? listA + db->nblocks + 1 : nullptr;
+    int32_t* const maxA = listA ? listA + 2 * (db->nblocks + 1) : nullptr;
+    int32_t* const list1 = db->d_lrescue ? db->d_lrescue + par * lstride : nullptr;  // flagged by the fp16 pass
+    int32_t* const list2 = list1 ? list1 + db->nlong + 1 : nullptr;                  // ... and again by int16
+    // the rescue tail on its own stream and boundary rows (see sw_handle::tail)
+    const bool deferred = defer && (!(multi_inter || multi_intra) || ensure_rbnd(db));
+    hipStream_t const ts = deferred ? h->tail : h->stream;
 
     // the rescue lists' counters (inter A, B, largest flagged block; intra
     // 1, 2) in one launch instead of five memsets, before the fork so the
     // side stream sees them
     {
-        int32_t* cA = (rescue && db->nblocks) ? db->d_rescue : nullptr;
-        int32_t* cB = (cA && f16) ? db->d_rescue + db->nblocks + 1 : nullptr;
-        int32_t* mA = (cA && f16) ? db->d_rescue + 2 * (db->nblocks + 1) : nullptr;
-        int32_t* c1 = (db->nlong && intra_x2) ? db->d_lrescue : nullptr;
-        int32_t* c2 = c1 ? db->d_lrescue + db->nlong + 1 : nullptr;
+        int32_t* cA = (rescue && db->nblocks) ? listA : nullptr;
+        int32_t* cB = (cA && f16) ? listB : nullptr;
+        int32_t* mA = (cA && f16) ? maxA : nullptr;
+        int32_t* c1 = (db->nlong && intra_x2) ? list1 : nullptr;
+        int32_t* c2 = c1 ? list2 : nullptr;
         if (cA || c1) HIPCHECK(swk::launch_reset_counters(cA, cB, mA, c1, c2, h->stream));
     }
     // One merged launch for the fp16 scan, longest work first (sw_scan_lpt):
@@ -1106,6 +1287,70 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     swk::IntraArgs lpt_intra{};
     // the long subjects' kernels: all of them, or (lpt_done) those after the
     // fp16 pass the merged launch ran
+    // The long subjects' rescue stages (the int16 form over the fp16 pass's
+    // list, then int32 over what is left), on stream st with boundary rows
+    // bh / bf: right after the passes (stream order), or deferred to the
+    // tail stream with the tail's own boundary rows.
+    swk::IntraArgs tail_x{}, tail_ia{};
+    bool intra_tail = false;
+    auto launch_intra_tail = [&](hipStream_t st, int32_t* bh, int32_t* bf) -> int {
+        if (!intra_i16_first) {
+            // the int16 form re-scores the fp16 pass's list (scores near
+            // 2048: high-scoring pairs, or linear scoring with cheap gaps)
+            // and flags near-32767 ones
+            swk::IntraArgs y = tail_x;
+            y.bnd_h = bh;
+            y.bnd_f = bf;
+            y.list_count = list1;
+            y.subj_list = list1 + 1;
+            y.rescue_count = list2;
+            y.rescue_list = list2 + 1;
+            HIPCHECK(swk::launch_intra_x2_list16(y, ri2, st));
+            ++h->launches;
+        }
+        // int32 re-scoring of what is left (device-side list)
+        swk::IntraArgs ia = tail_ia;
+        ia.bnd_h = bh;
+        ia.bnd_f = bf;
+        HIPCHECK(swk::launch_intra(ia, ri, affine, st));
+        ++h->launches;
+        return SW_OK;
+    };
+    // The inter scan's rescue tail: the int16 packed kernel over the blocks
+    // the fp16 kernel flagged (list A: scores near 2048; it flags its own
+    // near-32767 ones into list B), then int32 over list B (list A for the
+    // int16 scans), on stream st with boundary rows bh / bf.
+    swk::InterArgs tail_a{};
+    bool inter_tail = false;
+    auto launch_inter_tail = [&](hipStream_t st, int32_t* bh, int32_t* bf) -> int {
+        if (f16) {
+            swk::InterArgs r = tail_a;
+            r.bnd_h = bh;
+            r.bnd_f = bf;
+            r.qpad = qpad_list;
+            r.blk_list = listA + 1;
+            r.blk_count = listA;
+            r.rescue_list = listB + 1;
+            r.rescue_count = listB;
+            r.rescue_max = nullptr;
+            HIPCHECK(swk::launch_inter_x2s_list(r, affine, st));
+            ++h->launches;
+        }
+        swk::InterArgs r = tail_a;
+        r.bnd_h = bh;
+        r.bnd_f = bf;
+        r.prof = P.dev + P.off8;
+        r.qpad = qpad_rescue;
+        r.blk_list = (f16 ? listB : listA) + 1;
+        r.blk_count = f16 ? listB : listA;
+        r.rescue_list = nullptr;
+        r.rescue_count = nullptr;
+        HIPCHECK(swk::launch_inter_rescue(r, affine, st));
+        ++h->launches;
+        return SW_OK;
+    };
+    // the long subjects' kernels: all of them, or (lpt_done) those after the
+    // fp16 pass the merged launch ran
     auto launch_long = [&](bool lpt_done) -> int {
         if (!lpt_done && is != h->stream) HIPCHECK(hipStreamWaitEvent(is, h->ev[0], 0));
         swk::IntraArgs ia{};
@@ -1121,69 +1366,67 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         ia.bnd_h = db->d_lbnd_h;
         ia.bnd_f = db->d_lbnd_f;
         ia.scores = scores_dev;
-        if (intra_x2) {
-            swk::IntraArgs x = ia;
-            x.prof = P.dev + P.off16;
-            x.prof_stride = P.stride;
-            x.bias = affine ? 0 : go;  // the linear profile holds S + gap
-            x.qpad = qpad_intra2;
-            // biased cell: stored values up to (RI + 10) ge above the true ones
-            x.sat_limit = 2048 - 2 * std::max(max_s, 1) - 26 * ge;
-            for (int j = 0; j < 32; ++j) x.f16_step[j] = f16_pair(j * ge);
-            x.f16_gog = f16_pair(go - ge);
-            int32_t* list1 = db->d_lrescue;                  // flagged by the fp16 pass
-            int32_t* list2 = db->d_lrescue + db->nlong + 1;  // ... and again by the int16 pass
-            if (intra_i16_first) {
-                // the int16 form over every long subject, flagging near-32767 ones
-                x.rescue_count = list2;
-                x.rescue_list = list2 + 1;
-                HIPCHECK(swk::launch_intra_x2_int16(x, ri2, is));
-                h->launches += 1;
-            } else {
-                x.rescue_count = list1;
-                x.rescue_list = list1 + 1;
-                if (lpt && !lpt_done) {  // the merged launch runs this pass
-                    lpt_intra = x;
-                    return SW_OK;
-                }
-                if (!lpt_done) HIPCHECK(swk::launch_intra_x2(x, ri2, is));
-                // the fp16 pass's flagged count, read by a later scan
-                if (!db->h_lcount) {
-                    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&db->h_lcount), sizeof(int32_t),
-                                           hipHostMallocDefault));
-                    HIPCHECK(hipEventCreateWithFlags(&db->lcount_ev, hipEventDisableTiming));
-                }
-                const bool lseen = db->lcount_seen && db->lseen_key == skey && db->lseen_qhash == qhash &&
-                                   db->lseen_qlen == qlen;
-                if (!db->lcount_pending && !lseen) {
-                    HIPCHECK(hipMemcpyAsync(db->h_lcount, list1, sizeof(int32_t), hipMemcpyDeviceToHost, is));
-                    HIPCHECK(hipEventRecord(db->lcount_ev, is));
-                    db->lcount_pending = true;
-                    db->lcount_key = skey;
-                    db->lcount_qlen = qlen;
-                    db->lcount_qhash = qhash;
-                }
-                // the int16 form re-scores the fp16 pass's list (scores near
-                // 2048: high-scoring pairs, or linear scoring with cheap gaps)
-                // and flags near-32767 ones
-                swk::IntraArgs y = x;
-                y.list_count = list1;
-                y.subj_list = list1 + 1;
-                y.rescue_count = list2;
-                y.rescue_list = list2 + 1;
-                HIPCHECK(swk::launch_intra_x2_list16(y, ri2, is));
-                h->launches += 2;
-            }
-            // int32 re-scoring of what is left (device-side list)
-            ia.list_count = list2;
-            ia.subj_list = list2 + 1;
-        }
-        HIPCHECK(swk::launch_intra(ia, ri, affine, is));
-        ++h->launches;
         h->last_intra = intra_x2 ? "sw_intra_x2<" + std::to_string(ri2) + (intra_i16_first ? ",int16>" : ">")
                                  : "sw_intra<" + std::to_string(ri) + (affine ? ",affine>" : ",linear>");
         h->had_intra = true;
-        return SW_OK;
+        if (!intra_x2) {  // int32 over every long subject
+            HIPCHECK(swk::launch_intra(ia, ri, affine, is));
+            ++h->launches;
+            return SW_OK;
+        }
+        swk::IntraArgs x = ia;
+        x.prof = P.dev + P.off16;
+        x.prof_stride = P.stride;
+        x.bias = affine ? 0 : go;  // the linear profile holds S + gap
+        x.qpad = qpad_intra2;
+        // biased cell: stored values up to (RI + 10) ge above the true ones
+        x.sat_limit = 2048 - 2 * std::max(max_s, 1) - 26 * ge;
+        for (int j = 0; j < 32; ++j) x.f16_step[j] = f16_pair(j * ge);
+        x.f16_gog = f16_pair(go - ge);
+        if (intra_i16_first) {
+            // the int16 form over every long subject, flagging near-32767 ones
+            x.rescue_count = list2;
+            x.rescue_list = list2 + 1;
+            HIPCHECK(swk::launch_intra_x2_int16(x, ri2, is));
+            h->launches += 1;
+        } else {
+            x.rescue_count = list1;
+            x.rescue_list = list1 + 1;
+            if (lpt && !lpt_done) {  // the merged launch runs this pass
+                lpt_intra = x;
+                return SW_OK;
+            }
+            if (!lpt_done) {
+                HIPCHECK(swk::launch_intra_x2(x, ri2, is));
+                ++h->launches;
+            }
+            // the fp16 pass's flagged count, read by a later scan
+            if (!db->h_lcount) {
+                HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&db->h_lcount), sizeof(int32_t),
+                                       hipHostMallocDefault));
+                HIPCHECK(hipEventCreateWithFlags(&db->lcount_ev, hipEventDisableTiming));
+            }
+            const bool lseen = db->lcount_seen && db->lseen_key == skey && db->lseen_qhash == qhash &&
+                               db->lseen_qlen == qlen;
+            if (!db->lcount_pending && !lseen) {
+                HIPCHECK(hipMemcpyAsync(db->h_lcount, list1, sizeof(int32_t), hipMemcpyDeviceToHost, is));
+                HIPCHECK(hipEventRecord(db->lcount_ev, is));
+                db->lcount_pending = true;
+                db->lcount_key = skey;
+                db->lcount_qlen = qlen;
+                db->lcount_qhash = qhash;
+            }
+        }
+        tail_x = x;
+        tail_ia = ia;
+        tail_ia.list_count = list2;
+        tail_ia.subj_list = list2 + 1;
+        intra_tail = true;
+        if (deferred) {  // after the fp16 pass; launched on the tail stream below
+            HIPCHECK(hipEventRecord(h->side_done, is));
+            return SW_OK;
+        }
+        return launch_intra_tail(is, db->d_lbnd_h, db->d_lbnd_f);
     };
     if (db->nlong && (rc = launch_long(false))) return rc;
     if (!lpt) MARK(1, db->nlong ? is : h->stream);
@@ -1213,9 +1456,6 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             }
             HIPCHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.trace), db->h_trace, 0));
         }
-        int32_t* listA = db->d_rescue;                    // [count, ids...]
-        int32_t* listB = db->d_rescue ? db->d_rescue + db->nblocks + 1 : nullptr;
-        int32_t* maxA = db->d_rescue ? db->d_rescue + 2 * (db->nblocks + 1) : nullptr;
         // the widest blocks the int16 kernel takes first (see i16_span)
         const int32_t nr = (f16 && rescue && npair && !ncoop) ? i16_span : 0;
         db->last_i16_span = nr;
@@ -1309,55 +1549,55 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             db->icount_nr = nr;
             db->icount_qhash = qhash;
         }
-        if (f16) {
-            // fp16 chain, stage 2: the int16 packed kernel re-scores the
-            // blocks the fp16 kernel flagged (scores near 2048) and flags
-            // its own near-32767 ones into list B for the int32 stage
-            swk::InterArgs r = a;
-            r.qpad = qpad_list;
-            r.blk_list = listA + 1;
-            r.blk_count = listA;
-            r.rescue_list = listB + 1;
-            r.rescue_count = listB;
-            r.rescue_max = nullptr;
-            HIPCHECK(swk::launch_inter_x2s_list(r, affine, h->stream));
-            ++h->launches;
+        tail_a = a;
+        inter_tail = rescue;
+        if (deferred && inter_tail) HIPCHECK(hipEventRecord(h->main_done, h->stream));
+        else if (inter_tail && (rc = launch_inter_tail(h->stream, db->d_bnd_h, db->d_bnd_f))) return rc;
+    }
+    if (deferred && (inter_tail || intra_tail)) {
+        // this scan's rescue tail beside the next scan's fp16 passes
+        if (inter_tail) {
+            HIPCHECK(hipStreamWaitEvent(ts, h->main_done, 0));
+            if ((rc = launch_inter_tail(ts, db->d_rbnd_h, db->d_rbnd_f))) return rc;
         }
-        if (rescue) {
-            // int32 re-scoring of any block the 16-bit kernel flagged (rare:
-            // scores near 32767); the list and its count stay on the device
-            swk::InterArgs r = a;
-            r.prof = P.dev + P.off8;
-            r.qpad = qpad_rescue;
-            r.blk_list = (f16 ? listB : listA) + 1;
-            r.blk_count = f16 ? listB : listA;
-            r.rescue_list = nullptr;
-            r.rescue_count = nullptr;
-            HIPCHECK(swk::launch_inter_rescue(r, affine, h->stream));
-            ++h->launches;
+        if (intra_tail) {
+            HIPCHECK(hipStreamWaitEvent(ts, h->side_done, 0));
+            if ((rc = launch_intra_tail(ts, db->d_rlbnd_h, db->d_rlbnd_f))) return rc;
         }
+        HIPCHECK(hipEventRecord(h->tail_done[par], ts));
+        h->tail_pending[par] = true;
+        sw_handle::ProfSlot& S = h->prof[P.slot];
+        HIPCHECK(hipEventRecord(S.tail_read, ts));
+        S.tail_pending = true;
     }
     if (!db->nblocks)
         for (int k = 6; k < 8; ++k) MARK(k, h->stream);
     // (the merged launch has no separate inter end, nor a side stream to join)
     if (!lpt) MARK(2, h->stream);
     if (db->nlong && !lpt) HIPCHECK(hipStreamWaitEvent(h->stream, h->ev[1], 0));
+    if (!deferred)  // the scan completes on the handle's stream: so do earlier deferred tails
+        for (int q = 0; q < 2; ++q)
+            if (h->tail_pending[q]) {
+                HIPCHECK(hipStreamWaitEvent(h->stream, h->tail_done[q], 0));
+                h->tail_pending[q] = false;
+            }
     MARK(3, h->stream);
     h->evpool[h->nscans - 1].launches = h->launches;
     h->timed = true;
     if (std::getenv("SW_RESCUE_STATS")) {  // diagnostics: what the guard bands flagged (synchronises)
         HIPCHECK(hipStreamSynchronize(h->stream));
+        HIPCHECK(hipStreamSynchronize(h->tail));
         int32_t cA = 0, cB = 0, l1 = 0, l2 = 0;
         std::vector<int32_t> ids;
-        if (db->d_rescue) {
-            HIPCHECK(hipMemcpy(&cA, db->d_rescue, 4, hipMemcpyDeviceToHost));
-            HIPCHECK(hipMemcpy(&cB, db->d_rescue + db->nblocks + 1, 4, hipMemcpyDeviceToHost));
+        if (listA) {
+            HIPCHECK(hipMemcpy(&cA, listA, 4, hipMemcpyDeviceToHost));
+            HIPCHECK(hipMemcpy(&cB, listB, 4, hipMemcpyDeviceToHost));
             ids.resize(static_cast<size_t>(cA));
-            if (cA) HIPCHECK(hipMemcpy(ids.data(), db->d_rescue + 1, 4 * ids.size(), hipMemcpyDeviceToHost));
+            if (cA) HIPCHECK(hipMemcpy(ids.data(), listA + 1, 4 * ids.size(), hipMemcpyDeviceToHost));
         }
-        if (db->d_lrescue) {
-            HIPCHECK(hipMemcpy(&l1, db->d_lrescue, 4, hipMemcpyDeviceToHost));
-            HIPCHECK(hipMemcpy(&l2, db->d_lrescue + db->nlong + 1, 4, hipMemcpyDeviceToHost));
+        if (list1) {
+            HIPCHECK(hipMemcpy(&l1, list1, 4, hipMemcpyDeviceToHost));
+            HIPCHECK(hipMemcpy(&l2, list2, 4, hipMemcpyDeviceToHost));
         }
         int64_t res = 0;
         int32_t wmin = 1 << 30, wmax = 0, bmin = 1 << 30, bmax = -1;
@@ -1467,10 +1707,17 @@ int sw_create(int32_t device, sw_handle** out) {
     // reference scoring 12,840 -> 8,900 GCUPS).
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side2, hipStreamNonBlocking);
-    for (auto& S : h->prof)
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking);
+    for (hipEvent_t* ev : {&h->main_done, &h->side_done, &h->tail_done[0], &h->tail_done[1]})
+        if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    for (auto& S : h->prof) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&S.copied, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&S.tail_read, hipEventDisableTiming);
+    }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->coop_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->fork2, hipEventDisableTiming);
+    for (auto& ev : h->stage_ev)
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (e != hipSuccess) { delete h; return fail(SW_E_HIP, hipGetErrorString(e)); }
     *out = h;
     return SW_OK;
@@ -1485,15 +1732,24 @@ int sw_destroy(sw_handle* h) {
             if (ev) (void)hipEventDestroy(ev);
     if (h->side) (void)hipStreamSynchronize(h->side);
     if (h->side2) (void)hipStreamSynchronize(h->side2);
+    if (h->tail) (void)hipStreamSynchronize(h->tail);
     for (auto& S : h->prof) {
         if (S.d) (void)hipFree(S.d);
         if (S.h) (void)hipHostFree(S.h);
         if (S.copied) (void)hipEventDestroy(S.copied);
+        if (S.tail_read) (void)hipEventDestroy(S.tail_read);
     }
     if (h->d_scores) (void)hipFree(h->d_scores);
     if (h->d_topk_work) (void)hipFree(h->d_topk_work);
+    for (int b = 0; b < 2; ++b) {
+        if (h->stage[b]) (void)hipHostFree(h->stage[b]);
+        if (h->stage_ev[b]) (void)hipEventDestroy(h->stage_ev[b]);
+    }
     if (h->side) (void)hipStreamDestroy(h->side);
     if (h->side2) (void)hipStreamDestroy(h->side2);
+    if (h->tail) (void)hipStreamDestroy(h->tail);
+    for (hipEvent_t ev : {h->main_done, h->side_done, h->tail_done[0], h->tail_done[1]})
+        if (ev) (void)hipEventDestroy(ev);
     if (h->coop_done) (void)hipEventDestroy(h->coop_done);
     if (h->fork2) (void)hipEventDestroy(h->fork2);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
@@ -1533,7 +1789,7 @@ int sw_db_create(sw_handle* h, const uint8_t* residues, const int64_t* offsets, 
     db->h = h;
     db->n = n;
     try {
-        db->h_residues.assign(residues, residues + total);
+        db->h_residues.resize(static_cast<size_t>(total));
         db->h_offsets.assign(offsets, offsets + n + 1);
         if (n == 0) db->h_offsets.assign(1, 0);
         db->h_ids.resize(n);
@@ -1542,11 +1798,20 @@ int sw_db_create(sw_handle* h, const uint8_t* residues, const int64_t* offsets, 
         delete db;
         return fail(SW_E_NOMEM, "out of host memory");
     }
-    for (int64_t k = 0; k < total; ++k)
-        if (db->h_residues[k] >= SW_ALPHABET) {
-            delete db;
-            return fail(SW_E_INVALID, "residue code out of range (use sw_encode)");
-        }
+    // copy and validate in parallel 1 MiB pieces
+    constexpr int64_t kPiece = int64_t(1) << 20;
+    std::atomic<bool> bad{false};
+    parallel_for((total + kPiece - 1) / kPiece, [&](int64_t c) {
+        const int64_t lo = c * kPiece, hi = std::min(total, lo + kPiece);
+        std::memcpy(db->h_residues.data() + lo, residues + lo, static_cast<size_t>(hi - lo));
+        uint8_t m = 0;
+        for (int64_t k = lo; k < hi; ++k) m = std::max(m, residues[k]);
+        if (m >= SW_ALPHABET) bad = true;
+    }, 1);
+    if (bad) {
+        delete db;
+        return fail(SW_E_INVALID, "residue code out of range (use sw_encode)");
+    }
     db->residues = total;
     for (int64_t k = 0; k < n; ++k) {
         db->max_len = std::max<int32_t>(db->max_len, static_cast<int32_t>(offsets[k + 1] - offsets[k]));
@@ -1584,10 +1849,8 @@ int sw_db_save(const sw_db* db, const char* path) {
     if (!db || !path) return fail(SW_E_INVALID, "null argument");
     // length-sorted (descending, stable), ids kept: loading gives identical scores[id]
     const int64_t n = db->n;
-    std::vector<int64_t> order(n);
-    std::iota(order.begin(), order.end(), 0);
+    const std::vector<int64_t> order = length_order(db->h_offsets, n);
     auto len = [&](int64_t k) { return db->h_offsets[k + 1] - db->h_offsets[k]; };
-    std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return len(x) > len(y); });
     std::vector<int64_t> offs(n + 1, 0);
     std::vector<int32_t> ids(n);
     std::vector<uint8_t> res(static_cast<size_t>(db->residues));
@@ -1713,6 +1976,7 @@ int sw_db_free(sw_db* db) {
     (void)hipSetDevice(db->h->device);
     (void)hipStreamSynchronize(db->h->stream);
     if (db->h->side) (void)hipStreamSynchronize(db->h->side);
+    if (db->h->tail) (void)hipStreamSynchronize(db->h->tail);
     if (db->h_trace) {  // the last scan's block timeline (tail analysis builds)
         if (const char* path = std::getenv("SW_TRACE_FILE"))
             if (FILE* f = std::fopen(path, "wb")) {
@@ -1758,6 +2022,7 @@ int sw_db_set_long_threshold(sw_db* db, int32_t threshold) {
     HIPCHECK(hipSetDevice(db->h->device));
     HIPCHECK(hipStreamSynchronize(db->h->stream));
     if (db->h->side) HIPCHECK(hipStreamSynchronize(db->h->side));
+    if (db->h->tail) HIPCHECK(hipStreamSynchronize(db->h->tail));
     free_dev(db);
     db->long_threshold = t;
     return build_db(db);
@@ -1804,9 +2069,10 @@ int sw_scan_batch_device(sw_handle* h, const sw_db* db, const uint8_t* queries, 
     const size_t n = static_cast<size_t>(db->max_id + 1);
     // back to back on the handle's stream: no host synchronisation between
     // queries (profiles go through the slot ring), so the GPU never idles
+    // ... and each query's rescue tail runs beside the next query's passes
     for (int32_t k = 0; k < nq; ++k)
         if ((rc = scan_impl(h, db, queries + qoffsets[k], static_cast<int32_t>(qoffsets[k + 1] - qoffsets[k]), sc,
-                            scores_dev + k * n)))
+                            scores_dev + k * n, k + 1 < nq)))
             return rc;
     return SW_OK;
 }

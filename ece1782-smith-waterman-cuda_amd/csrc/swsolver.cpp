@@ -13,7 +13,7 @@
 // 384-390), uploaded, scanned and freed per call, like the reference does
 // (it re-packs per call too, SWSolver.cu:301-371).  Flattening + encoding
 // runs on the host's cores; sw_solver_last_timing() splits the call into
-// flatten / upload (pack + H2D) / scan.
+// flatten / device start-up (first call only) / upload (pack + H2D) / scan.
 #include <sys/time.h>
 
 #include <algorithm>
@@ -142,9 +142,13 @@ std::vector<int32_t> score_all(FASTAQuery& query, const Flat& f, bool char_compa
     int8_t mat[625];
     if (char_compat) check(sw_builtin_matrix(SW_MATRIX_BLOSUM50_CHAR, mat), "sw_builtin_matrix");
     const sw_scoring sc = {char_compat ? mat : nullptr, 2, 2};
+    // device start-up (HIP runtime, handle or group) is timed on its own
     double t0 = now_s();
-    if (gpus() == 1) {
-        sw_handle* h = handle();
+    sw_handle* h = gpus() == 1 ? handle() : nullptr;
+    sw_group* g = gpus() == 1 ? nullptr : group();
+    g_timing.init_s = now_s() - t0;
+    t0 = now_s();
+    if (h) {
         sw_db* db = nullptr;
         check(sw_db_create(h, f.residues.data(), f.offsets.data(), n, nullptr, &db), "sw_db_create");
         g_timing.upload_s = now_s() - t0;
@@ -154,7 +158,6 @@ std::vector<int32_t> score_all(FASTAQuery& query, const Flat& f, bool char_compa
         sw_db_free(db);
         check(rc, "sw_scan");
     } else {
-        sw_group* g = group();
         sw_gdb* db = nullptr;
         check(sw_group_db_create(g, f.residues.data(), f.offsets.data(), n, nullptr, &db), "sw_group_db_create");
         g_timing.upload_s = now_s() - t0;

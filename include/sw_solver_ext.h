@@ -16,9 +16,10 @@
  * resident shards) and scan (kernels + D2H of the scores). */
 struct sw_solver_timing {
     double flatten_s;
-    double upload_s;
+    double upload_s;  /* sw_db_create: host packing + H2D of the database */
     double scan_s;
     int gpus;
+    double init_s;    /* device start-up (HIP runtime, handle / group): the first call only */
 };
 sw_solver_timing sw_solver_last_timing();
 

@@ -337,6 +337,37 @@ def test_batch_all_shipped_queries_c3(sw, oracle, handle):
         assert np.array_equal(out[k], want), (QUERIES[k], np.nonzero(out[k] != want)[0][:10])
 
 
+@pytest.mark.parametrize("scoring", [(0, 2, 2), (1, 12, 1)])
+def test_batch_rescue_tails_overlap(sw, oracle, handle, scoring):
+    """A rescue-heavy batch: long queries under the reference's cheap linear
+    gaps (BLOSUM50 / 2: the widest blocks and most long subjects cross the
+    fp16 guard band) and BLOSUM62 11/1, planted near-copies scoring above
+    2048 and above 32767 in both the inter and the intra part.  In a batch
+    each query's rescue tail runs on the tail stream beside the next query's
+    fp16 passes (parity lists, own boundary rows, profile slots reused after
+    4 queries): every query equals the oracle and its single-query scan,
+    twice (the second batch takes the adaptive int16 paths)."""
+    mid, go, ge = scoring
+    names = ["Q9UKN1", "P02232", "P20930", "P04775", "Q9UKN1", "P07327", "P33450"]
+    qs = [sw.encode(read_query(n)) for n in names]
+    r, o = sw.synth.database(1500, shard=31)
+    big = qs[0]
+    extra = [big, big[:1000], qs[2][:1500], qs[6][200:1100]]  # intra / inter near-copies
+    r2 = np.concatenate([r] + extra)
+    o2 = np.concatenate([o, o[-1] + np.cumsum([len(x) for x in extra])])
+    db = sw.Database(handle, r2, o2, long_threshold=1200)
+    m = sw.capi.builtin_matrix(mid)
+    want = [oracle.scan(q, r2, o2, mat=m, gap_open=go, gap_extend=ge, nthreads=16) for q in qs]
+    for _ in range(2):
+        out = db.scan_batch(qs, m, go, ge)
+        for k in range(len(qs)):
+            assert np.array_equal(out[k], want[k]), (names[k], np.nonzero(out[k] != want[k])[0][:10])
+    for k in (0, 3):
+        assert np.array_equal(db.scan(qs[k], m, go, ge), want[k])
+    if mid == 0:
+        assert max(int(w.max()) for w in want) > 32767  # the int32 stage ran
+
+
 def test_db_save_load_roundtrip(sw, oracle, handle, tmp_path):
     """sw_db_save / sw_db_load: identical scores[id], custom ids kept, bad
     files rejected."""
