@@ -248,19 +248,20 @@ struct sw_handle {
     hipEvent_t coop_done = nullptr;
     hipEvent_t fork2 = nullptr;  // side2 starts after the rescue counters are reset
     // per-query workspace: profiles (inter: [32][stride]; intra: lane-slotted
-    // chunks) built in pinned host buffers, copied once per query
-    // A ring of profile slots (pinned staging + device copy): building the
-    // next query's profile waits only for the H2D copy made kProfSlots scans
-    // ago, not for the scans still running, so back-to-back scans
-    // (sw_scan_batch*) keep the GPU busy.
+    // chunks) built on the device by the scan's first launch.  A ring of
+    // slots: a deferred rescue tail (batches) may still read the profiles of
+    // the scan before while the next scan builds its own.  Reusing a slot
+    // waits until the scan that last used it has started on the device, so
+    // the host runs at most kProfSlots scans ahead of the GPU: the adaptive
+    // choices (the fp16 passes' flagged counts read back without waiting,
+    // scan_impl) then see scans a few queries back instead of none at all
+    // when many scans are enqueued at once.
     struct ProfSlot {
         int8_t* d = nullptr;
         size_t dcap = 0;
-        int8_t* h = nullptr;
-        size_t hcap = 0;
-        hipEvent_t copied = nullptr;  // the staging buffer may be rewritten after this
+        hipEvent_t built = nullptr;      // this slot's last scan started (its profiles are built)
         bool pending = false;
-        hipEvent_t tail_read = nullptr;  // a deferred rescue tail has read the device copy
+        hipEvent_t tail_read = nullptr;  // a deferred rescue tail has read the slot
         bool tail_pending = false;
     };
     // pinned staging of database uploads (build_db): the host packs one
@@ -815,8 +816,12 @@ struct Profiles {
     int slot = 0;            // the handle's profile slot holding them
 };
 
+// Built on the device (swk::sw_build_profile, one launch per 2,048 query
+// rows; the first also zeroes the rescue lists' counters `reset`) in one of
+// the handle's profile slots, on the scan's stream.
 int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* mat, int go, bool affine,
-                   int32_t qpad_inter, bool want16, int ri, int32_t qpad_intra, Profiles* P) {
+                   int32_t qpad_inter, bool want16, int ri, int32_t qpad_intra, int32_t* const (&reset)[5],
+                   Profiles* P) {
     for (int32_t i = 0; i < qlen; ++i)
         if (q[i] >= SW_ALPHABET) return fail(SW_E_INVALID, "query residue code out of range (use sw_encode)");
     const int bias = affine ? 0 : go;
@@ -837,57 +842,47 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     P->slot = h->prof_next;
     sw_handle::ProfSlot& S = h->prof[h->prof_next];
     h->prof_next = (h->prof_next + 1) % sw_handle::kProfSlots;
-    if (S.pending) HIPCHECK(hipEventSynchronize(S.copied));  // its last copy has consumed the staging buffer
+    if (S.pending) HIPCHECK(hipEventSynchronize(S.built));
     S.pending = false;
-    if (P->total > S.hcap) {
-        if (S.h) HIPCHECK(hipHostFree(S.h));
-        S.hcap = std::max<size_t>(P->total, 1 << 16);
-        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&S.h), S.hcap, hipHostMallocDefault));
-    }
     if (P->total > S.dcap) {
         if (S.d) {
             HIPCHECK(hipStreamSynchronize(h->stream));  // scans in flight may still read it
+            if (S.tail_pending) HIPCHECK(hipEventSynchronize(S.tail_read));
+            S.tail_pending = false;
             HIPCHECK(hipFree(S.d));
         }
         S.dcap = std::max<size_t>(P->total, 1 << 16);
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&S.d), S.dcap));
     }
     P->dev = S.d;
-    int8_t* hp = S.h;
-    auto value = [&](int c, int64_t row) -> int {
-        if (c >= SW_ALPHABET || row >= qlen) return bias;
-        return mat[25 * q[row] + c] + bias;
-    };
-    int8_t* p8 = hp + P->off8;
-    int16_t* p16 = reinterpret_cast<int16_t*>(hp + P->off16);
-    for (int c = 0; c < swk::kProfileRows; ++c)
-        for (int32_t i = 0; i < P->stride; ++i) {
-            const int v = value(c, i);
-            const size_t k = static_cast<size_t>(c) * P->stride + i;
-            p8[k] = static_cast<int8_t>(v);
-            if (want16) p16[k] = static_cast<int16_t>(v);
-        }
-    if (ri) {
-        const int64_t CH = static_cast<int64_t>(swk::kLanes) * ri;
-        int8_t* ip = hp + P->intra_off;
-        const int64_t nch = qpad_intra / CH;
-        for (int64_t ch = 0; ch < nch; ++ch)
-            for (int c = 0; c < swk::kProfileRows; ++c)
-                for (int t = 0; t < swk::kLanes; ++t) {
-                    int8_t* d = ip + ((ch * swk::kProfileRows + c) * swk::kLanes + t) * rip;
-                    for (int r = 0; r < rip; ++r) d[r] = static_cast<int8_t>(r < ri ? value(c, ch * CH + t * ri + r) : 0);
-                }
-    }
     // on the scan's stream: after the scans before it (the slot's last
-    // reader among them), before this one.  (A copy stream of its own, to
-    // overlap the copy with the running scan, measured no faster and costs
-    // a hardware queue: see sw_create.)
+    // reader among them), before this one
     if (S.tail_pending) {  // a deferred tail still reads the slot's last profiles
         HIPCHECK(hipStreamWaitEvent(h->stream, S.tail_read, 0));
         S.tail_pending = false;
     }
-    HIPCHECK(hipMemcpyAsync(S.d, hp, P->total, hipMemcpyHostToDevice, h->stream));
-    HIPCHECK(hipEventRecord(S.copied, h->stream));
+    swk::ProfileArgs a{};
+    a.p8 = S.d + P->off8;
+    a.p16 = want16 ? reinterpret_cast<int16_t*>(S.d + P->off16) : nullptr;
+    a.pin = ri ? S.d + P->intra_off : nullptr;
+    a.stride = P->stride;
+    a.qlen = qlen;
+    a.bias = bias;
+    a.ri = ri;
+    a.rip = rip;
+    a.qpad_intra = ri ? qpad_intra : 0;
+    for (int k = 0; k < 5; ++k) a.reset[k] = reset[k];
+    std::memcpy(a.mat, mat, 625);
+    const int32_t rows = std::max(P->stride, a.qpad_intra);
+    for (int32_t r0 = 0; r0 < rows; r0 += swk::kProfQueryChunk) {
+        a.row0 = r0;
+        a.row1 = std::min(rows, r0 + swk::kProfQueryChunk);
+        const int32_t nq = std::max(0, std::min(a.row1, qlen) - r0);
+        if (nq) std::memcpy(a.q, q + r0, static_cast<size_t>(nq));
+        HIPCHECK(swk::launch_build_profile(a, h->stream));
+        for (auto& p : a.reset) p = nullptr;  // once
+    }
+    HIPCHECK(hipEventRecord(S.built, h->stream));
     S.pending = true;
     return SW_OK;
 }
@@ -1217,10 +1212,6 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     db->last_npair = npair;
     db->last_pair_merged = npair != 0;
     const int32_t qpad_coop = ncoop ? static_cast<int32_t>(round_up(qlen, swk::inter_coop_rows())) : 0;
-    if ((rc = build_profiles(h, query, qlen, mat, go, affine,
-                             std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2}),
-                             x2 || intra_x2, ri, qpad_intra, &P)))
-        return rc;
     const int64_t rstride = 2 * (db->nblocks + 1) + 2;  // lists A and B, the largest flagged block
     const int64_t lstride = 2 * (db->nlong + 1);        // intra lists 1 and 2
     if (rescue && db->nblocks && !db->d_rescue) {
@@ -1251,16 +1242,18 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     const bool deferred = defer && (!(multi_inter || multi_intra) || ensure_rbnd(db));
     hipStream_t const ts = deferred ? h->tail : h->stream;
 
-    // the rescue lists' counters (inter A, B, largest flagged block; intra
-    // 1, 2) in one launch instead of five memsets, before the fork so the
-    // side stream sees them
+    // the profiles, and the rescue lists' counters (inter A, B, largest
+    // flagged block; intra 1, 2) zeroed by the same launch, before the fork
+    // so the side streams see them
     {
-        int32_t* cA = (rescue && db->nblocks) ? listA : nullptr;
-        int32_t* cB = (cA && f16) ? listB : nullptr;
-        int32_t* mA = (cA && f16) ? maxA : nullptr;
-        int32_t* c1 = (db->nlong && intra_x2) ? list1 : nullptr;
-        int32_t* c2 = c1 ? list2 : nullptr;
-        if (cA || c1) HIPCHECK(swk::launch_reset_counters(cA, cB, mA, c1, c2, h->stream));
+        int32_t* const cA = (rescue && db->nblocks) ? listA : nullptr;
+        int32_t* const c1 = (db->nlong && intra_x2) ? list1 : nullptr;
+        int32_t* const reset[5] = {cA, (cA && f16) ? listB : nullptr, (cA && f16) ? maxA : nullptr, c1,
+                                   c1 ? list2 : nullptr};
+        if ((rc = build_profiles(h, query, qlen, mat, go, affine,
+                                 std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2}),
+                                 x2 || intra_x2, ri, qpad_intra, reset, &P)))
+            return rc;
     }
     // One merged launch for the fp16 scan, longest work first (sw_scan_lpt):
     // the inter groups + single waves and the long subjects' fp16 pass, when
@@ -1711,8 +1704,8 @@ int sw_create(int32_t device, sw_handle** out) {
     for (hipEvent_t* ev : {&h->main_done, &h->side_done, &h->tail_done[0], &h->tail_done[1]})
         if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     for (auto& S : h->prof) {
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&S.copied, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&S.tail_read, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&S.built, hipEventDisableTiming);
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->coop_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->fork2, hipEventDisableTiming);
@@ -1735,9 +1728,8 @@ int sw_destroy(sw_handle* h) {
     if (h->tail) (void)hipStreamSynchronize(h->tail);
     for (auto& S : h->prof) {
         if (S.d) (void)hipFree(S.d);
-        if (S.h) (void)hipHostFree(S.h);
-        if (S.copied) (void)hipEventDestroy(S.copied);
         if (S.tail_read) (void)hipEventDestroy(S.tail_read);
+        if (S.built) (void)hipEventDestroy(S.built);
     }
     if (h->d_scores) (void)hipFree(h->d_scores);
     if (h->d_topk_work) (void)hipFree(h->d_topk_work);

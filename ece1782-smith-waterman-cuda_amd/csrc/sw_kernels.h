@@ -228,11 +228,34 @@ struct SynthFill {
 hipError_t launch_synth_fill(const SynthFill& f, hipStream_t s);
 uint64_t synth_hash(uint64_t seed, uint64_t id, uint64_t k);
 
+// Query profiles built on the device (sw_profile.hip) from the query codes
+// and the matrix in the kernel arguments: rows [row0, row1) per launch (at
+// most kProfQueryChunk), q[] = the codes of rows [row0, min(row1, qlen)).
+//   p8  : [kProfileRows][stride] int8, S + bias (rows >= qlen, codes >= 25: bias)
+//   p16 : the same values as int16 (null: not built)
+//   pin : the int32 intra kernel's lane-slotted image, rows < qpad_intra:
+//         [chunk of 64 ri rows][code][lane][rip] (null: not built)
+// The first launch also zeroes the rescue lists' counters (reset[2] := -1,
+// the largest-flagged-block slot; null pointers skipped).
+constexpr int kAlphabet = 25;
+constexpr int kProfQueryChunk = 2048;
+struct ProfileArgs {
+    int8_t* p8;
+    int16_t* p16;
+    int8_t* pin;
+    int32_t stride;
+    int32_t qlen;
+    int32_t row0, row1;
+    int32_t bias;
+    int32_t ri, rip, qpad_intra;
+    int32_t* reset[5];
+    int8_t mat[kAlphabet * kAlphabet + 15];
+    uint8_t q[kProfQueryChunk];
+};
+hipError_t launch_build_profile(const ProfileArgs& a, hipStream_t s);
+
 // Device top-K (sw_topk.hip): keys = score << 32 | (2^31 - 1 - id), best first.
 size_t topk_workspace_bytes(int64_t n, int k);
-// One thread zeroes the rescue lists' counters (c = -1: a largest-id slot);
-// null pointers are skipped.
-hipError_t launch_reset_counters(int32_t* a, int32_t* b, int32_t* c, int32_t* d, int32_t* e, hipStream_t s);
 hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, const int32_t* ids, int k,
                        int64_t* out, int64_t* work, hipStream_t s);
 

@@ -187,21 +187,6 @@ __global__ __launch_bounds__(kTopkThreads) void sw_topk_select(const int32_t* __
     }
 }
 
-__global__ void sw_reset_counters(int32_t* a, int32_t* b, int32_t* c, int32_t* d, int32_t* e) {
-    if (threadIdx.x == 0) {
-        if (a) *a = 0;
-        if (b) *b = 0;
-        if (c) *c = -1;
-        if (d) *d = 0;
-        if (e) *e = 0;
-    }
-}
-
-hipError_t launch_reset_counters(int32_t* a, int32_t* b, int32_t* c, int32_t* d, int32_t* e, hipStream_t s) {
-    hipLaunchKernelGGL(sw_reset_counters, dim3(1), dim3(64), 0, s, a, b, c, d, e);
-    return hipGetLastError();
-}
-
 // Workspace bytes sw_topk_device needs for n inputs and k outputs.
 size_t topk_workspace_bytes(int64_t n, int k) {
     size_t total = 0;
