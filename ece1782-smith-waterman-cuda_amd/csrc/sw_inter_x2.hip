@@ -410,57 +410,9 @@ __device__ __forceinline__ void x2s_finish(const InterArgs& a, int blk, int lane
 }
 
 
-// LDS ring between consecutive waves of a group (sw_inter_x2p): kRingSlots
+// LDS ring between the two waves of a pair (sw_inter_x2p): kRingSlots
 // sub-groups of boundary dwords, lane-contiguous int4s (conflict-free b128).
-// Six slots let a producer run up to seven sub-groups ahead of its consumer
-// (LDS: 73 KB per quad workgroup, still two workgroups per CU).
-constexpr int kRingSlots = 6;
-
-// Progress of the waves of a group (sw_inter_x2p), without a workgroup
-// barrier: each wave publishes the number of sub-group iterations it has
-// completed (over all its passes, S per pass) in an LDS counter, and a wave
-// waits on a counter only where it reads what another wave wrote (or is
-// about to overwrite what another has not read yet):
-//   * sub-group g of a pass's row -1 input (LDS ring from the wave before,
-//     or HBM from the group's last wave of the previous round) is written
-//     at the end of the producer's iteration g + 1 of the feeding pass, so
-//     its reader waits for  prod >= pb + g + 2  (pb: the producer's count
-//     at the start of that pass);
-//   * ring slot (it0 + g) % kRingSlots last held sequence it0 + g - 6, read
-//     once the consumer has completed  it0 + g - 5  iterations.
-// The release (publish) / acquire (wait) pair orders the ring's LDS writes
-// and the HBM boundary stores before the reads.  Waves wait with s_sleep so
-// the other waves of the SIMD issue meanwhile; every wait is on a wave of
-// the same workgroup (all resident) further up the dependency chain, which
-// ends at the group's last wave (no back-pressure): no cycle.
-struct GroupSync {
-    uint32_t* self;         // this wave's counter
-    const uint32_t* prod;   // the wave whose boundary this pass reads (null: first pass)
-    const uint32_t* cons;   // the wave reading this pass's ring (null: HBM out / none)
-    uint32_t it0;           // this wave's count at the pass start (= the consumer's)
-    uint32_t pb;            // the producer's count at the start of the feeding pass
-    uint32_t seen_p = 0, seen_c = 0;  // last observed values (wave-uniform)
-};
-
-__device__ __forceinline__ void gs_wait(const uint32_t* c, uint32_t need, uint32_t& seen) {
-    while (seen < need) {
-        seen = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (seen < need) __builtin_amdgcn_s_sleep(1);
-    }
-}
-
-__device__ __forceinline__ void gs_publish(uint32_t* c, uint32_t v, int lane) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_store(c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-__device__ __forceinline__ int ring_slot(uint32_t seq) { return static_cast<int>(seq % kRingSlots); }
-#ifndef SW_GROUP_LAG
-#define SW_GROUP_LAG 2
-#endif
-constexpr int kGroupLag = SW_GROUP_LAG;
-static_assert(kGroupLag >= 2 && kGroupLag <= kRingSlots, "group lag");
+constexpr int kRingSlots = 4;
 
 template <int SG>
 __device__ __forceinline__ void ring_store(int4* ring, int slot, int lane, const uint32_t (&v)[SG]) {
@@ -482,9 +434,9 @@ __device__ __forceinline__ void ring_load(uint32_t (&v)[SG], const int4* ring, i
 }
 
 // One pass (rows [s0, s0 + 2R)) of one 64-subject block.  PAIR: the pass
-// is part of a wave group's pipeline (sw_inter_x2p): the boundary comes from /
-// goes to the neighbouring wave through an LDS ring instead of HBM when
-// ring_in / ring_out are set, ordered by the group's progress counters (gs).
+// is part of a wave pair's pipeline (sw_inter_x2p): the boundary comes from /
+// goes to the partner wave through an LDS ring instead of HBM when ring_in /
+// ring_out are set, and every sub-group ends with one workgroup barrier (a tick).
 //
 // CHAIN (single-wave blocks): all passes of the block in ONE sweep over
 // npass x ncols virtual columns.  The low strip enters pass k at virtual
@@ -498,7 +450,7 @@ __device__ __forceinline__ void ring_load(uint32_t (&v)[SG], const int4* ring, i
 template <int R, int SG, bool AFFINE, bool F16, bool PAIR, int CR = 16, bool CHAIN = false>
 __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32_t ncols, uint64_t base, int lane,
                                          int s0, Best<F16>& best, const int4* ring_in, int4* ring_out,
-                                         GroupSync* gs) {
+                                         int* tick) {
     static_assert(!(CHAIN && PAIR), "chained passes: single-wave blocks only");
     // SG: sub-group width = the lag (columns) between the two strips
     // CR: profile rows per LDS chunk (16: 2 x 4 ds_read_b128 in flight; 8
@@ -561,13 +513,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     for (int q = 0; q < SG / 4; ++q) rp[q] = 0x19191919u;  // virtual columns before the subject
     load_codes<SG>(rc, a.residues + base, true);
     if (!first) {
-        // a ring consumer starts kGroupLag sub-groups behind its producer (at
-        // least 2: the data dependency), so a short stall of the producer
-        // does not stall it too
-        if constexpr (PAIR)
-            gs_wait(gs->prod, gs->pb + (ring_in ? min(static_cast<uint32_t>(kGroupLag), ncols / SG + 1) : 2u),
-                    gs->seen_p);
-        if (PAIR && ring_in) ring_load<SG>(bin, ring_in, ring_slot(gs->it0), lane);
+        if (PAIR && ring_in) ring_load<SG>(bin, ring_in, 0, lane);
         else load_pairs<SG>(bin, reinterpret_cast<const int32_t*>(bnd) + base);
     }
     int4 PL[2][CQ], PH[2][CQ];
@@ -635,8 +581,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
         if (has_next) {
             load_codes<SG>(rn, a.residues + base + noff, next_lo);
             if (!next_first && next_lo) {
-                if constexpr (PAIR) gs_wait(gs->prod, gs->pb + ncol / SG + 2, gs->seen_p);
-                if (PAIR && ring_in) ring_load<SG>(bin_n, ring_in, ring_slot(gs->it0 + ncol / SG), lane);
+                if (PAIR && ring_in) ring_load<SG>(bin_n, ring_in, (ncol / SG) % kRingSlots, lane);
                 else load_pairs<SG>(bin_n, reinterpret_cast<const int32_t*>(bnd) + base + noff);
             }
         }
@@ -779,9 +724,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
             for (int q = 0; q < SG; ++q) hb[q] = AFFINE ? hi_hi(dl_h[q], dl_f[q]) : (dl_h[q] >> 16);
             const uint32_t pc = CHAIN ? (lo_c == 0 ? ncols - SG : lo_c - SG) : col0 - SG;
             if (PAIR && ring_out) {
-                const uint32_t seq = gs->it0 + pc / SG;
-                if (seq + 1 > kRingSlots) gs_wait(gs->cons, seq + 1 - kRingSlots, gs->seen_c);
-                ring_store<SG>(ring_out, ring_slot(seq), lane, hb);
+                ring_store<SG>(ring_out, (pc / SG) % kRingSlots, lane, hb);
             } else {
                 const uint64_t poff = (pc >> 4) * kGroupBytes + (pc & 15);
                 store_pairs<SG>(reinterpret_cast<int32_t*>(bnd) + base + poff, hb);
@@ -796,7 +739,10 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
 #pragma unroll
             for (int q = 0; q < SG; ++q) bin[q] = (next_first || !next_lo) ? bz[q] : bin_n[q];
         }
-        if constexpr (PAIR) gs_publish(gs->self, gs->it0 + col0 / SG + 1, lane);
+        if constexpr (PAIR) {
+            __syncthreads();  // one tick of the pair's clock
+            ++*tick;
+        }
         if constexpr (CHAIN) {
             t2 = t1;
             lo_c = nreal;
@@ -835,19 +781,25 @@ __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>&
 // ragged round of short ones) bound the scan (profiles/r01_tail/).  Here the
 // G waves of a group (G = 2: a pair, two groups per workgroup; G = 4: a quad,
 // the whole workgroup) split the passes: wave w runs passes w, w + G,
-// w + 2G, ..., about three sub-groups behind wave w - 1.  Within a round the
+// w + 2G, ..., kPairLag sub-groups behind wave w - 1.  Within a round the
 // boundary (H | F << 16) goes from wave w to wave w + 1 through an LDS ring;
 // from one round to the next (wave G-1 -> wave 0) through HBM as in the
-// single-wave kernel.  The waves synchronise only through the progress
-// counters of GroupSync (a wave waits where it reads what another wrote):
-// until round 3 every sub-group ended with a workgroup barrier, so each of
-// the four waves ran at the pace of the slowest of them, sub-group by
-// sub-group.  Block latency drops from P x S to about ceil(P / G) x S + 3
-// (G - 1) sub-groups for P passes of S.  Pairs take the widest blocks of
-// large databases; quads those of
+// single-wave kernel.  All four waves of the workgroup share one clock: one
+// __syncthreads per sub-group.  Schedule of a block whose pass takes
+// S = width / SG + 1 ticks: round r of wave w starts at tick
+// r * max(S, G kPairLag) + kPairLag w, so
+//   * wave w + 1 reads sub-group g of a ring 2 ticks after wave w wrote it and
+//     wave w overwrites that slot only 3 ticks after the read (4 slots); a
+//     new round's first write comes after the old round's last read;
+//   * wave 0 of round r+1 prefetches from HBM what wave G-1 of round r stored
+//     at least one tick earlier (period >= G kPairLag).
+// Block latency drops from P x S to ceil(P / G) x S + kPairLag (G - 1)
+// ticks for P passes; the extra cost is one barrier per sub-group and the
+// idle lag.  Pairs take the widest blocks of large databases; quads those of
 // small ones (a rank's share of a strong-scaled database), where too few
 // blocks exist to fill the GPU and the widest block's latency bounds the
 // scan (sw_capi.cpp pair_blocks / pair_group).
+constexpr int kPairLag = 3;
 // Profile rows per LDS chunk in the group launches (the wave groups' passes
 // and the merged launch's single-wave blocks): 8, not the per-wave kernel's
 // 16.  These kernels hold 2 waves per SIMD (LDS and the ring buffers) and
@@ -869,17 +821,24 @@ constexpr int kSingleCR = SW_SINGLE_CR;
 #endif
 constexpr int kGroupWavesPerEU = SW_GROUP_WAVES_PER_EU;
 
+__device__ __forceinline__ int group_ticks(uint32_t ncols, int passes, int SG, int G) {
+    if (ncols == 0 || passes <= 0) return 0;
+    const int S = static_cast<int>(ncols) / SG + 1;
+    const int per = max(S, G * kPairLag);
+    int t = 0;
+    for (int p = max(0, passes - G); p < passes; ++p) t = max(t, (p / G) * per + kPairLag * (p % G) + S);
+    return t;
+}
+
 // The LDS of one workgroup of the group form: the waves' profile images, the
 // rings between consecutive waves of a group (3 for a quad, 2 for two
-// pairs), the partial maxima, the progress counters.  61 KB for pairs, 73 KB
-// for quads: both still leave 2 workgroups per CU, the register-bound
-// occupancy.
+// pairs), the partial maxima.  53 KB for pairs, 61 KB for quads: both still
+// leave 2 workgroups per CU, the register-bound occupancy.
 template <int R, int SG, int GMAX>
 struct X2pSmem {
     X2Lds<R> lds[kWavesPerWG];
     int4 ring[kWavesPerWG - kWavesPerWG / GMAX][kRingSlots * (SG / 4) * kLanes];
     uint32_t part[kWavesPerWG][kLanes];
-    uint32_t cnt[kWavesPerWG];
 };
 
 // One workgroup's work (wgi = its index in the launch's numbering):
@@ -912,33 +871,36 @@ __device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, int quad_end
     const int first = quad ? a.blk_base + wgi : qend + (wgi - qwg) * 2;
     const int gi = wave / G, w = wave % G;
     const int passes = (a.qpad + 2 * R - 1) / (2 * R);
-    (void)NG;
+    // the workgroup's clock runs to the longest of its blocks
+    int tmax = 0;
+    for (int q = 0; q < NG; ++q) {
+        const int b = first + q;
+        if (b < npair) tmax = max(tmax, group_ticks(a.blk_groups[b] * kGroupCols, passes, SG, G));
+    }
     const int blk = first + gi;
     Best<F16> best;
     best.init();
-    if (lane == 0) sm.cnt[wave] = 0;
-    __syncthreads();  // the counters are zero before any wave reads them
+    int tick = 0;
     const uint64_t t0 = trace_now();
     if (blk < npair) {
         const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
         const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
-        const uint32_t S = ncols / SG + 1;  // sub-group iterations per pass
+        const int per = max(static_cast<int>(ncols) / SG + 1, G * kPairLag);
         const int4* rin = w > 0 ? ring[gi * (G - 1) + w - 1] : nullptr;
         int4* rout = w < G - 1 ? ring[gi * (G - 1) + w] : nullptr;
-        GroupSync gs{};
-        gs.self = &sm.cnt[wave];
-        gs.cons = rout ? &sm.cnt[wave + 1] : nullptr;
-        uint32_t r = 0;
-        for (int p = w; p < passes && ncols > 0; p += G, ++r) {
-            gs.it0 = r * S;
-            // row -1 input: the ring from wave w - 1 (same round), or HBM
-            // from the group's last wave (previous round)
-            gs.prod = w > 0 ? &sm.cnt[wave - 1] : (r > 0 ? &sm.cnt[gi * G + G - 1] : nullptr);
-            gs.pb = w > 0 ? r * S : (r > 0 ? (r - 1) * S : 0u);
-            x2s_pass<R, SG, AFFINE, F16, true, kPairCR>(a, lds[wave], ncols, base, lane, p * 2 * R, best, rin, rout, &gs);
+        for (int p = w; p < passes && ncols > 0; p += G) {
+            const int start = (p / G) * per + kPairLag * w;
+            while (tick < start) {
+                __syncthreads();
+                ++tick;
+            }
+            x2s_pass<R, SG, AFFINE, F16, true, kPairCR>(a, lds[wave], ncols, base, lane, p * 2 * R, best, rin, rout, &tick);
         }
     }
-    __syncthreads();  // every wave's passes are done (the maxima below; the LDS for the next workgroup)
+    while (tick < tmax) {
+        __syncthreads();
+        ++tick;
+    }
     if (blk < npair && w > 0) part[wave][lane] = P::bits(best.value(a));
     __syncthreads();
     if (blk < npair && w == 0) {
