@@ -50,59 +50,22 @@ __device__ __forceinline__ s2 usub2(s2 a, u2 g) {
 // 16-byte slots so lanes reading different codes spread over the banks
 __host__ __device__ constexpr int x2_row_dwords(int R) { return (R / 4) % 2 == 1 ? R : R + 4; }
 
+// Profile codes an image holds: the 25 residue codes and the pad code (the
+// database holds no others; sw_db_create validates every byte).
+constexpr int kImgCodes = kPadCode + 1;
+
+// One wave's profile images: `lo` / `hi` for the two strips of a pass.
+// (Copies for column 0 of every sub-group, one sub-group's bias lower, would
+// save the per-sub-group rebase of H: 2 % fewer VALU instructions on C2, but
+// at 77 KB of LDS per pair workgroup the scan ran 2 % SLOWER beside the
+// long-subject kernel, 7.43 against 7.25 ms per step; not kept.)
 template <int R>
-struct X2Lds {
-    uint32_t lo[kProfileRows * x2_row_dwords(R)];
-    uint32_t hi[kProfileRows * x2_row_dwords(R)];
+struct __attribute__((aligned(16))) X2Lds {  // 16-byte aligned: the waves' images are read by ds_read_b128
+    static constexpr int kImg = kImgCodes * x2_row_dwords(R);
+    uint32_t lo[kImg];
+    uint32_t hi[kImg];
 };
-
-// Stage rows [s0, s0+R) of the int16 profile into both images: 32 codes x R
-// rows = 4R int4 loads of 8 rows each, spread over the lanes.
-template <int R>
-__device__ __forceinline__ void stage_x2(X2Lds<R>& L, const int16_t* __restrict__ prof, int stride, int s0,
-                                         int lane) {
-    constexpr int RD = x2_row_dwords(R);
-#pragma unroll
-    for (int t = lane; t < kProfileRows * (R / 8); t += kLanes) {
-        const int c = t / (R / 8);
-        const int k = t % (R / 8);
-        const int4 v = *reinterpret_cast<const int4*>(prof + static_cast<size_t>(c) * stride + s0 + 8 * k);
-        const uint32_t w[4] = {static_cast<uint32_t>(v.x), static_cast<uint32_t>(v.y), static_cast<uint32_t>(v.z),
-                               static_cast<uint32_t>(v.w)};
-        uint32_t l[8], h[8];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            l[2 * e] = w[e] & 0xffffu;
-            l[2 * e + 1] = w[e] >> 16;
-            h[2 * e] = w[e] << 16;
-            h[2 * e + 1] = w[e] & 0xffff0000u;
-        }
-        int4* dl = reinterpret_cast<int4*>(L.lo + c * RD + 8 * k);
-        int4* dh = reinterpret_cast<int4*>(L.hi + c * RD + 8 * k);
-        dl[0] = make_int4(l[0], l[1], l[2], l[3]);
-        dl[1] = make_int4(l[4], l[5], l[6], l[7]);
-        dh[0] = make_int4(h[0], h[1], h[2], h[3]);
-        dh[1] = make_int4(h[4], h[5], h[6], h[7]);
-    }
-}
-
-// 16 rows [16k, 16k+16) of one column from both images (code ca for the low
-// half, cb for the high half).  `dep` ties the read to a value computed by
-// the previous step so the compiler cannot hoist every unrolled read.
-template <int R, int N = 4>
-__device__ __forceinline__ void read_x2(int4 (&pl)[N], int4 (&ph)[N], const X2Lds<R>& L, uint32_t ca, uint32_t cb,
-                                        int k, uint32_t dep) {
-    constexpr int RD = x2_row_dwords(R);
-    uint32_t oa = ca * (RD * 4) + 16 * N * k, ob = cb * (RD * 4) + 16 * N * k;
-    asm volatile("" : "+v"(oa), "+v"(ob) : "v"(dep));
-    const int4* a = reinterpret_cast<const int4*>(reinterpret_cast<const uint8_t*>(L.lo) + oa);
-    const int4* b = reinterpret_cast<const int4*>(reinterpret_cast<const uint8_t*>(L.hi) + ob);
-#pragma unroll
-    for (int q = 0; q < N; ++q) {
-        pl[q] = a[q];
-        ph[q] = b[q];
-    }
-}
+static_assert(sizeof(X2Lds<32>) % 16 == 0 && sizeof(X2Lds<48>) % 16 == 0, "image alignment");
 
 template <int N>
 __device__ __forceinline__ uint32_t word(const int4 (&v)[N], int w) {
@@ -134,6 +97,15 @@ __device__ __forceinline__ void load_codes(uint32_t (&w)[SG / 4], const uint8_t*
 }
 
 __device__ __forceinline__ uint32_t code_of(const uint32_t* w, int jj) { return (w[jj >> 2] >> (8 * (jj & 3))) & 0xffu; }
+
+// LDS byte address base + code(jj) * RB of column jj's profile row in ONE
+// v_dot4_u32_u8 (byte jj & 3 of the code word times RB in the same byte of
+// the constant) instead of a byte extract and a multiply-add
+template <uint32_t RB>
+__device__ __forceinline__ uint32_t code_row(const uint32_t* w, int jj, uint32_t base) {
+    static_assert(RB < 256, "row stride must fit a byte");
+    return __builtin_amdgcn_udot4(w[jj >> 2], RB << (8 * (jj & 3)), base, false);
+}
 
 template <int SG>
 __device__ __forceinline__ void load_pairs(uint32_t (&v)[SG], const int32_t* p) {
@@ -173,66 +145,45 @@ __device__ __forceinline__ uint32_t to_f16_bits(uint32_t v16) {
     return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, static_cast<_Float16>(static_cast<int16_t>(v16))));
 }
 
-// F16: the images hold S + bias (the column-biased cell's gap extension).
-template <int R, bool F16 = false>
+// Stage the profile images of one pass: img 0 (lo) <- rows [s0, s0+R), img 1
+// (hi) <- rows [s0+R, s0+2R), both when img < 0 (2 x 26 codes x R/8 int4
+// loads of 8 rows each, spread over the lanes).  Each dword pairs a row's
+// score with 1 (1.0 in fp16) in the other half: the kernel forms the pair
+// as lo * hi + H_diag in one v_pk_fma_f16 / v_pk_mad_u16.
+// F16: the images hold S + bias (the column-biased cell's gap extension), and
+// the first row of each 16-row group S + bias + bias0: the diagonal entering
+// that row still carries the previous row group's bias, 16 ge above its own
+// (bias0 = -16 ge folds the shift back into the profile; see x2s_pass).
+template <int R, bool F16>
 __device__ __forceinline__ void stage_x2s(X2Lds<R>& L, const int16_t* __restrict__ prof, int stride, int s0,
-                                          int lane, int bias = 0) {
+                                          int lane, int bias, int bias0, int img) {
     constexpr int RD = x2_row_dwords(R);
+    constexpr int PER = kImgCodes * (R / 8);  // int4 loads per image
     constexpr uint32_t one = F16 ? 0x3c00u : 1u;
-    // lo image <- rows [s0, s0+R), hi image <- rows [s0+R, s0+2R)
-#pragma unroll
-    for (int t = lane; t < 2 * kProfileRows * (R / 8); t += kLanes) {
-        const int img = t / (kProfileRows * (R / 8));
-        const int u = t % (kProfileRows * (R / 8));
+    const int n = img < 0 ? 2 * PER : PER;
+    for (int t = lane; t < n; t += kLanes) {
+        const int im = img < 0 ? t / PER : img;
+        const int u = img < 0 ? t % PER : t;
         const int c = u / (R / 8);
         const int k = u % (R / 8);
-        const int4 v = *reinterpret_cast<const int4*>(prof + static_cast<size_t>(c) * stride + s0 + img * R + 8 * k);
+        const int4 v = *reinterpret_cast<const int4*>(prof + static_cast<size_t>(c) * stride + s0 + im * R + 8 * k);
         const uint32_t w[4] = {static_cast<uint32_t>(v.x), static_cast<uint32_t>(v.y), static_cast<uint32_t>(v.z),
                                static_cast<uint32_t>(v.w)};
         uint32_t o[8];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            uint32_t a0 = w[e] & 0xffffu, a1 = w[e] >> 16;
+            const int s0v = static_cast<int16_t>(w[e] & 0xffffu), s1v = static_cast<int16_t>(w[e] >> 16);
+            // row 8k + 2e of the strip starts a row group when k is even and e = 0
+            const int b0 = (F16 && k % 2 == 0 && e == 0) ? bias0 : 0;
+            uint32_t a0 = static_cast<uint32_t>(s0v) & 0xffffu, a1 = static_cast<uint32_t>(s1v) & 0xffffu;
             if constexpr (F16) {
-                a0 = to_f16_bits(static_cast<uint32_t>(static_cast<int16_t>(a0) + bias));
-                a1 = to_f16_bits(static_cast<uint32_t>(static_cast<int16_t>(a1) + bias));
+                a0 = to_f16_bits(static_cast<uint32_t>(s0v + bias + b0));
+                a1 = to_f16_bits(static_cast<uint32_t>(s1v + bias));
             }
-            // the other half holds 1 (1.0 in fp16): the kernel forms the pair
-            // as lo * hi + H_diag in one v_pk_fma_f16 / v_pk_mad_u16
-            o[2 * e] = img ? (a0 << 16) | one : a0 | (one << 16);
-            o[2 * e + 1] = img ? (a1 << 16) | one : a1 | (one << 16);
+            o[2 * e] = im ? (a0 << 16) | one : a0 | (one << 16);
+            o[2 * e + 1] = im ? (a1 << 16) | one : a1 | (one << 16);
         }
-        int4* d = reinterpret_cast<int4*>((img ? L.hi : L.lo) + c * RD + 8 * k);
-        d[0] = make_int4(o[0], o[1], o[2], o[3]);
-        d[1] = make_int4(o[4], o[5], o[6], o[7]);
-    }
-}
-
-// One of the two images (img 0: lo <- rows [s0, s0+R); img 1: hi <- rows
-// [s0+R, s0+2R)), for the chained passes of sw_inter_x2s.
-template <int R, bool F16 = false>
-__device__ __forceinline__ void stage_x2s_one(X2Lds<R>& L, const int16_t* __restrict__ prof, int stride, int s0,
-                                              int lane, int bias, int img) {
-    constexpr int RD = x2_row_dwords(R);
-    constexpr uint32_t one = F16 ? 0x3c00u : 1u;
-    for (int u = lane; u < kProfileRows * (R / 8); u += kLanes) {
-        const int c = u / (R / 8);
-        const int k = u % (R / 8);
-        const int4 v = *reinterpret_cast<const int4*>(prof + static_cast<size_t>(c) * stride + s0 + img * R + 8 * k);
-        const uint32_t w[4] = {static_cast<uint32_t>(v.x), static_cast<uint32_t>(v.y), static_cast<uint32_t>(v.z),
-                               static_cast<uint32_t>(v.w)};
-        uint32_t o[8];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            uint32_t a0 = w[e] & 0xffffu, a1 = w[e] >> 16;
-            if constexpr (F16) {
-                a0 = to_f16_bits(static_cast<uint32_t>(static_cast<int16_t>(a0) + bias));
-                a1 = to_f16_bits(static_cast<uint32_t>(static_cast<int16_t>(a1) + bias));
-            }
-            o[2 * e] = img ? (a0 << 16) | one : a0 | (one << 16);
-            o[2 * e + 1] = img ? (a1 << 16) | one : a1 | (one << 16);
-        }
-        int4* d = reinterpret_cast<int4*>((img ? L.hi : L.lo) + c * RD + 8 * k);
+        int4* d = reinterpret_cast<int4*>((im ? L.hi : L.lo) + c * RD + 8 * k);
         d[0] = make_int4(o[0], o[1], o[2], o[3]);
         d[1] = make_int4(o[4], o[5], o[6], o[7]);
     }
@@ -447,6 +398,11 @@ __device__ __forceinline__ void ring_load(uint32_t (&v)[SG], const int4* ring, i
 // restart; SG columns later the same for the hi image and the high halves.
 // The low strip's row -1 input of pass k's first columns was stored by pass
 // k-1's high strip at least one sub-group earlier (ncols >= 32).
+#ifndef SW_HOIST_FMA
+#define SW_HOIST_FMA 1
+#endif
+constexpr bool kHoistFma = SW_HOIST_FMA != 0;
+
 template <int R, int SG, bool AFFINE, bool F16, bool PAIR, int CR = 16, bool CHAIN = false>
 __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32_t ncols, uint64_t base, int lane,
                                          int s0, Best<F16>& best, const int4* ring_in, int4* ring_out,
@@ -479,8 +435,14 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     const uint32_t total = npass * ncols;
     const int sbias = F16 ? (AFFINE ? 2 : 1) * a.gap_extend : 0;
     // fp16: the images hold S + 2 ge (the diagonal comes from bias r - 1 + jj - 1;
-    // the linear profile already holds S + g)
-    stage_x2s<R, F16>(L, prof16, a.prof_stride, s0, lane, F16 ? (AFFINE ? 2 : 1) * a.gap_extend : 0);
+    // the linear profile already holds S + g); a row group's first row S + 2 ge
+    // - 16 ge: its diagonal (the row above, or row -1 from the boundary / delay
+    // line) still has the previous row group's bias, and the profile, not an
+    // extra subtraction per column, takes it back
+    const int gbias0 = F16 ? -kRowGroup * a.gap_extend : 0;
+    // packed H of row -1 at the previous step, with the last row group's bias
+    const uint32_t dtop0 = F16 ? a.f16_step[SG - 2 + kRowGroup] : 0u;
+    stage_x2s<R, F16>(L, prof16, a.prof_stride, s0, lane, sbias, gbias0, -1);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -496,7 +458,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     for (int r = 0; r < R; ++r) H[r] = P::from(F16 ? a.f16_step[r % kRowGroup + SG - 1] : 0u);
 #pragma unroll
     for (int r = 0; r < (AFFINE ? R : 1); ++r) E[r] = P::from(0u);
-    uint32_t dtop = F16 ? a.f16_step[SG - 2] : 0u;  // packed H of row -1 at the previous step
+    uint32_t dtop = dtop0;             // packed H of row -1 at the previous step
     uint32_t dl_h[SG], dl_f[SG];       // low strip's bottom row, SG steps back
     uint32_t bin[SG], bin_n[SG];       // HBM boundary in (H | F << 16), this / next sub-group
     uint32_t bz[SG];                   // the zero boundary row
@@ -520,7 +482,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     constexpr uint32_t RB = x2_row_dwords(R) * 4;
     const uint32_t blo = lds_addr(L.lo), bhi = lds_addr(L.hi);
     // LDS addresses of the code rows of the column being prefetched
-    uint32_t aa = blo + code_of(rc, 0) * RB, ab = bhi + code_of(rp, 0) * RB;
+    uint32_t aa = code_row<RB>(rc, 0, blo), ab = code_row<RB>(rp, 0, bhi);
     read_x2a<CQ>(PL[0], PH[0], aa, ab, 0, 0);
 
     // sub-groups 0 .. total/SG: the last one runs the high strip only.
@@ -544,32 +506,32 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
         const bool next_t1 = CHAIN && wrap && next_lo;
         const bool next_t2 = t1;
         if (t1) {
-            stage_x2s_one<R, F16>(L, prof16, a.prof_stride, static_cast<int>(lo_p) * 2 * R, lane, sbias, 0);
+            stage_x2s<R, F16>(L, prof16, a.prof_stride, static_cast<int>(lo_p) * 2 * R, lane, sbias, gbias0, 0);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 H[r] = P::from(__builtin_amdgcn_perm(P::bits(H[r]), F16 ? a.f16_step[r % kRowGroup + SG - 1] : 0u,
                                                      0x07060100u));
                 if constexpr (AFFINE) E[r] = P::from(P::bits(E[r]) & 0xffff0000u);
             }
-            dtop = __builtin_amdgcn_perm(dtop, F16 ? a.f16_step[SG - 2] : 0u, 0x07060100u);
+            dtop = __builtin_amdgcn_perm(dtop, dtop0, 0x07060100u);
         }
         if (t2) {
             // the high strip enters pass lo_p (the low strip entered it one sub-group ago)
-            stage_x2s_one<R, F16>(L, prof16, a.prof_stride, static_cast<int>(lo_p) * 2 * R, lane, sbias, 1);
+            stage_x2s<R, F16>(L, prof16, a.prof_stride, static_cast<int>(lo_p) * 2 * R, lane, sbias, gbias0, 1);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 H[r] = P::from(__builtin_amdgcn_perm(F16 ? a.f16_step[r % kRowGroup + SG - 1] : 0u, P::bits(H[r]),
                                                      0x07060100u));
                 if constexpr (AFFINE) E[r] = P::from(P::bits(E[r]) & 0xffffu);
             }
-            dtop = __builtin_amdgcn_perm(F16 ? a.f16_step[SG - 2] : 0u, dtop, 0x07060100u);
+            dtop = __builtin_amdgcn_perm(dtop0, dtop, 0x07060100u);
         }
         if (t1 || t2) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            aa = blo + code_of(rc, 0) * RB;
-            ab = bhi + code_of(rp, 0) * RB;
+            aa = code_row<RB>(rc, 0, blo);
+            ab = code_row<RB>(rp, 0, bhi);
             read_x2a<CQ>(PL[0], PH[0], aa, ab, 0, 0);
         }
         if (next_t1) {
@@ -605,10 +567,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
                 // H~ = max(max3(left, up, H_diag + S + 2 g), floor): 3 packed
                 // ops per cell pair + the anti-diagonal maxima.
                 const int rg = r % kRowGroup;
-                if (rg == 0 && r > 0) {  // next row group: its bias restarts at 0
-                    up = up - grp_h;
-                    diag = diag - grp_h;
-                }
+                if (rg == 0 && r > 0) up = up - grp_h;  // next row group: its bias restarts at 0
                 const h2 t = max3h(H[r], up, __builtin_elementwise_fma(slo, shi, diag));
                 const h2 h = __builtin_elementwise_maximum(t, __builtin_bit_cast(h2, a.f16_step[rg + jj]));
                 h2& acc = best.acc[rg + jj];
@@ -631,10 +590,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
                 // for the maximum, 2 per row per sub-group for the column
                 // rebase, 4 per column for the row-group resets).
                 const int rg = r % kRowGroup;
-                if (rg == 0 && r > 0) {  // next row group: its bias restarts at 0
-                    f = f - grp_h;
-                    diag = diag - grp_h;
-                }
+                if (rg == 0 && r > 0) f = f - grp_h;  // next row group: its bias restarts at 0
                 const h2 h = max3h(E[r], f, __builtin_elementwise_fma(slo, shi, diag));
                 const h2 m = h - gog_h;
                 E[r] = __builtin_elementwise_maximum(E[r], m);
@@ -666,6 +622,27 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
                 best.v = max2(best.v, h);
             }
         };
+        // the biased Farrar cell above with its diagonal sum d given
+        auto cell_d = [&](const int r, const int jj, V& up, V& diag, V& f, const V d) {
+          if constexpr (F16 && AFFINE) {
+            const int rg = r % kRowGroup;
+            if (rg == 0 && r > 0) f = f - grp_h;
+            const h2 h = max3h(E[r], f, d);
+            const h2 m = h - gog_h;
+            E[r] = __builtin_elementwise_maximum(E[r], m);
+            f = max3h(f, m, __builtin_bit_cast(h2, a.f16_step[rg + jj + 1]));
+            h2& acc = best.acc[rg + jj];
+            if (jj & 1) {
+                if (rg + 1 < kRowGroup) acc = max3h(acc, h, H[r + 1]);
+                else acc = __builtin_elementwise_maximum(acc, h);
+            } else if (rg == 0) {
+                acc = __builtin_elementwise_maximum(acc, h);
+            }
+            diag = H[r];
+            H[r] = h;
+            up = h;
+          }
+        };
         // end of column jj: its bottom row feeds the high strip SG steps later
         auto col_done = [&](const V up, const V f, const int jj) {
             dl_h[jj] = P::bits(up);
@@ -675,9 +652,11 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
         // high strip from the low strip's bottom row SG steps back (fp16:
         // both from the last row group's bias to row -1's / row 0's)
         auto col_start = [&](V& up, V& diag, V& f, const int jj) {
-            uint32_t u = lo_lo(bin[jj], dl_h[jj]);
-            if constexpr (F16) u = P::bits(P::from(u) - grp_h);
+            const uint32_t u = lo_lo(bin[jj], dl_h[jj]);
+            // fp16: row 0's diagonal keeps the last row group's bias (the
+            // profile's row 0 takes it back); the linear cell's up term drops it
             up = P::from(u);
+            if constexpr (F16 && !AFFINE) up = up - grp_h;
             diag = P::from(dtop);
             dtop = u;
             if constexpr (AFFINE) f = P::from(hi_lo(bin[jj], dl_f[jj]));
@@ -692,20 +671,36 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
             if (t + 1 < STEPS) {
                 const int jn = (t + 1) / NCH, kn = (t + 1) % NCH;
                 if (kn == 0) {
-                    aa = blo + code_of(rc, jn) * RB;
-                    ab = bhi + code_of(rp, jn) * RB;
+                    aa = code_row<RB>(rc, jn, blo);
+                    ab = code_row<RB>(rp, jn, bhi);
                 }
                 read_x2a<CQ>(PL[(t + 1) & 1], PH[(t + 1) & 1], aa, ab, kn, dep);
             } else if (has_next && !next_t1 && !next_t2) {
-                aa = blo + code_of(rn, 0) * RB;
-                ab = bhi + code_of(rc, 0) * RB;
+                aa = code_row<RB>(rn, 0, blo);
+                ab = code_row<RB>(rc, 0, bhi);
                 read_x2a<CQ>(PL[(t + 1) & 1], PH[(t + 1) & 1], aa, ab, 0, dep);
             }
             if (k == 0) col_start(up, diag, f, jj);
             const int4(&pl)[CQ] = PL[t & 1];
             const int4(&ph)[CQ] = PH[t & 1];
+            if constexpr (F16 && AFFINE && kHoistFma) {
+                // the step's CR diagonal sums first (they read only the old H
+                // values), so the dependent chain h -> m -> F of each row has
+                // independent work beside it
+                V dd[CR];
 #pragma unroll
-            for (int i = 0; i < CR; ++i) cell(CR * k + i, jj, up, diag, f, P::from(word(pl, i)), P::from(word(ph, i)));
+                for (int i = 0; i < CR; ++i)
+                    dd[i] = __builtin_elementwise_fma(P::from(word(pl, i)), P::from(word(ph, i)),
+                                                      i == 0 ? diag : H[CR * k + i - 1]);
+#pragma unroll
+                for (int i = 0; i < CR; ++i) asm volatile("" : "+v"(dd[i]));
+#pragma unroll
+                for (int i = 0; i < CR; ++i) cell_d(CR * k + i, jj, up, diag, f, dd[i]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < CR; ++i)
+                    cell(CR * k + i, jj, up, diag, f, P::from(word(pl, i)), P::from(word(ph, i)));
+            }
             if (k == NCH - 1) col_done(up, f, jj);
             // pin the running maxima at every step: left free, the compiler
             // defers the max reductions and keeps every h alive (spills)
