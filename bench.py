@@ -776,14 +776,21 @@ def main():
                         # measured packed-op cost, over every SIMD's cycles at
                         # the clock GRBM_GUI_ACTIVE shows under this load
                         insts = tj["sq_insts_valu_per_launch"]
-                        # GRBM_GUI_ACTIVE is summed over the 8 XCDs by rocprofv3
-                        clk = tj["grbm_gui_active_per_launch"] / 8 / tj["profiled_ns_per_launch"]  # GHz
+                        # GRBM_GUI_ACTIVE is summed over the 8 XCDs by rocprofv3:
+                        # /8 = the cycles of the profiled launch itself, so the
+                        # fraction uses that one pass's clock AND duration
+                        cyc = tj["grbm_gui_active_per_launch"] / 8
+                        clk = cyc / tj["profiled_ns_per_launch"]  # GHz
                         cells_launch = float(qtot) / nq * wave_res
                         valu_hw = {"sq_insts_valu_per_launch": insts,
                                    "valu_insts_per_128_cells": round(insts / (cells_launch / 128), 3),
-                                   "clock_ghz_under_load": round(clk, 3), "cycles_per_valu_inst": 4.25,
-                                   "issue_frac": round(insts * 4.25 / (SIMDS * clk * 1e9 * kernel_ms * 1e-3), 4),
-                                   "source": "stored rocprofv3 --pmc SQ pass (pmc_traffic.json), same kernel sources"}
+                                   "clock_ghz_under_load": round(clk, 3),
+                                   "profiled_ms_per_launch": round(tj["profiled_ns_per_launch"] * 1e-6, 4),
+                                   "cycles_per_valu_inst": 4.25,
+                                   "issue_frac": round(insts * 4.25 / (SIMDS * cyc), 4),
+                                   "issue_frac_4cyc": round(insts * 4.0 / (SIMDS * cyc), 4),
+                                   "source": "stored rocprofv3 --pmc SQ pass (pmc_traffic.json), same kernel sources; "
+                                             "instructions, cycles and duration all of that one profiled launch"}
                     traffic_note = ("stored rocprofv3 --pmc measurement (FETCH_SIZE x2 + WRITE_SIZE) of this "
                                     "workload, taken on a build with the same kernel sources (%s, %s)"
                                     % (tj.get("kernel_src_sha16"), tj.get("measured", "?")))

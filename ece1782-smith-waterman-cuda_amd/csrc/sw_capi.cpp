@@ -34,6 +34,9 @@ namespace {
 
 thread_local std::string g_err;
 
+// fp16 represents every integer in [-kF16Span, kF16Span] exactly
+constexpr int kF16Span = 2048;
+
 // packed fp16 pair (v, v) of a small integer (|v| <= 2048: exact)
 uint32_t f16_pair(int v) {
     const _Float16 x = static_cast<_Float16>(static_cast<float>(v));
@@ -1101,10 +1104,11 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     const int ri2 = intra_x2 ? swk::intra_x2_rows_for(qlen, db->long_max) : 0;
     // The intra chain's order.  Linear scoring with cheap gaps makes random
     // pairs' scores grow with their lengths, so on long subjects the fp16
-    // pass can flag nearly everything (C5 with the reference's BLOSUM50 / 2:
-    // all of it) and its time is wasted.  Once a scan with the same scoring
-    // has flagged over half of the long subjects at a query no longer than
-    // this one, the int16 form runs first, over all of them.
+    // pass can flag many of them and its time on those is wasted.  Once a
+    // scan with the same scoring has flagged over a third of the long
+    // subjects at a query no longer than this one, the int16 form runs
+    // first, over all of them (the int16 cell costs ~1.4x the fp16 one, so
+    // fp16 first + int16 over the flagged fraction p wins while p < ~0.3).
     // SW_INTRA_I16_FIRST=0 / 1: never / always.
     uint64_t skey = 1469598103934665603ull;  // FNV-1a of the scoring
     for (int k = 0; k < 625; ++k) skey = (skey ^ static_cast<uint8_t>(mat[k])) * 1099511628211ull;
@@ -1117,7 +1121,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         db->lseen_key = db->lcount_key;
         db->lseen_qhash = db->lcount_qhash;
         db->lseen_qlen = db->lcount_qlen;
-        if (2 * static_cast<int64_t>(*db->h_lcount) > db->nlong) {
+        if (3 * static_cast<int64_t>(*db->h_lcount) > db->nlong) {
             bool seen = false;
             for (auto& e : db->i16_first)
                 if (e.first == db->lcount_key) {
@@ -1372,9 +1376,13 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         x.prof_stride = P.stride;
         x.bias = affine ? 0 : go;  // the linear profile holds S + gap
         x.qpad = qpad_intra2;
-        // biased cell: stored values up to (RI + 10) ge above the true ones
-        x.sat_limit = 2048 - 2 * std::max(max_s, 1) - 26 * ge;
-        for (int j = 0; j < 32; ++j) x.f16_step[j] = f16_pair(j * ge);
+        // biased cell: stored values up to (RI + 10) ge above the true ones,
+        // offset by zero = -2048 + 2 ge as the inter cell's (the lowest value
+        // an addition reads is a rebased row -1 H of bias -2 ge: exact)
+        const int zero = -kF16Span + 2 * ge;
+        x.sat_limit = kF16Span - zero - 2 * std::max(max_s, 1) - 26 * ge;
+        for (int j = 0; j < 32; ++j) x.f16_step[j] = f16_pair(j * ge + zero);
+        x.f16_zero = f16_pair(zero);
         x.f16_gog = f16_pair(go - ge);
         if (intra_i16_first) {
             // the int16 form over every long subject, flagging near-32767 ones
@@ -1456,12 +1464,22 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             a.rescue_count = listA;
             a.rescue_list = listA + 1;
             if (f16) a.rescue_max = maxA;  // counters reset before the fork
-            // fp16 exact range: every integer up to 2048; H grows by <= max S
+            // fp16 exact range: every integer in [-2048, 2048].  The cell
+            // stores true + bias + zero with zero = -2048 + 2 ge, which
+            // nearly doubles the range of true values: the lowest value a
+            // later addition reads is a rebased H of bias -ge (>= -2048:
+            // exact); values further below lose to the floor, which sits at
+            // zero or above, and only need their order.  H grows by <= max S
             // per cell and the biased cell stores values up to 26 ge above
-            // the true ones (bias (15 + 7 + 2) ge, + 2 ge in the profile)
-            a.sat_limit = 2048 - 2 * std::max(max_s, 1) - 26 * ge;
-            for (int j = 0; j < 32; ++j) a.f16_step[j] = f16_pair(j * ge);
+            // the true ones (bias (15 + 7 + 2) ge, + 2 ge in the profile).
+            const int zero = -kF16Span + 2 * ge;
+            a.sat_limit = kF16Span - zero - 2 * std::max(max_s, 1) - 26 * ge;
+            for (int j = 0; j < 32; ++j) a.f16_step[j] = f16_pair(j * ge + zero);
             a.f16_gog = f16_pair(go - ge);
+            a.f16_zero = f16_pair(zero);
+            a.f16_diff[0] = f16_pair(4 * ge);
+            a.f16_diff[1] = f16_pair(8 * ge);
+            a.f16_diff[2] = f16_pair(16 * ge);
         }
         if (ncoop) {
             // on its own stream, so the per-wave kernel fills the GPU beside it
@@ -1700,7 +1718,16 @@ int sw_create(int32_t device, sw_handle** out) {
     // reference scoring 12,840 -> 8,900 GCUPS).
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side2, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking);
+    // The deferred rescue tails (batches) run at high priority: HIP serves
+    // those streams from a separate queue pool, so a tail never shares a
+    // hardware queue with the next query's scan (sharing one, the next
+    // scan waited behind the tail: C3, the reference scoring's long queries
+    // stalled 9-13 ms each behind their int16 list kernel).
+    if (e == hipSuccess) {
+        int least = 0, greatest = 0;
+        e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&h->tail, hipStreamNonBlocking, greatest);
+    }
     for (hipEvent_t* ev : {&h->main_done, &h->side_done, &h->tail_done[0], &h->tail_done[1]})
         if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     for (auto& S : h->prof) {

@@ -282,15 +282,16 @@ constexpr int kAcc = kRowGroup + 8 - 1;
 template <bool F16>
 struct Best {
     typename PkCell<F16>::V v;
-    __device__ __forceinline__ void init() { v = PkCell<F16>::from(0u); }
+    __device__ __forceinline__ void init(const InterArgs&) { v = PkCell<F16>::from(0u); }
     __device__ __forceinline__ typename PkCell<F16>::V value(const InterArgs&) const { return v; }
 };
 template <>
 struct Best<true> {
     h2 acc[kAcc];
-    __device__ __forceinline__ void init() {
+    // the maxima start at the offset zero (every cell is at least that)
+    __device__ __forceinline__ void init(const InterArgs& a) {
 #pragma unroll
-        for (int k = 0; k < kAcc; ++k) acc[k] = h2{0, 0};
+        for (int k = 0; k < kAcc; ++k) acc[k] = __builtin_bit_cast(h2, a.f16_zero);
     }
     __device__ __forceinline__ void pin() {
         static_assert(kAcc == 23, "pin list");
@@ -301,11 +302,15 @@ struct Best<true> {
         asm volatile("" : "+v"(acc[16]), "+v"(acc[17]), "+v"(acc[18]), "+v"(acc[19]), "+v"(acc[20]),
                      "+v"(acc[21]), "+v"(acc[22]));
     }
+    // the maximum with the bias removed but the offset kept (the true score
+    // may exceed 2048, which fp16 no longer holds exactly; x2s_finish
+    // removes the offset in integers)
     __device__ __forceinline__ h2 value(const InterArgs& a) const {
+        const h2 z = __builtin_bit_cast(h2, a.f16_step[0]);
         h2 b = acc[0];
 #pragma unroll
         for (int k = 1; k < kAcc; ++k)
-            b = __builtin_elementwise_maximum(b, acc[k] - __builtin_bit_cast(h2, a.f16_step[k]));
+            b = __builtin_elementwise_maximum(b, acc[k] - (__builtin_bit_cast(h2, a.f16_step[k]) - z));
         return b;
     }
 };
@@ -344,8 +349,9 @@ __device__ __forceinline__ void trace_block(const InterArgs& a, int blk, uint64_
 template <bool F16>
 __device__ __forceinline__ void x2s_finish(const InterArgs& a, int blk, int lane, typename PkCell<F16>::V best) {
     int b;
-    if constexpr (F16)
-        b = static_cast<int>(static_cast<float>(__builtin_elementwise_maximum(best.x, best.y)));
+    if constexpr (F16)  // offset removed in integers: true scores go up to ~4096
+        b = static_cast<int>(static_cast<float>(__builtin_elementwise_maximum(best.x, best.y))) -
+            static_cast<int>(static_cast<float>(__builtin_bit_cast(h2, a.f16_step[0]).x));
     else
         b = max(static_cast<int>(best.x), static_cast<int>(best.y));
     const int id = a.lane_ids[static_cast<size_t>(blk) * kLanes + lane];
@@ -425,8 +431,10 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     h2 gog_h = {}, reb_h = {}, grp_h = {};
     if constexpr (F16) {
         gog_h = __builtin_bit_cast(h2, a.f16_gog);
-        reb_h = __builtin_bit_cast(h2, a.f16_step[SG]);
-        grp_h = __builtin_bit_cast(h2, a.f16_step[kRowGroup]);
+        // unshifted: SG ge (the rebase per sub-group), 16 ge (the row-group reset)
+        static_assert(SG == 4 || SG == 8, "rebase constants");
+        reb_h = __builtin_bit_cast(h2, a.f16_diff[SG == 4 ? 0 : 1]);
+        grp_h = __builtin_bit_cast(h2, a.f16_diff[2]);
     }
     const bool first = (s0 == 0);
     const bool last = (s0 + 2 * R >= a.qpad);
@@ -457,7 +465,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
 #pragma unroll
     for (int r = 0; r < R; ++r) H[r] = P::from(F16 ? a.f16_step[r % kRowGroup + SG - 1] : 0u);
 #pragma unroll
-    for (int r = 0; r < (AFFINE ? R : 1); ++r) E[r] = P::from(0u);
+    for (int r = 0; r < (AFFINE ? R : 1); ++r) E[r] = P::from(F16 ? a.f16_zero : 0u);
     uint32_t dtop = dtop0;             // packed H of row -1 at the previous step
     uint32_t dl_h[SG], dl_f[SG];       // low strip's bottom row, SG steps back
     uint32_t bin[SG], bin_n[SG];       // HBM boundary in (H | F << 16), this / next sub-group
@@ -511,7 +519,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
             for (int r = 0; r < R; ++r) {
                 H[r] = P::from(__builtin_amdgcn_perm(P::bits(H[r]), F16 ? a.f16_step[r % kRowGroup + SG - 1] : 0u,
                                                      0x07060100u));
-                if constexpr (AFFINE) E[r] = P::from(P::bits(E[r]) & 0xffff0000u);
+                if constexpr (AFFINE) E[r] = P::from(__builtin_amdgcn_perm(P::bits(E[r]), F16 ? a.f16_zero : 0u, 0x07060100u));
             }
             dtop = __builtin_amdgcn_perm(dtop, dtop0, 0x07060100u);
         }
@@ -522,7 +530,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
             for (int r = 0; r < R; ++r) {
                 H[r] = P::from(__builtin_amdgcn_perm(F16 ? a.f16_step[r % kRowGroup + SG - 1] : 0u, P::bits(H[r]),
                                                      0x07060100u));
-                if constexpr (AFFINE) E[r] = P::from(P::bits(E[r]) & 0xffffu);
+                if constexpr (AFFINE) E[r] = P::from(__builtin_amdgcn_perm(F16 ? a.f16_zero : 0u, P::bits(E[r]), 0x07060100u));
             }
             dtop = __builtin_amdgcn_perm(dtop0, dtop, 0x07060100u);
         }
@@ -756,7 +764,7 @@ __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>&
     const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
     const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
     Best<F16> best;
-    best.init();
+    best.init(a);
     const uint64_t t0 = trace_now();
     if (kChainPasses && ncols >= 32 && a.qpad > 2 * R) {
         x2s_pass<R, SG, AFFINE, F16, false, CR, true>(a, L, ncols, base, lane, 0, best, nullptr, nullptr, nullptr);
@@ -874,7 +882,7 @@ __device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, int quad_end
     }
     const int blk = first + gi;
     Best<F16> best;
-    best.init();
+    best.init(a);
     int tick = 0;
     const uint64_t t0 = trace_now();
     if (blk < npair) {

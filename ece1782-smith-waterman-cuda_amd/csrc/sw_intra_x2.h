@@ -74,7 +74,17 @@ struct IntraCell {
     static __device__ __forceinline__ uint32_t bits(V x) { return __builtin_bit_cast(uint32_t, x); }
     static __device__ __forceinline__ V max2(V a, V b) { return __builtin_elementwise_maximum(a, b); }
     static __device__ __forceinline__ V max3(V a, V b, V c) { return hmax3(a, b, c); }
+    // the cell values carry the offset zero (IntraArgs::f16_zero): step(j) =
+    // (j ge + zero); diff(j) = (j ge), for the rebase and the hand-off drops,
+    // is step(j) - step(0) (exact: small integers)
     static __device__ __forceinline__ uint32_t step(const IntraArgs& a, int j) { return a.f16_step[j]; }
+    static __device__ __forceinline__ uint32_t diff(const IntraArgs& a, int j) {
+        return __builtin_bit_cast(uint32_t, __builtin_bit_cast(h2, a.f16_step[j]) - __builtin_bit_cast(h2, a.f16_step[0]));
+    }
+    static __device__ __forceinline__ uint32_t zero(const IntraArgs& a) { return a.f16_zero; }
+    static __device__ __forceinline__ int zero_int(const IntraArgs& a) {
+        return static_cast<int>(static_cast<float>(__builtin_bit_cast(h2, a.f16_zero).x));
+    }
     static __device__ __forceinline__ uint32_t pair_of(int v) { const uint32_t b = f16_bits(v); return b | (b << 16); }
     static __device__ __forceinline__ uint32_t convert(uint32_t w, int b) { return f16x2_of(w, b); }
     static __device__ __forceinline__ int lo(V x) { return static_cast<int>(static_cast<float>(x.x)); }
@@ -89,6 +99,9 @@ struct IntraCell<false> {
     static __device__ __forceinline__ V max2(V a, V b) { return __builtin_elementwise_max(a, b); }
     static __device__ __forceinline__ V max3(V a, V b, V c) { return max2(max2(a, b), c); }
     static __device__ __forceinline__ uint32_t step(const IntraArgs& a, int j) { return pair_of(j * a.gap_extend); }
+    static __device__ __forceinline__ uint32_t diff(const IntraArgs& a, int j) { return step(a, j); }
+    static __device__ __forceinline__ uint32_t zero(const IntraArgs&) { return 0u; }
+    static __device__ __forceinline__ int zero_int(const IntraArgs&) { return 0; }
     static __device__ __forceinline__ uint32_t pair_of(int v) {
         const uint32_t b = static_cast<uint16_t>(v);
         return b | (b << 16);
@@ -189,7 +202,8 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
     uint32_t* bnd_h = reinterpret_cast<uint32_t*>(a.bnd_h) + (LA >= LB ? offA : (hasB ? a.subj_off[sb] : 0));
     uint32_t* bnd_f = reinterpret_cast<uint32_t*>(a.bnd_f) + (LA >= LB ? offA : (hasB ? a.subj_off[sb] : 0));
     const int16_t* prof16 = reinterpret_cast<const int16_t*>(a.prof);
-    auto step = [&](int j) { return C::from(C::step(a, j)); };  // (j ge, j ge)
+    auto step = [&](int j) { return C::from(C::step(a, j)); };  // (j ge, j ge) + the offset
+    auto diff = [&](int j) { return C::from(C::diff(a, j)); };  // (j ge, j ge)
     const V gog = C::from(C::pair_of(a.gap_open - a.gap_extend));
     // Biased cell (the two-strips kernel's, sw_inter_x2.hip): at step k,
     // row i of a lane holds H~ = H + (i + k % NB) ge, E' and F~ likewise, so
@@ -203,7 +217,7 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
     // anti-diagonal i + k % NB, two cells per v_pk_maximum3_f16.
     V acc[NACC];
 #pragma unroll
-    for (int q = 0; q < NACC; ++q) acc[q] = C::from(0u);
+    for (int q = 0; q < NACC; ++q) acc[q] = C::from(C::zero(a));
     constexpr uint32_t kPadPair = kPadCode | (kPadCode << 8);
 
     for (int c0 = 0; c0 < a.qpad; c0 += CH) {
@@ -227,7 +241,7 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
 #pragma unroll
         for (int r = 0; r < RI; ++r) {
             H[r] = step(r + NB - 1);
-            if constexpr (!LIN) E[r] = C::from(0u);
+            if constexpr (!LIN) E[r] = C::from(C::zero(a));
         }
         // bottom row (H, F) of this lane one step back, and H of the row above
         // at the previous column (row 0's diagonal): zeros of step -1
@@ -276,8 +290,10 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
                 in_res = in_res_nb;
                 in_res_nb = codes_at(col + kLanes);
                 const int bz = RI - 2 + (col % NB) + ((col % NB) == 0 ? NB : 0);
-                in_bh = (!first && col < L) ? bnd_h[col] : C::pair_of(bz * a.gap_extend);
-                in_bf = (!first && col < L) ? bnd_f[col] : C::pair_of((bz + 1) * a.gap_extend);
+                // (bz ge + zero) computed, not indexed: a lane-varying index
+                // into the argument table would copy the table to registers
+                in_bh = (!first && col < L) ? bnd_h[col] : C::pair_of(bz * a.gap_extend + C::zero_int(a));
+                in_bf = (!first && col < L) ? bnd_f[col] : C::pair_of((bz + 1) * a.gap_extend + C::zero_int(a));
             }
             if (kPrefetch && k0 == 0) {
                 rc_n = shr1u(__builtin_amdgcn_readlane(in_res, 0), rc);
@@ -308,11 +324,11 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
                         read_words(rc, wa, wb);
                     }
                     // hand-off: the row above's bottom (H, F) from one step back
-                    const V adj = step(RI - 1 + (b == 0 ? NB : 0));
+                    const V adj = diff(RI - 1 + (b == 0 ? NB : 0));
                     const uint32_t up0 = C::bits(C::from(shr1u(sbh, hl)) - adj);
                     V f = LIN ? C::from(0u) : C::from(shr1u(sbf, fl)) - adj;
                     if (b == 0) {  // rebase: the bias period restarts
-                        const V reb = step(NB);
+                        const V reb = diff(NB);
 #pragma unroll
                         for (int r = 0; r < RI; ++r) {
                             H[r] = H[r] - reb;
@@ -373,18 +389,19 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
             }
         }
     }
-    // the lane's maximum (unbiased), then the wave's
+    // the lane's maximum (bias removed, offset kept: fp16 does not hold the
+    // true scores above 2048 exactly), then the wave's
     V best = acc[0];
 #pragma unroll
-    for (int q = 1; q < NACC; ++q) best = C::max2(best, acc[q] - step(q));
+    for (int q = 1; q < NACC; ++q) best = C::max2(best, acc[q] - diff(q));
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(C::bits(best)), off));
         best = C::max2(best, C::from(o));
     }
     if (lane == 0) {
-        const int ba = C::lo(best);
-        const int bb = C::hi(best);
+        const int ba = C::lo(best) - C::zero_int(a);
+        const int bb = C::hi(best) - C::zero_int(a);
         if (hasA) {
             a.scores[a.subj_id[sa]] = ba;
             if (a.rescue_list && C::flag(a, ba)) a.rescue_list[atomicAdd(a.rescue_count, 1)] = sa;

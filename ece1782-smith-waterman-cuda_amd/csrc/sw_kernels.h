@@ -74,10 +74,18 @@ struct InterArgs {
     // fp16 kernel: a lane whose running maximum reaches this flags its block
     int32_t sat_limit;
     // fp16 kernel, biased cell (sw_inter_x2.hip): f16_step[j] = the packed
-    // fp16 pair (j * gap_extend, j * gap_extend), j = 0..31, and f16_gog =
+    // fp16 pair (j * gap_extend + f16 offset), j = 0..31, and f16_gog =
     // packed (gap_open - gap_extend); host-built so they stay in SGPRs
+    // All fp16 cell values carry the offset f16_zero = (z, z), z = -2048 +
+    // 2 ge: fp16 holds every integer in [-2048, 2048] exactly, so the
+    // shifted cell is exact for true values up to ~4096 (max/add commute
+    // with the shift; sw_capi.cpp states the bound).  f16_step[j] is then
+    // the pair (j ge + z), and f16_diff the unshifted pairs (4 ge, 8 ge,
+    // 16 ge): the rebase per sub-group of 4 or 8 columns, the row-group reset.
     uint32_t f16_step[32];
     uint32_t f16_gog;
+    uint32_t f16_zero;
+    uint32_t f16_diff[3];
     // sw_inter_x2p: its pair blocks are [blk_base, blk_first) (merged) or
     // [blk_base, nblocks); blocks below blk_base run elsewhere
     int32_t blk_base;
@@ -112,7 +120,8 @@ struct IntraArgs {
     int32_t prof_stride = 0;
     int32_t bias = 0;
     int32_t sat_limit = 0;       // flag subjects whose maximum reaches this
-    uint32_t f16_step[32] = {};  // as InterArgs: packed fp16 (j ge, j ge)
+    uint32_t f16_step[32] = {};  // as InterArgs: packed fp16 (j ge + z, j ge + z)
+    uint32_t f16_zero = 0;       // the offset z = -2048 + 2 ge of every fp16 cell value
     uint32_t f16_gog = 0;        // packed fp16 (go - ge, go - ge)
     int32_t* rescue_list = nullptr;
     int32_t* rescue_count = nullptr;

@@ -340,9 +340,9 @@ def test_batch_all_shipped_queries_c3(sw, oracle, handle):
 @pytest.mark.parametrize("scoring", [(0, 2, 2), (1, 12, 1)])
 def test_batch_rescue_tails_overlap(sw, oracle, handle, scoring):
     """A rescue-heavy batch: long queries under the reference's cheap linear
-    gaps (BLOSUM50 / 2: the widest blocks and most long subjects cross the
-    fp16 guard band) and BLOSUM62 11/1, planted near-copies scoring above
-    2048 and above 32767 in both the inter and the intra part.  In a batch
+    gaps (BLOSUM50 / 2) and BLOSUM62 11/1, planted near-copies scoring above
+    the fp16 bound (~4,000) and above 32767 in both the inter and the intra
+    part.  In a batch
     each query's rescue tail runs on the tail stream beside the next query's
     fp16 passes (parity lists, own boundary rows, profile slots reused after
     4 queries): every query equals the oracle and its single-query scan,
@@ -392,9 +392,11 @@ def test_db_save_load_roundtrip(sw, oracle, handle, tmp_path):
 @pytest.mark.parametrize("qlen,selfhit", [(375, True), (900, True), (2400, False)])
 def test_fp16_guard_band(sw, oracle, handle, monkeypatch, qlen, selfhit, scoring):
     """The fp16 kernels (biased cells: stored values sit up to 26 ge above
-    the true ones) are exact below 2048 - 2 max S - 26 ge and flag their block
-    otherwise: subjects scoring around and far above 2048 (planted near-copies
-    of the query) next to ordinary ones, affine (BLOSUM62 11/1 and 13/3) and
+    the true ones, all of them offset by -2048 + 2 ge) are exact below
+    4096 - 2 ge - 2 max S - 26 ge and flag their block otherwise: subjects
+    scoring around and far above 2048 and 4096 (planted near-copies of the
+    query: the 375-aa self-hits score 1,935-2,473, the 900-aa ones
+    4,655-5,932) next to ordinary ones, affine (BLOSUM62 11/1 and 13/3) and
     linear (BLOSUM50, gap 2 and 5) against the oracle."""
     mid, go, ge = scoring
     monkeypatch.setenv("SW_INTER_VARIANT", "f32x8")
@@ -446,7 +448,7 @@ def test_wave_pair_kernel(sw, oracle, handle, monkeypatch, variant, width, group
         else:
             assert pairs == 0
         if qlen == 900:
-            assert want.max() > 2048  # the fp16 guard band is crossed
+            assert want.max() > 4096  # the fp16 guard band is crossed
 
 
 @pytest.mark.parametrize("packed,ri", [("1", ""), ("1", "6"), ("1", "10"), ("0", "")])
@@ -456,7 +458,8 @@ def test_intra_two_subjects_per_wave(sw, oracle, handle, monkeypatch, packed, ri
     40..2100, one to several chunk passes) or forced to the 2-row-element
     shapes 6 and 10, an odd number of long subjects, pairs of unequal length,
     linear and affine scoring, and planted near-copies of the query whose fp16
-    maxima cross 2048 (re-scored by sw_intra in list mode)."""
+    maxima cross the fp16 bound (~4,000: cells offset by -2048 + 2 ge;
+    re-scored by sw_intra in list mode)."""
     monkeypatch.setenv("SW_INTRA_X2", packed)
     if ri:
         monkeypatch.setenv("SW_INTRA_X2_RI", ri)
@@ -477,19 +480,21 @@ def test_intra_two_subjects_per_wave(sw, oracle, handle, monkeypatch, packed, ri
         want = oracle.scan(q, r, o, mat=m, gap_open=go, gap_extend=ge)
         assert np.array_equal(got, want), (qlen, mid, go, ge, np.nonzero(got != want)[0][:10])
         if qlen >= 1500:
-            assert want.max() > 2048
+            assert want.max() > 4096
 
 
 @pytest.mark.parametrize("order", ["", "0", "1"])
 def test_intra_rescue_chain_fp16_int16_int32(sw, oracle, handle, monkeypatch, order):
     """The intra rescue chain end to end: sw_intra_x2 (fp16) flags subjects
-    near 2048 into list 1, its int16 form re-scores list 1 and flags those
-    near 32767 into list 2, and int32 sw_intra re-scores list 2.  Cheap linear
-    gaps (the reference scoring, BLOSUM50, 2 per gap) make random 5k-aa pairs score
-    in the thousands; a planted copy of the 6,500-aa query scores above 32767;
+    near its bound (4096 - 2 ge - 2 max S - 26 ge: cells offset by -2048 +
+    2 ge) into list 1, its int16 form re-scores list 1 and flags those near
+    32767 into list 2, and int32 sw_intra re-scores list 2.  Cheap linear
+    gaps (the reference scoring, BLOSUM50, 2 per gap) make random 5k-aa pairs
+    score 2,300-7,100 (13 of the 19 above the bound); a planted copy of the
+    6,500-aa query scores above 32767;
     ordinary subjects sit next to both in the same pairs.  The chain's order
     (SW_INTRA_I16_FIRST): adaptive (int16 first once a scan with the same
-    scoring flagged over half of the long subjects at a query no longer than
+    scoring flagged over a third of the long subjects at a query no longer than
     this one), never, always."""
     if order:
         monkeypatch.setenv("SW_INTRA_I16_FIRST", order)
@@ -514,24 +519,27 @@ def test_intra_rescue_chain_fp16_int16_int32(sw, oracle, handle, monkeypatch, or
             i16 = handle.last_intra_kernel().endswith(",int16>")
             assert i16 == (order == "1" or (order == "" and rnd == 2)), (order, rnd, len(qq))
             if len(qq) == 5000:
-                assert (w >= 1966).sum() * 2 > len(subs) or ge == 1
+                assert (w >= 4010).sum() * 3 > len(subs) or ge == 1
         assert want.max() > 32767
-        assert ((want > 2048) & (want < 32000)).sum() >= (2 if ge == 2 else 1)
+        assert ((want > 4096) & (want < 32000)).sum() >= (2 if ge == 2 else 1)
 
 
 def test_inter_widest_blocks_int16_first(sw, oracle, handle, monkeypatch):
-    """Long queries under the reference scoring (BLOSUM50, linear 2) put the
-    widest blocks in the fp16 guard band; once a scan has flagged most of
-    blocks [0, span), later scans with queries at least as long run those
-    blocks in int16 by wave pairs beside the fp16 launch (SW_INTER_I16_SPAN
-    forces a span: one block, some, more than the pair blocks, all of them;
-    and under affine scoring).  Every scan bit-exact against the oracle."""
+    """Long queries whose scores against the widest blocks leave the fp16
+    range (true scores up to ~4,000; here BLOSUM50 + 3 with linear gap 2,
+    under which random 2,600 x 1,650 pairs score 4,900-8,200, while short
+    subjects stay below 1,800) put those blocks in the fp16 guard band; once
+    a scan has flagged most of blocks [0, span), later scans with queries at
+    least as long run those blocks in int16 by wave pairs beside the fp16
+    launch (SW_INTER_I16_SPAN forces a span: one block, some, more than the
+    pair blocks, all of them; and under affine scoring).  Every scan
+    bit-exact against the oracle."""
     r1, o1 = sw.synth.fixed_length_database(1280, 1650, 200, shard=41)
     r2, o2 = sw.synth.fixed_length_database(3000, 250, 80, shard=42)
     r = np.concatenate([r1, r2])
     o = np.concatenate([o1, o2[1:] + o1[-1]])
     q = sw.synth.query(2600, shard=43)
-    m = sw.capi.builtin_matrix(0)
+    m = (np.asarray(sw.capi.builtin_matrix(0), dtype=np.int32) + 3).astype(np.int8)
     db = sw.Database(handle, r, o, long_threshold=4096)
     assert db.stats()["n_long"] == 0
     want = oracle.scan(q, r, o, mat=m, gap_open=2, gap_extend=2)
