@@ -811,8 +811,9 @@ def main():
             "vs_baseline": None,
             "dtype": ("fp16" if ("fp16" in roof_kernel or "intra_x2" in roof_kernel)
                       else "int16" if "_x2" in roof_kernel else "int32"),
-            "dtype_note": "the DP cells compute in packed 16-bit pairs (fp16 holds every integer up to 2048 "
-                          "exactly; a lane whose maximum nears that bound is re-scored in int16, then int32); "
+            "dtype_note": "the DP cells compute in packed 16-bit pairs (fp16 holds every integer in [-2048, "
+                          "2048] exactly and the cells are offset by -2048 + 2 ge, so scores up to ~4,000 stay "
+                          "exact; a lane whose maximum nears that bound is re-scored in int16, then int32); "
                           "scores are bit-exact int32",
             "data": "synthetic",
             "config": {
