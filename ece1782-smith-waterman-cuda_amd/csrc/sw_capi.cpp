@@ -301,6 +301,7 @@ struct sw_db {
     size_t res_bytes = 0;
     uint64_t* d_blk_off = nullptr;
     uint32_t* d_blk_groups = nullptr;
+    uint32_t* d_blk_cols = nullptr;      // block widths rounded to 8 columns (sw_inter_x2s)
     int32_t* d_lane_ids = nullptr;
     int32_t* d_bnd_h = nullptr;
     int32_t* d_bnd_f = nullptr;
@@ -432,12 +433,13 @@ int32_t default_long_threshold(const sw_db* db) {
 }
 
 void free_dev(sw_db* db) {
-    void* ptrs[] = {db->d_res, db->d_blk_off, db->d_blk_groups, db->d_lane_ids, db->d_bnd_h, db->d_bnd_f,
+    void* ptrs[] = {db->d_res, db->d_blk_off, db->d_blk_groups, db->d_blk_cols, db->d_lane_ids, db->d_bnd_h, db->d_bnd_f,
                     db->d_rescue, db->d_lres, db->d_loff, db->d_llen, db->d_lid, db->d_lbnd_h, db->d_lbnd_f,
                     db->d_lrescue, db->d_rbnd_h, db->d_rbnd_f, db->d_rlbnd_h, db->d_rlbnd_f};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     db->d_res = nullptr; db->d_blk_off = nullptr; db->d_blk_groups = nullptr; db->d_lane_ids = nullptr;
+    db->d_blk_cols = nullptr;
     db->d_bnd_h = nullptr; db->d_bnd_f = nullptr; db->d_rescue = nullptr; db->d_lres = nullptr; db->d_loff = nullptr;
     db->d_llen = nullptr; db->d_lid = nullptr; db->d_lbnd_h = nullptr; db->d_lbnd_f = nullptr;
     db->d_lrescue = nullptr;
@@ -623,7 +625,7 @@ int build_db(sw_db* db) {
     const int64_t nshort = n - nlong;
     const int64_t nblocks = (nshort + swk::kLanes - 1) / swk::kLanes;
     std::vector<uint64_t> blk_off(nblocks + 1);
-    std::vector<uint32_t> blk_groups(nblocks);
+    std::vector<uint32_t> blk_groups(nblocks), blk_cols(nblocks);
     std::vector<int32_t> lane_ids(nblocks * swk::kLanes, -1);
     std::vector<int64_t> blk_res(nblocks, 0);  // unpadded residues per block
     uint64_t total = 0;
@@ -632,6 +634,7 @@ int build_db(sw_db* db) {
         const int64_t w = round_up(len(order[first]), swk::kGroupCols);
         blk_off[b] = total;
         blk_groups[b] = static_cast<uint32_t>(w / swk::kGroupCols);
+        blk_cols[b] = static_cast<uint32_t>(round_up(len(order[first]), 8));
         total += static_cast<uint64_t>(blk_groups[b]) * swk::kGroupBytes;
     }
     blk_off[nblocks] = total;
@@ -692,6 +695,7 @@ int build_db(sw_db* db) {
     }
     if ((rc = upload(&db->d_blk_off, blk_off, s, &acc))) return rc;
     if ((rc = upload(&db->d_blk_groups, blk_groups, s, &acc))) return rc;
+    if ((rc = upload(&db->d_blk_cols, blk_cols, s, &acc))) return rc;
     if ((rc = upload(&db->d_lane_ids, lane_ids, s, &acc))) return rc;
     loff.pop_back();
     if ((rc = upload(&db->d_loff, loff, s, &acc))) return rc;
@@ -1436,6 +1440,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         a.residues = db->d_res;
         a.blk_off = db->d_blk_off;
         a.blk_groups = db->d_blk_groups;
+        if (!std::getenv("SW_BLK_COLS16")) a.blk_cols = db->d_blk_cols;
         a.lane_ids = db->d_lane_ids;
         a.nblocks = static_cast<int32_t>(db->nblocks);
         a.prof = P.dev + (x2 ? P.off16 : P.off8);

@@ -759,9 +759,17 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
 #endif
 constexpr bool kChainPasses = SW_X2_CHAIN != 0;
 
+// A block's width for the fp16 / int16 kernels: the longest subject rounded
+// up to 8 columns when the host provides it (the last 16-column group may be
+// half used: 8 pad columns fewer per pass for half the blocks, C2 2.1 -> 1.0 %
+// of the cells; C2 +1.2 %, C3 +1.0 %, profiles/r03_ab/cols8/).
+__device__ __forceinline__ uint32_t block_cols(const InterArgs& a, int blk) {
+    return a.blk_cols ? a.blk_cols[blk] : a.blk_groups[blk] * kGroupCols;
+}
+
 template <int R, int SG, bool AFFINE, bool F16, int CR>
 __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>& L, int lane) {
-    const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
+    const uint32_t ncols = block_cols(a, blk);
     const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
     Best<F16> best;
     best.init(a);
@@ -878,7 +886,7 @@ __device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, int quad_end
     int tmax = 0;
     for (int q = 0; q < NG; ++q) {
         const int b = first + q;
-        if (b < npair) tmax = max(tmax, group_ticks(a.blk_groups[b] * kGroupCols, passes, SG, G));
+        if (b < npair) tmax = max(tmax, group_ticks(block_cols(a, b), passes, SG, G));
     }
     const int blk = first + gi;
     Best<F16> best;
@@ -886,7 +894,7 @@ __device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, int quad_end
     int tick = 0;
     const uint64_t t0 = trace_now();
     if (blk < npair) {
-        const uint32_t ncols = a.blk_groups[blk] * kGroupCols;
+        const uint32_t ncols = block_cols(a, blk);
         const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
         const int per = max(static_cast<int>(ncols) / SG + 1, G * kPairLag);
         const int4* rin = w > 0 ? ring[gi * (G - 1) + w - 1] : nullptr;

@@ -51,6 +51,9 @@ struct InterArgs {
     const uint8_t* residues;
     const uint64_t* blk_off;     // byte offset of group 0 of each block
     const uint32_t* blk_groups;  // number of 16-column groups per block
+    // the single-wave fp16/int16 kernel's block widths: the longest subject
+    // rounded up to 8 columns, not 16 (nullable: groups x 16)
+    const uint32_t* blk_cols;
     const int32_t* lane_ids;     // [nblocks][64] result slot, -1 = empty lane
     int32_t nblocks;
     const int8_t* prof;          // [kProfileRows][prof_stride] query profile (see host)
