@@ -23,12 +23,13 @@ MATRIX_BLOSUM50_CHAR = 3  # the _char path's table as its lookup reads it ('*' =
 
 # Every symbol include/sw_amd.h declares (checked by tests/test_abi.py).
 EXPORTED = (
-    "sw_version", "sw_last_error", "sw_encode", "sw_builtin_matrix",
+    "sw_version", "sw_build_id", "sw_last_error", "sw_encode", "sw_builtin_matrix",
     "sw_create", "sw_destroy", "sw_stream", "sw_set_stream",
     "sw_db_create", "sw_db_free", "sw_db_get_stats", "sw_db_set_long_threshold",
     "sw_scan", "sw_scan_device", "sw_scan_batch", "sw_scan_batch_device", "sw_get_timing",
     "sw_timing_reset", "sw_timing_total", "sw_last_kernel", "sw_last_intra_kernel",
-    "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_topk_device_ids", "sw_score_pair", "sw_align",
+    "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_topk_device_ids", "sw_scan_topk", "sw_score_pair",
+    "sw_align",
     "sw_db_save", "sw_db_load", "sw_db_subjects", "sw_db_create_synthetic", "sw_synth_tables",
     "sw_synth_lengths", "sw_group_create", "sw_group_destroy", "sw_group_info", "sw_group_handle",
     "sw_group_db_create", "sw_group_db_free", "sw_group_db_shard", "sw_group_scan", "sw_group_topk",
@@ -95,6 +96,7 @@ def lib():
     i64p = ctypes.POINTER(ctypes.c_int64)
     sig = {
         "sw_version": (i32, []),
+        "sw_build_id": (ctypes.c_char_p, []),
         "sw_last_error": (ctypes.c_char_p, []),
         "sw_encode": (ctypes.c_int, [ctypes.c_char_p, i64, u8p]),
         "sw_builtin_matrix": (ctypes.c_int, [i32, ctypes.POINTER(ctypes.c_int8)]),
@@ -127,6 +129,7 @@ def lib():
         "sw_topk_device": (ctypes.c_int, [vp, vp, i64, i64, i32, vp]),
         "sw_topk_keys_device": (ctypes.c_int, [vp, vp, i64, i32, vp]),
         "sw_topk_device_ids": (ctypes.c_int, [vp, vp, i64, vp, i32, vp]),
+        "sw_scan_topk": (ctypes.c_int, [vp, vp, u8p, i32, ctypes.POINTER(Scoring), i32, i64p]),
         "sw_score_pair": (ctypes.c_int, [vp, u8p, i32, u8p, i32, ctypes.POINTER(Scoring), i32p]),
         "sw_group_create": (ctypes.c_int, [i32p, i32, ctypes.POINTER(vp)]),
         "sw_group_destroy": (ctypes.c_int, [vp]),
@@ -142,8 +145,28 @@ def lib():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    built, want = L.sw_build_id().decode(), source_id()
+    if built != want:
+        raise SWError("stale HIP library %s: built from sources %s, the tree's are %s; rebuild it "
+                      "(__graft_entry__.build() or make -C ece1782-smith-waterman-cuda_amd/csrc)"
+                      % (LIB_PATH, built, want))
     _LIB = L
     return L
+
+
+def source_id(repo_root=None):
+    """The id of the library sources in this tree (csrc/build_id.py, the
+    same computation the Makefile compiles into sw_build_id)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_sw_build_id", os.path.join(PKG_DIR, "csrc", "build_id.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.source_id(repo_root or os.path.dirname(PKG_DIR))
+
+
+def build_id():
+    """sw_build_id() of the loaded library."""
+    return lib().sw_build_id().decode()
 
 
 def _check(rc):
@@ -376,6 +399,16 @@ class Database:
         sc = _ScoringArg(matrix, gap_open, gap_extend)
         _check(lib().sw_scan_device(self.handle.ptr, self._d, qp, len(q), sc.ptr(),
                                     ctypes.c_void_p(scores_dev_ptr)))
+
+    def scan_topk(self, query_codes, k, matrix=None, gap_open=2, gap_extend=None):
+        """The k best subjects as int64 keys (score << 32 | 2^31-1-id, best
+        first; sw_scan_topk: scan + device top-K, k keys copied back)."""
+        q, qp = _u8(query_codes)
+        sc = _ScoringArg(matrix, gap_open, gap_extend)
+        out = np.zeros(k, dtype=np.int64)
+        _check(lib().sw_scan_topk(self.handle.ptr, self._d, qp, len(q), sc.ptr(), k,
+                                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        return out
 
     def align(self, query_codes, ids, matrix=None, gap=2, gap_extend=None):
         """Traceback of the query against the subjects with these result ids

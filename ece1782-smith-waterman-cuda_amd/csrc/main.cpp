@@ -14,8 +14,16 @@
 // writes OUT (sw_db_save) and exits; --db X.swdb scans such a file with the
 // same output (same ids, same order) as the FASTA it came from, without
 // parsing FASTA.
+// Scoring (the reference hard-wires BLOSUM50 and a linear gap of 2,
+// SWSolver.cu:7-8,54-81): --matrix blosum50|blosum62|FILE, --gap-open G,
+// --gap-extend E (a k-residue gap costs G + (k-1) E; E defaults to G, i.e.
+// linear, G to the reference's 2).  --topk K prints only the K best subjects
+// (score descending, record id ascending), ranked on the device.  Without
+// these flags the output is the reference's, byte for byte.
 #include <sys/time.h>
 
+#include <algorithm>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
@@ -42,7 +50,20 @@ void usage() {
               << "  --query arg           Path to query file (required)\n"
               << "  --db arg              Path to database file (required; FASTA, or a .swdb file)\n"
               << "  --make-db arg         Write the FASTA --db as a binary .swdb database and exit\n"
-              << "  --gpus arg            Shard the FASTA database over this many GPUs (default 1)\n";
+              << "  --gpus arg            Shard the FASTA database over this many GPUs (default 1)\n"
+              << "  --matrix arg          blosum50 (default, the reference's), blosum62, or a matrix file\n"
+              << "  --gap-open arg        Cost of a gap's first residue (default 2)\n"
+              << "  --gap-extend arg      Cost of each further gap residue (default: --gap-open, linear)\n"
+              << "  --topk arg            Print only the arg best subjects (score desc, id asc)\n";
+}
+
+// a whole-string integer in [lo, hi]
+bool parse_int(const std::string& s, long lo, long hi, int* out) {
+    char* end = nullptr;
+    const long v = std::strtol(s.c_str(), &end, 10);
+    if (s.empty() || *end != '\0' || v < lo || v > hi) return false;
+    *out = static_cast<int>(v);
+    return true;
 }
 
 }  // namespace
@@ -65,7 +86,8 @@ int main(int argc, char* argv[]) {
             if (i + 1 >= argc) { usage(); return 1; }
             val = argv[++i];
         }
-        if (key != "query" && key != "db" && key != "metrics-json" && key != "make-db" && key != "gpus") {
+        if (key != "query" && key != "db" && key != "metrics-json" && key != "make-db" && key != "gpus" &&
+            key != "matrix" && key != "gap-open" && key != "gap-extend" && key != "topk") {
             std::cerr << "unrecognised option '--" << key << "'\n";
             return 1;
         }
@@ -94,6 +116,31 @@ int main(int argc, char* argv[]) {
         if (n < 1) { usage(); return 1; }
         sw_solver_set_gpus(n);
     }
+    // scoring: the reference's unless a scoring flag is given
+    const bool custom = opt.count("matrix") || opt.count("gap-open") || opt.count("gap-extend");
+    int8_t mat[625];
+    int gap_open = 2, gap_extend = 2, topk = 0;
+    if (custom) {
+        std::string err;
+        if (!sw_solver_read_matrix(opt.count("matrix") ? opt["matrix"] : "blosum50", mat, &err)) {
+            std::cerr << "--matrix " << err << "\n";
+            return 1;
+        }
+        if (opt.count("gap-open") && !parse_int(opt["gap-open"], 1, 1000, &gap_open)) {
+            std::cerr << "--gap-open must be an integer in 1..1000\n";
+            return 1;
+        }
+        gap_extend = gap_open;
+        if (opt.count("gap-extend") && !parse_int(opt["gap-extend"], 1, 1000, &gap_extend)) {
+            std::cerr << "--gap-extend must be an integer in 1..1000\n";
+            return 1;
+        }
+        sw_solver_set_scoring(mat, gap_open, gap_extend);
+    }
+    if (opt.count("topk") && !parse_int(opt["topk"], 1, INT32_MAX, &topk)) {
+        std::cerr << "--topk must be a positive integer\n";
+        return 1;
+    }
     const std::string& dbpath = opt["db"];
     const bool binary = dbpath.size() > 5 && dbpath.compare(dbpath.size() - 5, 5, ".swdb") == 0;
 
@@ -113,7 +160,8 @@ int main(int argc, char* argv[]) {
         parse_s = now_s() - t_parse;
         const double t_solve = now_s();
         try {
-            smith_waterman_cuda(query, db, result);
+            if (topk) result = smith_waterman_cuda_topk(query, db, topk);
+            else smith_waterman_cuda(query, db, result);
         } catch (const std::exception& e) {
             std::cerr << e.what() << "\n";
             return 1;
@@ -138,19 +186,42 @@ int main(int argc, char* argv[]) {
         std::vector<int32_t> ids(static_cast<size_t>(st.n_subjects));
         sw_db_subjects(sdb, lens.data(), ids.data());
         std::string q = query.get_buffer();
-        while (q.size() % 8 != 0) q += "/";  // the reference pads the query (SWSolver.cu:267-269)
+        // the reference pads the query (SWSolver.cu:267-269); its pad rows
+        // score 0 only under its own table (see swsolver.cpp encode_query)
+        while (!custom && q.size() % 8 != 0) q += "/";
         std::vector<uint8_t> qc(q.size());
         sw_encode(q.data(), static_cast<int64_t>(q.size()), qc.data());
-        std::vector<int32_t> scores(static_cast<size_t>(st.max_id + 1), 0);
-        const sw_scoring sc = {nullptr, 2, 2};  // BLOSUM50 (SWSolver.cu:54-81), gap 2 (:7)
+        // BLOSUM50 (SWSolver.cu:54-81), gap 2 (:7), unless chosen
+        const sw_scoring sc = {custom ? mat : nullptr, gap_open, gap_extend};
         const double t_solve = now_s();
-        if (st.n_subjects && sw_scan(h, sdb, qc.data(), static_cast<int32_t>(qc.size()), &sc, scores.data()))
-            return die("sw_scan");
-        solve_s = now_s() - t_solve;
-        for (int64_t k = 0; k < st.n_subjects; ++k) {
-            result.push_back(std::make_pair(static_cast<int>(ids[k]), scores[ids[k]]));
-            length_sum += lens[k];
+        if (topk && topk <= 4096) {
+            std::vector<int64_t> keys(static_cast<size_t>(topk));
+            if (sw_scan_topk(h, sdb, qc.data(), static_cast<int32_t>(qc.size()), &sc, topk, keys.data()))
+                return die("sw_scan_topk");
+            for (int64_t key : keys) {
+                if (key == INT64_MIN) break;
+                result.push_back(std::make_pair(static_cast<int>((int64_t{1} << 31) - 1 - (key & 0xffffffff)),
+                                                static_cast<int>(key >> 32)));
+            }
+        } else {
+            std::vector<int32_t> scores(static_cast<size_t>(st.max_id + 1), 0);
+            if (st.n_subjects && sw_scan(h, sdb, qc.data(), static_cast<int32_t>(qc.size()), &sc, scores.data()))
+                return die("sw_scan");
+            for (int64_t k = 0; k < st.n_subjects; ++k)
+                result.push_back(std::make_pair(static_cast<int>(ids[k]), scores[ids[k]]));
+            if (topk) {  // beyond the device top-K's 4096: ranked here
+                const size_t kk = std::min<size_t>(result.size(), static_cast<size_t>(topk));
+                std::partial_sort(result.begin(), result.begin() + kk, result.end(),
+                                  [](const seqid_score& a, const seqid_score& b) {
+                                      return a.second != b.second ? a.second > b.second : a.first < b.first;
+                                  });
+                result.resize(kk);
+            }
         }
+        solve_s = now_s() - t_solve;
+        // the FASTA parser's padded sizes (TILE_SIZE, FASTAParsers.h): files
+        // hold the subjects as written (older ones '/'-padded: the same sums)
+        for (int64_t k = 0; k < st.n_subjects; ++k) length_sum += roundUp(static_cast<int>(lens[k]), TILE_SIZE);
         num_subjects = st.n_subjects;
         sw_db_free(sdb);
         sw_destroy(h);

@@ -303,6 +303,7 @@ struct sw_db {
     uint32_t* d_blk_groups = nullptr;
     uint32_t* d_blk_cols = nullptr;      // block widths rounded to 8 columns (sw_inter_x2s)
     int32_t* d_lane_ids = nullptr;
+    int32_t* d_ids = nullptr;            // every subject's result id (sw_scan_topk), on first use
     int32_t* d_bnd_h = nullptr;
     int32_t* d_bnd_f = nullptr;
     // two rescue lists [count, block ids...] of nblocks + 1 ints each: the
@@ -435,7 +436,7 @@ int32_t default_long_threshold(const sw_db* db) {
 void free_dev(sw_db* db) {
     void* ptrs[] = {db->d_res, db->d_blk_off, db->d_blk_groups, db->d_blk_cols, db->d_lane_ids, db->d_bnd_h, db->d_bnd_f,
                     db->d_rescue, db->d_lres, db->d_loff, db->d_llen, db->d_lid, db->d_lbnd_h, db->d_lbnd_f,
-                    db->d_lrescue, db->d_rbnd_h, db->d_rbnd_f, db->d_rlbnd_h, db->d_rlbnd_f};
+                    db->d_lrescue, db->d_rbnd_h, db->d_rbnd_f, db->d_rlbnd_h, db->d_rlbnd_f, db->d_ids};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     db->d_res = nullptr; db->d_blk_off = nullptr; db->d_blk_groups = nullptr; db->d_lane_ids = nullptr;
@@ -444,6 +445,7 @@ void free_dev(sw_db* db) {
     db->d_llen = nullptr; db->d_lid = nullptr; db->d_lbnd_h = nullptr; db->d_lbnd_f = nullptr;
     db->d_lrescue = nullptr;
     db->d_rbnd_h = db->d_rbnd_f = db->d_rlbnd_h = db->d_rlbnd_f = nullptr;
+    db->d_ids = nullptr;
     db->rbnd_tried = false;
     for (auto& t : db->lpt_tables) (void)hipFree(t.d_order);
     db->lpt_tables.clear();
@@ -766,28 +768,36 @@ int ensure_bnd(sw_db* db, bool affine, bool intra_f) {
     return SW_OK;
 }
 
-// The deferred tails' own boundary rows (same sizes as ensure_bnd's), tried
-// once per layout; false when device memory would drop below a quarter of
-// the card's (a 50M-subject database keeps its tails in stream order).
-bool ensure_rbnd(sw_db* db) {
-    if (db->d_rbnd_h || db->d_rlbnd_h) return true;
-    if (db->rbnd_tried) return false;
-    db->rbnd_tried = true;
-    const size_t need = db->res_bytes * 8 + db->lres_bytes * 8;
-    size_t freeb = 0, totalb = 0;
-    if (hipMemGetInfo(&freeb, &totalb) != hipSuccess || freeb < need + totalb / 4) return false;
+// The deferred tails' own boundary rows, sized as ensure_bnd's: H always, F
+// only for affine scoring (inter) or when the intra form keeps F (intra_f).
+// Arrays a later scan needs are allocated then.  False when device memory
+// would drop below a quarter of the card's (a 50M-subject database keeps its
+// tails in stream order); a refused size is not tried again for this layout.
+bool ensure_rbnd(sw_db* db, bool affine, bool intra_f) {
     void** p[4] = {reinterpret_cast<void**>(&db->d_rbnd_h), reinterpret_cast<void**>(&db->d_rbnd_f),
                    reinterpret_cast<void**>(&db->d_rlbnd_h), reinterpret_cast<void**>(&db->d_rlbnd_f)};
-    const size_t sz[4] = {db->res_bytes * 4, db->res_bytes * 4, db->lres_bytes * 4, db->lres_bytes * 4};
+    const size_t sz[4] = {db->res_bytes * 4, affine ? db->res_bytes * 4 : 0, db->lres_bytes * 4,
+                          (affine || intra_f) ? db->lres_bytes * 4 : 0};
+    size_t need = 0;
     for (int k = 0; k < 4; ++k)
-        if (sz[k] && hipMalloc(p[k], sz[k]) != hipSuccess) {
-            for (int j = 0; j < 4; ++j)
-                if (*p[j]) (void)hipFree(*p[j]);
-            for (int j = 0; j < 4; ++j) *p[j] = nullptr;
-            (void)hipGetLastError();
-            return false;
+        if (sz[k] && !*p[k]) need += sz[k];
+    if (need == 0) return true;
+    if (db->rbnd_tried) return false;
+    size_t freeb = 0, totalb = 0;
+    if (hipMemGetInfo(&freeb, &totalb) != hipSuccess || freeb < need + totalb / 4) {
+        db->rbnd_tried = true;
+        return false;
+    }
+    for (int k = 0; k < 4; ++k)
+        if (sz[k] && !*p[k]) {
+            if (hipMalloc(p[k], sz[k]) != hipSuccess) {
+                *p[k] = nullptr;
+                (void)hipGetLastError();
+                db->rbnd_tried = true;
+                return false;
+            }
+            db->device_bytes += sz[k];
         }
-    db->device_bytes += need;
     return true;
 }
 
@@ -1042,6 +1052,18 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     return SW_OK;
 }
 
+// The handle's stream waits for every deferred rescue tail still pending, so
+// what completes on it (a non-deferred scan, the end of a batch) includes
+// the rescued scores of the scans before it.
+int join_tails(sw_handle* h) {
+    for (int q = 0; q < 2; ++q)
+        if (h->tail_pending[q]) {
+            HIPCHECK(hipStreamWaitEvent(h->stream, h->tail_done[q], 0));
+            h->tail_pending[q] = false;
+        }
+    return SW_OK;
+}
+
 int next_events(sw_handle* h) {
     if (h->nscans >= 4096) h->nscans = 0;  // bound the pool; older sums are dropped
     if (h->nscans == h->evpool.size()) {
@@ -1194,6 +1216,9 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         db->last_npair = 0;
         h->last_kernel = "none";
         h->last_intra = "none";
+        // a non-deferred scan completes on the handle's stream: so do the
+        // earlier scans' deferred tails (a batch may end with an empty query)
+        if (!defer && (rc = join_tails(h))) return rc;
         MARK(0, h->stream);
         if (db->max_id >= 0)
             HIPCHECK(hipMemsetAsync(scores_dev, 0, static_cast<size_t>(db->max_id + 1) * 4, h->stream));
@@ -1247,7 +1272,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     int32_t* const list1 = db->d_lrescue ? db->d_lrescue + par * lstride : nullptr;  // flagged by the fp16 pass
     int32_t* const list2 = list1 ? list1 + db->nlong + 1 : nullptr;                  // ... and again by int16
     // the rescue tail on its own stream and boundary rows (see sw_handle::tail)
-    const bool deferred = defer && (!(multi_inter || multi_intra) || ensure_rbnd(db));
+    const bool deferred = defer && (!(multi_inter || multi_intra) || ensure_rbnd(db, affine, intra_x2));
     hipStream_t const ts = deferred ? h->tail : h->stream;
 
     // the profiles, and the rescue lists' counters (inter A, B, largest
@@ -1591,12 +1616,8 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // (the merged launch has no separate inter end, nor a side stream to join)
     if (!lpt) MARK(2, h->stream);
     if (db->nlong && !lpt) HIPCHECK(hipStreamWaitEvent(h->stream, h->ev[1], 0));
-    if (!deferred)  // the scan completes on the handle's stream: so do earlier deferred tails
-        for (int q = 0; q < 2; ++q)
-            if (h->tail_pending[q]) {
-                HIPCHECK(hipStreamWaitEvent(h->stream, h->tail_done[q], 0));
-                h->tail_pending[q] = false;
-            }
+    // the scan completes on the handle's stream: so do earlier deferred tails
+    if (!deferred && (rc = join_tails(h))) return rc;
     MARK(3, h->stream);
     h->evpool[h->nscans - 1].launches = h->launches;
     h->timed = true;
@@ -1647,7 +1668,7 @@ int ensure_scores(sw_handle* h, size_t n) {
 
 namespace {
 int topk_impl(sw_handle* h, const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base,
-              const int32_t* ids, int32_t k, int64_t* out) {
+              const int32_t* ids, int32_t k, int64_t* out, bool by_id = false) {
     if (!h || !out || n < 0 || k <= 0 || k > 4096 || (n > 0 && !scores && !keys))
         return fail(SW_E_INVALID, "bad top-k arguments (1 <= k <= 4096)");
     if (id_base < 0 || id_base + n > (int64_t(1) << 31)) return fail(SW_E_INVALID, "ids must fit in 31 bits");
@@ -1661,7 +1682,7 @@ int topk_impl(sw_handle* h, const int32_t* scores, const int64_t* keys, int64_t 
         h->topk_cap = std::max<size_t>(need, 1 << 20);
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&h->d_topk_work), h->topk_cap));
     }
-    HIPCHECK(swk::launch_topk(scores, keys, n, id_base, ids, k, out, h->d_topk_work, h->stream));
+    HIPCHECK(swk::launch_topk(scores, keys, n, id_base, ids, k, out, h->d_topk_work, h->stream, by_id));
     return SW_OK;
 }
 }  // namespace
@@ -1670,6 +1691,11 @@ int topk_impl(sw_handle* h, const int32_t* scores, const int64_t* keys, int64_t 
 extern "C" {
 
 int32_t sw_version(void) { return 10000 * 0 + 100 * 1 + 0; }
+
+#ifndef SW_SOURCE_ID
+#define SW_SOURCE_ID "unknown"
+#endif
+const char* sw_build_id(void) { return SW_SOURCE_ID; }
 
 const char* sw_last_error(void) { return g_err.c_str(); }
 
@@ -2093,12 +2119,19 @@ int sw_scan_batch_device(sw_handle* h, const sw_db* db, const uint8_t* queries, 
     const size_t n = static_cast<size_t>(db->max_id + 1);
     // back to back on the handle's stream: no host synchronisation between
     // queries (profiles go through the slot ring), so the GPU never idles
-    // ... and each query's rescue tail runs beside the next query's passes
+    // ... and each query's rescue tail runs beside the next query's passes,
+    // when a later non-empty query (a real scan, which joins the tails) follows
+    int32_t last_scan = -1;
+    for (int32_t k = 0; k < nq; ++k)
+        if (qoffsets[k + 1] > qoffsets[k]) last_scan = k;
     for (int32_t k = 0; k < nq; ++k)
         if ((rc = scan_impl(h, db, queries + qoffsets[k], static_cast<int32_t>(qoffsets[k + 1] - qoffsets[k]), sc,
-                            scores_dev + k * n, k + 1 < nq)))
+                            scores_dev + k * n, k < last_scan)))
             return rc;
-    return SW_OK;
+    // every tail has joined the handle's stream by now; join again in case a
+    // scan above fell back to stream order after deferring an earlier one
+    HIPCHECK(hipSetDevice(h->device));
+    return join_tails(h);
 }
 
 int sw_scan_batch(sw_handle* h, const sw_db* db, const uint8_t* queries, const int64_t* qoffsets, int32_t nq,
@@ -2212,6 +2245,34 @@ int sw_topk_device_ids(sw_handle* h, const int32_t* scores_dev, int64_t n, const
 
 int sw_topk_keys_device(sw_handle* h, const int64_t* keys_dev, int64_t n, int32_t k, int64_t* keys_out_dev) {
     return topk_impl(h, nullptr, keys_dev, n, 0, nullptr, k, keys_out_dev);
+}
+
+int sw_scan_topk(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen, const sw_scoring* sc, int32_t k,
+                 int64_t* keys_host) {
+    sw_db* db = const_cast<sw_db*>(cdb);
+    if (!h || !db || !keys_host || k <= 0 || k > 4096) return fail(SW_E_INVALID, "bad argument (1 <= k <= 4096)");
+    if (db->n == 0) {
+        for (int32_t i = 0; i < k; ++i) keys_host[i] = INT64_MIN;
+        return SW_OK;
+    }
+    int rc;
+    HIPCHECK(hipSetDevice(h->device));
+    if (!db->built && (rc = build_db(db))) return rc;
+    if (!db->d_ids) {  // the ranking runs over the result ids of the subjects
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_ids), static_cast<size_t>(db->n) * sizeof(int32_t)));
+        HIPCHECK(hipMemcpy(db->d_ids, db->h_ids.data(), static_cast<size_t>(db->n) * sizeof(int32_t),
+                           hipMemcpyHostToDevice));
+        db->device_bytes += static_cast<size_t>(db->n) * sizeof(int32_t);
+    }
+    const size_t slots = static_cast<size_t>(db->max_id + 1);
+    if ((rc = ensure_scores(h, slots + static_cast<size_t>(2 * k) + 2))) return rc;  // scores, then the k keys
+    int64_t* keys_dev = reinterpret_cast<int64_t*>(h->d_scores + round_up(static_cast<int64_t>(slots), 2));
+    if ((rc = scan_impl(h, db, query, qlen, sc, h->d_scores))) return rc;
+    if ((rc = topk_impl(h, h->d_scores, nullptr, db->n, 0, db->d_ids, k, keys_dev, true))) return rc;
+    HIPCHECK(hipMemcpyAsync(keys_host, keys_dev, static_cast<size_t>(k) * sizeof(int64_t), hipMemcpyDeviceToHost,
+                            h->stream));
+    HIPCHECK(hipStreamSynchronize(h->stream));
+    return SW_OK;
 }
 
 int sw_align(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen, const sw_scoring* sc,

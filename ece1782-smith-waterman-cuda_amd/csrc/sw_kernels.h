@@ -267,8 +267,10 @@ struct ProfileArgs {
 hipError_t launch_build_profile(const ProfileArgs& a, hipStream_t s);
 
 // Device top-K (sw_topk.hip): keys = score << 32 | (2^31 - 1 - id), best first.
+// by_id: entry i is (scores[ids[i]], ids[i]) — a scan's scores[id] over the
+// database's result ids.
 size_t topk_workspace_bytes(int64_t n, int k);
 hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, const int32_t* ids, int k,
-                       int64_t* out, int64_t* work, hipStream_t s);
+                       int64_t* out, int64_t* work, hipStream_t s, bool by_id = false);
 
 }  // namespace swk

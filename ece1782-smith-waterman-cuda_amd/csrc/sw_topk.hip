@@ -38,9 +38,10 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
 
 // in_scores != nullptr: keys are built from scores (ids = id_base + i, or
 // ids[i] when an id map is given: a rank's residue-balanced shard of one
-// database holds scattered global ids); otherwise they come from in_keys.
-// FINAL: one workgroup, sorted output.
-template <bool FINAL>
+// database holds scattered global ids; BY_ID: entry i is scores[ids[i]], the
+// score array of a scan, indexed by result id); otherwise they come from
+// in_keys.  FINAL: one workgroup, sorted output.
+template <bool FINAL, bool BY_ID = false>
 __global__ __launch_bounds__(kTopkThreads) void sw_topk_select(const int32_t* __restrict__ in_scores,
                                                               const int64_t* __restrict__ in_keys, int64_t n,
                                                               int64_t id_base, const int32_t* __restrict__ ids,
@@ -60,7 +61,8 @@ __global__ __launch_bounds__(kTopkThreads) void sw_topk_select(const int32_t* __
         u[j] = 0;
         if (i < m) {
             const int64_t g = start + i;
-            u[j] = key_ord(in_scores ? make_key(in_scores[g], ids ? ids[g] : id_base + g) : in_keys[g]);
+            if (BY_ID) u[j] = key_ord(make_key(in_scores[ids[g]], ids[g]));
+            else u[j] = key_ord(in_scores ? make_key(in_scores[g], ids ? ids[g] : id_base + g) : in_keys[g]);
             all_and &= u[j];
             all_or |= u[j];
         }
@@ -200,16 +202,20 @@ size_t topk_workspace_bytes(int64_t n, int k) {
 }
 
 hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, const int32_t* ids,
-                       int k, int64_t* out, int64_t* work, hipStream_t s) {
-    if (k <= 0 || k > kTopkMaxK) return hipErrorInvalidValue;
+                       int k, int64_t* out, int64_t* work, hipStream_t s, bool by_id) {
+    if (k <= 0 || k > kTopkMaxK || (by_id && (!scores || !ids))) return hipErrorInvalidValue;
     const int32_t* sc = scores;
     const int64_t* kin = keys;
     int64_t cur = n;
     int64_t* w = work;
     while (cur > kTopkChunk) {  // each stage keeps k of every 16,384 keys (k <= 4,096)
         const int64_t chunks = (cur + kTopkChunk - 1) / kTopkChunk;
-        hipLaunchKernelGGL((sw_topk_select<false>), dim3(static_cast<unsigned>(chunks)), dim3(kTopkThreads), 0, s,
-                           sc, kin, cur, id_base, ids, k, w);
+        if (sc && by_id)
+            hipLaunchKernelGGL((sw_topk_select<false, true>), dim3(static_cast<unsigned>(chunks)), dim3(kTopkThreads),
+                               0, s, sc, kin, cur, id_base, ids, k, w);
+        else
+            hipLaunchKernelGGL((sw_topk_select<false>), dim3(static_cast<unsigned>(chunks)), dim3(kTopkThreads), 0, s,
+                               sc, kin, cur, id_base, ids, k, w);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         sc = nullptr;
@@ -217,8 +223,12 @@ hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, in
         cur = chunks * k;
         w += cur;
     }
-    hipLaunchKernelGGL((sw_topk_select<true>), dim3(1), dim3(kTopkThreads), 0, s, sc, kin, cur, id_base,
-                       sc ? ids : nullptr, k, out);
+    if (sc && by_id)
+        hipLaunchKernelGGL((sw_topk_select<true, true>), dim3(1), dim3(kTopkThreads), 0, s, sc, kin, cur, id_base, ids,
+                           k, out);
+    else
+        hipLaunchKernelGGL((sw_topk_select<true>), dim3(1), dim3(kTopkThreads), 0, s, sc, kin, cur, id_base,
+                           sc ? ids : nullptr, k, out);
     return hipGetLastError();
 }
 

@@ -114,6 +114,10 @@ typedef struct sw_db sw_db;
 
 /* ---- housekeeping ---------------------------------------------------- */
 SW_API int32_t sw_version(void);                         /* 10000*major + 100*minor + patch */
+/* The id of the sources this library was built from (16 hex digits of a
+ * SHA-256 over csrc/ and include/, csrc/build_id.py); the Python binding
+ * refuses a library whose id differs from the tree's (a stale build).     */
+SW_API const char* sw_build_id(void);
 SW_API const char* sw_last_error(void);                  /* thread-local text of the last failure */
 SW_API int sw_encode(const char* ascii, int64_t n, uint8_t* codes);    /* SWSolver.cu:91-120 */
 SW_API int sw_builtin_matrix(int32_t id, int8_t* out625);               /* SWSolver.cu:54-81 */
@@ -236,6 +240,14 @@ SW_API int sw_topk_device(sw_handle* h, const int32_t* scores_dev, int64_t n, in
                    int32_t k, int64_t* keys_out_dev);
 SW_API int sw_topk_keys_device(sw_handle* h, const int64_t* keys_dev, int64_t n, int32_t k,
                         int64_t* keys_out_dev);
+/* A scan and its ranking in one synchronous call: the k best subjects of
+ * the database for this query as int64 keys (sw_topk_device's: score << 32 |
+ * 2^31 - 1 - result id, score descending, id ascending; INT64_MIN past the
+ * database's end) in keys_host[k], from the device top-K over the scores of
+ * every subject — only k keys cross PCIe.  The ranked output of main --topk
+ * (the reference prints every score, main.cpp:58-60).  1 <= k <= 4096.    */
+SW_API int sw_scan_topk(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen,
+                        const sw_scoring* sc, int32_t k, int64_t* keys_host);
 /* Same as sw_topk_device with the global id of entry i read from
  * ids_dev[i] (device int32, >= 0) instead of id_base + i: a rank's
  * residue-balanced shard of one database holds scattered

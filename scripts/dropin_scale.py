@@ -47,9 +47,9 @@ def read_query(name):
         return "".join(f.read().split("\n")[1:])
 
 
-def run_main(query, fasta, gpus=1, env=None):
+def run_main(query, fasta, gpus=1, env=None, extra=()):
     cmd = [os.path.join(LIB, "main"), "--query", os.path.join(QDIR, query + ".fasta"), "--db", fasta,
-           "--metrics-json"]
+           "--metrics-json"] + list(extra)
     if gpus > 1:
         cmd += ["--gpus", str(gpus)]
     t = time.perf_counter()

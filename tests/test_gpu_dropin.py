@@ -116,3 +116,44 @@ def test_group_distinct_devices_cli(oracle, fasta_100k):
     out = subprocess.run([lib, "--query", qf, "--db", path, "--gpus", "2"], capture_output=True, text=True,
                          env=env, timeout=300)
     assert out.returncode != 0 and "device" in out.stderr
+
+
+def test_main_100k_headline_scoring_and_topk(sw, oracle, fasta_100k):
+    """The headline scoring through the drop-in CLI at scale: main --matrix
+    blosum62 --gap-open 12 --gap-extend 1 on 100,000 records equals the
+    oracle on every record; --topk 100 prints the oracle's top-100 (score
+    desc, id asc), one GPU and the sharded path (one device listed twice)."""
+    import dropin_scale
+    path, res, offs = fasta_100k
+    m = sw.capi.builtin_matrix(1)
+    q = oracle.encode(read_query("P07327"))  # not padded: a chosen scoring scans the query as written
+    want = oracle.scan(q, res, offs, mat=m, gap_open=12, gap_extend=1, nthreads=16)
+    flags = ["--matrix", "blosum62", "--gap-open", "12", "--gap-extend", "1"]
+    pairs, _, _ = dropin_scale.run_main("P07327", path, extra=flags)
+    got = np.zeros(100_000, dtype=np.int64)
+    got[pairs[:, 0]] = pairs[:, 1]
+    assert len(pairs) == 100_000 and np.array_equal(got, want)
+    order = np.lexsort((np.arange(len(want)), -want.astype(np.int64)))[:100]
+    top = np.stack([order, want[order]], axis=1)
+    for gpus, env in ((1, None), (2, dict(os.environ, SW_DEVICES="0,0"))):
+        tp, m2, _ = dropin_scale.run_main("P07327", path, gpus=gpus, env=env, extra=flags + ["--topk", "100"])
+        assert m2["gpus"] == gpus and np.array_equal(tp, top), gpus
+
+
+def test_scan_topk_ranks_result_ids(sw, oracle, handle):
+    """sw_scan_topk: the device top-K over the database's result ids only
+    (custom ids with gaps: unmapped score slots never appear), k beyond the
+    database padded with INT64_MIN, ties by id ascending."""
+    res, offs = sw.synth.database(3000, shard=17)
+    ids = np.random.default_rng(5).permutation(9000)[:3000].astype(np.int32)
+    db = sw.Database(handle, res, offs, ids=ids)
+    q = sw.encode(read_query("P02232"))
+    for mat, go, ge in ((None, 2, 2), (sw.capi.builtin_matrix(1), 12, 1)):
+        m = mat if mat is not None else sw.capi.builtin_matrix(0)
+        want = oracle.scan(q, res, offs, mat=m, gap_open=go, gap_extend=ge, nthreads=16)
+        for k in (1, 64, 3000, 4096):
+            keys = db.scan_topk(q, k, mat, go, ge)
+            assert np.array_equal(keys, sw.dist.local_topk(want, ids, k) if k <= 3000 else
+                                  np.concatenate([sw.dist.local_topk(want, ids, 3000),
+                                                  np.full(k - 3000, np.iinfo(np.int64).min)])), k
+    db.close()

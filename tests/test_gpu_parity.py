@@ -364,6 +364,17 @@ def test_batch_rescue_tails_overlap(sw, oracle, handle, scoring):
             assert np.array_equal(out[k], want[k]), (names[k], np.nonzero(out[k] != want[k])[0][:10])
     for k in (0, 3):
         assert np.array_equal(db.scan(qs[k], m, go, ge), want[k])
+    # empty queries at the end and in the middle of a batch: the
+    # batch still waits for every deferred rescue tail before it completes
+    empty = np.zeros(0, dtype=np.uint8)
+    for sel in ([0, 1, 2, None], [0, None, 3, None, None], [None, 6, 0]):
+        batch = [qs[k] if k is not None else empty for k in sel]
+        out = db.scan_batch(batch, m, go, ge)
+        for j, k in enumerate(sel):
+            if k is None:
+                assert not out[j].any()
+            else:
+                assert np.array_equal(out[j], want[k]), (sel, names[k])
     if mid == 0:
         assert max(int(w.max()) for w in want) > 32767  # the int32 stage ran
 
