@@ -600,9 +600,12 @@ def main():
     log("rank %d: share %d/%d: %d subjects, %d residues, generated + packed + resident in %.1fs: %s"
         % (rank, shard_rank, shard_world, n, residues, time.perf_counter() - t0, st))
 
-    # two score buffers: the top-K exchange of step i (on its own stream)
-    # overlaps the scan of step i + 1
-    scores_buf = [torch.zeros((nq, max(n, 1)), dtype=torch.int32, device=dev) for _ in range(2)]
+    # a ring of score buffers: the top-K exchange of step i (on its own
+    # stream) overlaps the scans after it; with 8 buffers the exchange that
+    # last read a buffer has finished long before the buffer is scanned into
+    # again, so the scan's stream usually needs no wait packet for it
+    NBUF = 8
+    scores_buf = [torch.zeros((nq, max(n, 1)), dtype=torch.int32, device=dev) for _ in range(NBUF)]
     K = args.topk
     top = torch.empty((nq, K), dtype=torch.int64, device=dev)
     gathered = torch.empty((world, nq, K), dtype=torch.int64, device=dev)
@@ -620,22 +623,25 @@ def main():
     if not args.no_overlap:
         xhandle = sw.Handle(gpu)
         xhandle.set_stream(xstream.cuda_stream)
-    scanned = [torch.cuda.Event(), torch.cuda.Event()]
-    ranked = [torch.cuda.Event(), torch.cuda.Event()]
+    ranked = [torch.cuda.Event() for _ in range(NBUF)]
     counter = [0]
 
     def step():
-        b = counter[0] % 2
+        b = counter[0] % NBUF
         counter[0] += 1
         scores = scores_buf[b]
-        if counter[0] > 2:
-            stream.wait_event(ranked[b])  # step i-2's top-K has read this buffer
+        # step i-NBUF's top-K has read this buffer (a wait is a packet the
+        # command processor spends ~5 us on: skipped when the host already
+        # sees the event complete)
+        if counter[0] > NBUF and not ranked[b].query():
+            stream.wait_event(ranked[b])
         if nq == 1:
             db.scan_device(queries[0], scores.data_ptr(), *scoring)
         else:
             db.scan_batch_device(queries, scores.data_ptr(), *scoring)
-        scanned[b].record(stream)
-        xstream.wait_event(scanned[b])
+        # the exchange waits for the scan's own end event (no record here)
+        if xstream is not stream:
+            handle.stream_wait_scan(xstream.cuda_stream)
         with torch.cuda.stream(xstream):
             # device top-K per query: int64 keys (score << 32 | 2^31-1-global id), best first
             for k in range(nq):
@@ -693,7 +699,7 @@ def main():
     final_keys = (final if world > 1 else top).cpu().numpy()
     top_ids, top_scores = sw.capi.decode_keys(final_keys[0])
     # the measured run's scores and keys (its last step's buffer), for the parity leg
-    gs = scores_buf[(counter[0] - 1) % 2].cpu().numpy()[:, :n]
+    gs = scores_buf[(counter[0] - 1) % NBUF].cpu().numpy()[:, :n]
     dev_top = top.cpu().numpy()
 
     ref = None

@@ -27,7 +27,7 @@ EXPORTED = (
     "sw_create", "sw_destroy", "sw_stream", "sw_set_stream",
     "sw_db_create", "sw_db_free", "sw_db_get_stats", "sw_db_set_long_threshold",
     "sw_scan", "sw_scan_device", "sw_scan_batch", "sw_scan_batch_device", "sw_get_timing",
-    "sw_timing_reset", "sw_timing_total", "sw_last_kernel", "sw_last_intra_kernel",
+    "sw_timing_reset", "sw_timing_total", "sw_stream_wait_scan", "sw_last_kernel", "sw_last_intra_kernel",
     "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_topk_device_ids", "sw_scan_topk", "sw_score_pair",
     "sw_align",
     "sw_db_save", "sw_db_load", "sw_db_subjects", "sw_db_create_synthetic", "sw_synth_tables",
@@ -115,6 +115,7 @@ def lib():
         "sw_get_timing": (ctypes.c_int, [vp, ctypes.POINTER(Timing)]),
         "sw_timing_reset": (ctypes.c_int, [vp]),
         "sw_timing_total": (ctypes.c_int, [vp, ctypes.POINTER(Timing), i32p]),
+        "sw_stream_wait_scan": (ctypes.c_int, [vp, vp]),
         "sw_last_kernel": (ctypes.c_char_p, [vp]),
         "sw_last_intra_kernel": (ctypes.c_char_p, [vp]),
         "sw_db_save": (ctypes.c_int, [vp, ctypes.c_char_p]),
@@ -249,6 +250,11 @@ class Handle:
 
     def timing_reset(self):
         _check(lib().sw_timing_reset(self._h))
+
+    def stream_wait_scan(self, hip_stream):
+        """Make hip_stream wait for this handle's most recent scan (its end
+        event; no event record of the caller's on the scan's stream)."""
+        _check(lib().sw_stream_wait_scan(self._h, hip_stream))
 
     def last_kernel(self):
         """Per-wave inter kernel of the last scan, e.g. 'sw_inter_x2<16,16,affine>'."""

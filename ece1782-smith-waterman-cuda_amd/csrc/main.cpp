@@ -207,8 +207,15 @@ int main(int argc, char* argv[]) {
             std::vector<int32_t> scores(static_cast<size_t>(st.max_id + 1), 0);
             if (st.n_subjects && sw_scan(h, sdb, qc.data(), static_cast<int32_t>(qc.size()), &sc, scores.data()))
                 return die("sw_scan");
-            for (int64_t k = 0; k < st.n_subjects; ++k)
-                result.push_back(std::make_pair(static_cast<int>(ids[k]), scores[ids[k]]));
+            // the reference's report order: padded length descending, file
+            // (= record id) order within a length (SWSolver.cu:309,384-390)
+            std::vector<int64_t> order(static_cast<size_t>(st.n_subjects));
+            for (int64_t k = 0; k < st.n_subjects; ++k) order[k] = k;
+            std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+                const int pa = roundUp(static_cast<int>(lens[a]), TILE_SIZE), pb = roundUp(static_cast<int>(lens[b]), TILE_SIZE);
+                return pa != pb ? pa > pb : ids[a] < ids[b];
+            });
+            for (int64_t k : order) result.push_back(std::make_pair(static_cast<int>(ids[k]), scores[ids[k]]));
             if (topk) {  // beyond the device top-K's 4096: ranked here
                 const size_t kk = std::min<size_t>(result.size(), static_cast<size_t>(topk));
                 std::partial_sort(result.begin(), result.begin() + kk, result.end(),

@@ -262,7 +262,11 @@ struct sw_handle {
     struct ProfSlot {
         int8_t* d = nullptr;
         size_t dcap = 0;
-        hipEvent_t built = nullptr;      // this slot's last scan started (its profiles are built)
+        // the end event (ev[3]) of the slot's last scan: reusing the slot
+        // waits for it.  Not an event of its own: each event record is a
+        // packet the command processor spends ~5 us on between two kernels
+        // (rocprofv3 trace of C2's 1/8 share, scripts/step_gaps.py)
+        hipEvent_t last_end = nullptr;
         bool pending = false;
         hipEvent_t tail_read = nullptr;  // a deferred rescue tail has read the slot
         bool tail_pending = false;
@@ -370,6 +374,15 @@ struct sw_db {
     };
     std::vector<LptTable> lpt_tables;
     bool last_pair_merged = false;
+    bool last_drain = false;             // the last scan's merged launch drained its own rescue lists
+    // device copies of the merged launch's drain arguments (swk::DrainArgs),
+    // one per distinct content (profile slot x list parity x score buffer
+    // x query shape): uploaded once, then reused with no copy per scan
+    static constexpr int kDrainSlots = 32;
+    swk::DrainArgs* d_drain = nullptr;
+    swk::DrainArgs* h_drain = nullptr;   // pinned: the copies' sources
+    std::vector<std::vector<uint64_t>> drain_keys;  // what each slot's content is a function of
+    int drain_next = 0;
     // intra part (long subjects)
     int64_t nlong = 0;
     int32_t long_max = 0;
@@ -449,6 +462,12 @@ void free_dev(sw_db* db) {
     db->rbnd_tried = false;
     for (auto& t : db->lpt_tables) (void)hipFree(t.d_order);
     db->lpt_tables.clear();
+    if (db->d_drain) (void)hipFree(db->d_drain);
+    if (db->h_drain) (void)hipHostFree(db->h_drain);
+    db->d_drain = nullptr;
+    db->h_drain = nullptr;
+    db->drain_keys.clear();
+    db->drain_next = 0;
     if (db->h_trace) (void)hipHostFree(db->h_trace);  // sized for this block layout
     db->h_trace = nullptr;
     db->trace_entries = 0;
@@ -837,7 +856,7 @@ struct Profiles {
 // rows; the first also zeroes the rescue lists' counters `reset`) in one of
 // the handle's profile slots, on the scan's stream.
 int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* mat, int go, bool affine,
-                   int32_t qpad_inter, bool want16, int ri, int32_t qpad_intra, int32_t* const (&reset)[5],
+                   int32_t qpad_inter, bool want16, int ri, int32_t qpad_intra, int32_t* const (&reset)[9],
                    Profiles* P) {
     for (int32_t i = 0; i < qlen; ++i)
         if (q[i] >= SW_ALPHABET) return fail(SW_E_INVALID, "query residue code out of range (use sw_encode)");
@@ -859,7 +878,7 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     P->slot = h->prof_next;
     sw_handle::ProfSlot& S = h->prof[h->prof_next];
     h->prof_next = (h->prof_next + 1) % sw_handle::kProfSlots;
-    if (S.pending) HIPCHECK(hipEventSynchronize(S.built));
+    if (S.pending) HIPCHECK(hipEventSynchronize(S.last_end));
     S.pending = false;
     if (P->total > S.dcap) {
         if (S.d) {
@@ -888,7 +907,7 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     a.ri = ri;
     a.rip = rip;
     a.qpad_intra = ri ? qpad_intra : 0;
-    for (int k = 0; k < 5; ++k) a.reset[k] = reset[k];
+    for (int k = 0; k < 9; ++k) a.reset[k] = reset[k];
     std::memcpy(a.mat, mat, 625);
     const int32_t rows = std::max(P->stride, a.qpad_intra);
     for (int32_t r0 = 0; r0 < rows; r0 += swk::kProfQueryChunk) {
@@ -899,7 +918,7 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
         HIPCHECK(swk::launch_build_profile(a, h->stream));
         for (auto& p : a.reset) p = nullptr;  // once
     }
-    HIPCHECK(hipEventRecord(S.built, h->stream));
+    S.last_end = h->ev[3];  // recorded at the end of this scan (scan_impl)
     S.pending = true;
     return SW_OK;
 }
@@ -1052,6 +1071,37 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     return SW_OK;
 }
 
+// The device copy of a merged launch's drain arguments (swk::DrainArgs: read
+// from the kernel arguments, the drain's values stayed in registers across
+// the scan loops and spilled).  `key` lists everything the content is a
+// function of (profile slot, list parity, score buffer, query length,
+// scoring, split); a miss uploads the content in stream order, a hit (every
+// scan of a steady loop after the first few) costs no copy.
+int drain_blob(sw_db* db, hipStream_t s, const std::vector<uint64_t>& key, const swk::DrainArgs& d,
+               const swk::DrainArgs** out) {
+    if (!db->d_drain) {
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_drain), sw_db::kDrainSlots * sizeof(swk::DrainArgs)));
+        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&db->h_drain), sw_db::kDrainSlots * sizeof(swk::DrainArgs),
+                               hipHostMallocDefault));
+        db->device_bytes += sw_db::kDrainSlots * sizeof(swk::DrainArgs);
+    }
+    for (size_t k = 0; k < db->drain_keys.size(); ++k)
+        if (db->drain_keys[k] == key) {
+            *out = db->d_drain + k;
+            return SW_OK;
+        }
+    // a slot is rewritten only after the 31 uploads since its last one, each
+    // in stream order behind the scans that read it
+    const int k = db->drain_next;
+    db->drain_next = (k + 1) % sw_db::kDrainSlots;
+    if (static_cast<int>(db->drain_keys.size()) <= k) db->drain_keys.resize(k + 1);
+    db->drain_keys[k] = key;
+    db->h_drain[k] = d;
+    HIPCHECK(hipMemcpyAsync(db->d_drain + k, &db->h_drain[k], sizeof d, hipMemcpyHostToDevice, s));
+    *out = db->d_drain + k;
+    return SW_OK;
+}
+
 // The handle's stream waits for every deferred rescue tail still pending, so
 // what completes on it (a non-deferred scan, the end of a batch) includes
 // the rescued scores of the scans before it.
@@ -1120,8 +1170,9 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                                                                                : 0;
     const int R = swk::inter_rows(affine, x2_ok);
     const int32_t qpad_inter = static_cast<int32_t>(round_up(qlen, R));
-    const int ri = db->nlong ? swk::intra_rows_for(qlen, db->long_max) : 0;
-    const int32_t qpad_intra = ri ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri)) : 0;
+    // (the merged launch's drain takes the int32 rows per lane from ri2, below)
+    int ri = db->nlong ? swk::intra_rows_for(qlen, db->long_max) : 0;
+    int32_t qpad_intra = ri ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri)) : 0;
     // Long subjects: two per wave in packed fp16 (sw_intra_x2) when the guard
     // applies, with the int32 sw_intra re-scoring the subjects it flags
     // (SW_INTRA_X2=0: int32 only).
@@ -1244,50 +1295,6 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     db->last_ncoop = ncoop;
     db->last_npair = npair;
     db->last_pair_merged = npair != 0;
-    const int32_t qpad_coop = ncoop ? static_cast<int32_t>(round_up(qlen, swk::inter_coop_rows())) : 0;
-    const int64_t rstride = 2 * (db->nblocks + 1) + 2;  // lists A and B, the largest flagged block
-    const int64_t lstride = 2 * (db->nlong + 1);        // intra lists 1 and 2
-    if (rescue && db->nblocks && !db->d_rescue) {
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rescue), 2 * rstride * sizeof(int32_t)));
-        db->device_bytes += 2 * rstride * sizeof(int32_t);
-    }
-    const bool multi_inter = qpad_inter > R || qpad_rescue > swk::rescue_rows(affine) ||
-                             qpad_coop > swk::inter_coop_rows() || qpad_list > (affine ? 64 : 96);
-    const bool multi_intra = (ri && qpad_intra > swk::kLanes * ri) || (ri2 && qpad_intra2 > swk::kLanes * ri2);
-    if ((multi_inter || multi_intra) && (rc = ensure_bnd(db, affine, intra_x2))) return rc;
-    if (intra_x2 && !db->d_lrescue) {  // two lists: [count, subjects...] x 2
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lrescue), 2 * lstride * sizeof(int32_t)));
-        db->device_bytes += 2 * lstride * sizeof(int32_t);
-    }
-    // this scan's list set; a deferred tail of the scan before last used it
-    const int par = h->parity;
-    h->parity ^= 1;
-    if (h->tail_pending[par]) {
-        HIPCHECK(hipStreamWaitEvent(h->stream, h->tail_done[par], 0));
-        h->tail_pending[par] = false;
-    }
-    int32_t* const listA = db->d_rescue ? db->d_rescue + par * rstride : nullptr;  // [count, ids...]
-    int32_t* const listB = listA ? listA + db->nblocks + 1 : nullptr;
-    int32_t* const maxA = listA ? listA + 2 * (db->nblocks + 1) : nullptr;
-    int32_t* const list1 = db->d_lrescue ? db->d_lrescue + par * lstride : nullptr;  // flagged by the fp16 pass
-    int32_t* const list2 = list1 ? list1 + db->nlong + 1 : nullptr;                  // ... and again by int16
-    // the rescue tail on its own stream and boundary rows (see sw_handle::tail)
-    const bool deferred = defer && (!(multi_inter || multi_intra) || ensure_rbnd(db, affine, intra_x2));
-    hipStream_t const ts = deferred ? h->tail : h->stream;
-
-    // the profiles, and the rescue lists' counters (inter A, B, largest
-    // flagged block; intra 1, 2) zeroed by the same launch, before the fork
-    // so the side streams see them
-    {
-        int32_t* const cA = (rescue && db->nblocks) ? listA : nullptr;
-        int32_t* const c1 = (db->nlong && intra_x2) ? list1 : nullptr;
-        int32_t* const reset[5] = {cA, (cA && f16) ? listB : nullptr, (cA && f16) ? maxA : nullptr, c1,
-                                   c1 ? list2 : nullptr};
-        if ((rc = build_profiles(h, query, qlen, mat, go, affine,
-                                 std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2}),
-                                 x2 || intra_x2, ri, qpad_intra, reset, &P)))
-            return rc;
-    }
     // One merged launch for the fp16 scan, longest work first (sw_scan_lpt):
     // the inter groups + single waves and the long subjects' fp16 pass, when
     // the scan takes exactly that shape, on databases far from filling the
@@ -1302,15 +1309,78 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                      f16 && rescue && npair && !ncoop && i16_span == 0 &&
                      swk::lpt_supported(ri2);
     db->last_lpt = lpt;
+    // ... and that launch re-scores what it flags itself (sw_scan_lpt's drain,
+    // swk::DrainArgs): no rescue launches after it, on boundary rows of its
+    // own (the deferred tails', when device memory allows them), with the
+    // int32 long-subject stage at the fp16 form's rows per lane
+    const bool drain = lpt && ensure_rbnd(db, affine, intra_x2);
+    db->last_drain = drain;
+    if (drain) {
+        ri = ri2;
+        qpad_intra = static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri));
+    }
+    const int32_t qpad_coop = ncoop ? static_cast<int32_t>(round_up(qlen, swk::inter_coop_rows())) : 0;
+    // lists A and B, the largest flagged block, a spare word, the dequeue
+    // heads of A and B (the merged launch's drain); every entry starts at -1
+    // (sw_kernels.h: whoever takes an entry resets it)
+    const int64_t rstride = 2 * (db->nblocks + 1) + 4;
+    const int64_t lstride = 2 * (db->nlong + 1) + 2;  // intra lists 1 and 2, their heads
+    if (rescue && db->nblocks && !db->d_rescue) {
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rescue), 2 * rstride * sizeof(int32_t)));
+        HIPCHECK(hipMemsetAsync(db->d_rescue, 0xff, 2 * rstride * sizeof(int32_t), h->stream));
+        db->device_bytes += 2 * rstride * sizeof(int32_t);
+    }
+    const bool multi_inter = qpad_inter > R || qpad_rescue > swk::rescue_rows(affine) ||
+                             qpad_coop > swk::inter_coop_rows() || qpad_list > (affine ? 64 : 96);
+    const bool multi_intra = (ri && qpad_intra > swk::kLanes * ri) || (ri2 && qpad_intra2 > swk::kLanes * ri2);
+    if ((multi_inter || multi_intra) && (rc = ensure_bnd(db, affine, intra_x2))) return rc;
+    if (intra_x2 && !db->d_lrescue) {  // two lists: [count, subjects...] x 2
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lrescue), 2 * lstride * sizeof(int32_t)));
+        HIPCHECK(hipMemsetAsync(db->d_lrescue, 0xff, 2 * lstride * sizeof(int32_t), h->stream));
+        db->device_bytes += 2 * lstride * sizeof(int32_t);
+    }
+    // this scan's list set; a deferred tail of the scan before last used it
+    const int par = h->parity;
+    h->parity ^= 1;
+    if (h->tail_pending[par]) {
+        HIPCHECK(hipStreamWaitEvent(h->stream, h->tail_done[par], 0));
+        h->tail_pending[par] = false;
+    }
+    int32_t* const listA = db->d_rescue ? db->d_rescue + par * rstride : nullptr;  // [count, ids...]
+    int32_t* const listB = listA ? listA + db->nblocks + 1 : nullptr;
+    int32_t* const maxA = listA ? listA + 2 * (db->nblocks + 1) : nullptr;
+    int32_t* const list1 = db->d_lrescue ? db->d_lrescue + par * lstride : nullptr;  // flagged by the fp16 pass
+    int32_t* const list2 = list1 ? list1 + db->nlong + 1 : nullptr;                  // ... and again by int16
+    int32_t* const headA = listA ? maxA + 2 : nullptr;  // the drain's dequeue heads: A, B, 1, 2
+    int32_t* const head1 = list1 ? list2 + db->nlong + 1 : nullptr;
+    // the rescue tail on its own stream and boundary rows (see sw_handle::tail)
+    const bool deferred = !drain && defer && (!(multi_inter || multi_intra) || ensure_rbnd(db, affine, intra_x2));
+    hipStream_t const ts = deferred ? h->tail : h->stream;
+
+    // the profiles, and the rescue lists' counters (inter A, B, largest
+    // flagged block; intra 1, 2) zeroed by the same launch, before the fork
+    // so the side streams see them
+    {
+        int32_t* const cA = (rescue && db->nblocks) ? listA : nullptr;
+        int32_t* const c1 = (db->nlong && intra_x2) ? list1 : nullptr;
+        int32_t* const reset[9] = {cA, (cA && f16) ? listB : nullptr, (cA && f16) ? maxA : nullptr, c1,
+                                   c1 ? list2 : nullptr, drain ? headA : nullptr, drain ? headA + 1 : nullptr,
+                                   drain ? head1 : nullptr, drain ? head1 + 1 : nullptr};
+        if ((rc = build_profiles(h, query, qlen, mat, go, affine,
+                                 std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2}),
+                                 x2 || intra_x2, ri, qpad_intra, reset, &P)))
+            return rc;
+    }
     h->evpool[h->nscans - 1].merged = lpt;
-    // fork: the side stream starts when the main stream reaches ev[0]
-    MARK(0, h->stream);
+    // fork: the side streams start when the main stream reaches ev[0] (the
+    // merged launch has none: its scan time runs from ev[6])
+    if (!lpt) MARK(0, h->stream);
     h->last_intra = "none";
     // the long subjects' stream: a side stream, concurrent with the inter
     // kernels; with the merged launch, the main stream after it (only the
     // rescue stages are left to run)
     hipStream_t is = lpt ? h->stream : h->side;
-    swk::IntraArgs lpt_intra{};
+    swk::IntraArgs lpt_intra{}, lpt_i32{};  // the merged launch's fp16 pass and its drain's int32 stage
     // the long subjects' kernels: all of them, or (lpt_done) those after the
     // fp16 pass the merged launch ran
     // The long subjects' rescue stages (the int16 form over the fp16 pass's
@@ -1424,6 +1494,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             x.rescue_list = list1 + 1;
             if (lpt && !lpt_done) {  // the merged launch runs this pass
                 lpt_intra = x;
+                lpt_i32 = ia;
                 return SW_OK;
             }
             if (!lpt_done) {
@@ -1446,6 +1517,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                 db->lcount_qlen = qlen;
                 db->lcount_qhash = qhash;
             }
+            if (drain) return SW_OK;  // the merged launch re-scored its flagged subjects itself
         }
         tail_x = x;
         tail_ia = ia;
@@ -1552,8 +1624,54 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             const int32_t nquad = lpt_quad_blocks(db, npair);
             a.blk_quad = nquad;
             if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, &order, &nwg))) return rc;
-            HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, order, nwg, affine, ri2, h->stream));
-            MARK(7, h->stream);
+            const swk::DrainArgs* dargs = nullptr;
+            if (drain) {
+                // the four rescue stages of launch_inter_tail / launch_intra_tail,
+                // on the tails' boundary rows (sw_kernels.h DrainArgs)
+                swk::DrainArgs d{};
+                d.a16 = a;
+                d.a16.bnd_h = db->d_rbnd_h;
+                d.a16.bnd_f = db->d_rbnd_f;
+                d.a16.qpad = qpad_list;
+                d.a16.rescue_list = listB + 1;
+                d.a16.rescue_count = listB;
+                d.a16.rescue_max = nullptr;
+                d.a16.trace = nullptr;
+                d.a32 = a;
+                d.a32.bnd_h = db->d_rbnd_h;
+                d.a32.bnd_f = db->d_rbnd_f;
+                d.a32.prof = P.dev + P.off8;
+                d.a32.qpad = qpad_rescue;
+                d.a32.rescue_list = nullptr;
+                d.a32.rescue_count = nullptr;
+                d.a32.rescue_max = nullptr;
+                d.a32.trace = nullptr;
+                d.i16 = lpt_intra;
+                d.i16.bnd_h = db->d_rlbnd_h;
+                d.i16.bnd_f = db->d_rlbnd_f;
+                d.i16.rescue_list = list2 + 1;
+                d.i16.rescue_count = list2;
+                d.i32 = lpt_i32;
+                d.i32.bnd_h = db->d_rlbnd_h;
+                d.i32.bnd_f = db->d_rlbnd_f;
+                d.lists[0] = listA;
+                d.lists[1] = listB;
+                d.lists[2] = list1;
+                d.lists[3] = list2;
+                d.heads[0] = headA;
+                d.heads[1] = headA + 1;
+                d.heads[2] = head1;
+                d.heads[3] = head1 + 1;
+                const std::vector<uint64_t> key = {
+                    reinterpret_cast<uint64_t>(P.dev), P.off8, P.off16, P.intra_off, static_cast<uint64_t>(par),
+                    reinterpret_cast<uint64_t>(scores_dev), static_cast<uint64_t>(qlen), skey,
+                    static_cast<uint64_t>(npair), static_cast<uint64_t>(nquad), static_cast<uint64_t>(P.stride),
+                    reinterpret_cast<uint64_t>(a.trace)};
+                if ((rc = drain_blob(db, h->stream, key, d, &dargs))) return rc;
+            }
+            HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, order, nwg, affine, ri2, h->stream, dargs));
+            // (a draining launch ends the scan: its end event is ev[3])
+            if (!drain) MARK(7, h->stream);
             if ((rc = launch_long(true))) return rc;
         } else if (npair) {
             // one launch: pairs for blocks [nr, npair), one wave per block after
@@ -1566,7 +1684,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         h->last_kernel = swk::inter_kernel_name(affine, x2_ok);
         if (npair) h->last_kernel.replace(0, std::strlen("sw_inter_x2s"), "sw_inter_x2p");  // + wave pairs
         if (nr) h->last_kernel += "+int16[0," + std::to_string(nr) + ")";
-        if (lpt) h->last_kernel += "+lpt";
+        if (lpt) h->last_kernel += drain ? "+lpt+drain" : "+lpt";
         if (!lpt) MARK(7, h->stream);
         ++h->launches;
         if (ncoop || nr) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
@@ -1591,7 +1709,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             db->icount_qhash = qhash;
         }
         tail_a = a;
-        inter_tail = rescue;
+        inter_tail = rescue && !drain;
         if (deferred && inter_tail) HIPCHECK(hipEventRecord(h->main_done, h->stream));
         else if (inter_tail && (rc = launch_inter_tail(h->stream, db->d_bnd_h, db->d_bnd_f))) return rc;
     }
@@ -1763,7 +1881,6 @@ int sw_create(int32_t device, sw_handle** out) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     for (auto& S : h->prof) {
         if (e == hipSuccess) e = hipEventCreateWithFlags(&S.tail_read, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&S.built, hipEventDisableTiming);
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->coop_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->fork2, hipEventDisableTiming);
@@ -1787,7 +1904,6 @@ int sw_destroy(sw_handle* h) {
     for (auto& S : h->prof) {
         if (S.d) (void)hipFree(S.d);
         if (S.tail_read) (void)hipEventDestroy(S.tail_read);
-        if (S.built) (void)hipEventDestroy(S.built);
     }
     if (h->d_scores) (void)hipFree(h->d_scores);
     if (h->d_topk_work) (void)hipFree(h->d_topk_work);
@@ -2162,16 +2278,19 @@ int read_events(const ScanEvents& se, sw_timing* t) {
     // intra runs on the side stream from the fork (ev0) to ev1; inter on the
     // main stream from ev0 to ev2; they overlap.
     // (events a scan did not record: the intra and inter spans fall back to
-    // the whole scan, the cooperative kernel's to 0)
+    // the whole scan, the cooperative kernel's to 0; a scan without a fork,
+    // the merged launch, starts at ev6)
     auto has = [&](int k) { return (se.rec >> k & 1u) != 0; };
+    const hipEvent_t start = has(0) ? se.ev[0] : se.ev[6];
     float t01 = 0, t02 = 0, t03 = 0;
-    HIPCHECK(hipEventElapsedTime(&t03, se.ev[0], se.ev[3]));
+    HIPCHECK(hipEventElapsedTime(&t03, start, se.ev[3]));
     t01 = t02 = t03;
-    if (has(1)) HIPCHECK(hipEventElapsedTime(&t01, se.ev[0], se.ev[1]));
-    if (has(2)) HIPCHECK(hipEventElapsedTime(&t02, se.ev[0], se.ev[2]));
+    if (has(1)) HIPCHECK(hipEventElapsedTime(&t01, start, se.ev[1]));
+    if (has(2)) HIPCHECK(hipEventElapsedTime(&t02, start, se.ev[2]));
     float t45 = 0, t67 = 0;
     if (has(4) && has(5)) HIPCHECK(hipEventElapsedTime(&t45, se.ev[4], se.ev[5]));
-    if (has(6) && has(7)) HIPCHECK(hipEventElapsedTime(&t67, se.ev[6], se.ev[7]));
+    // (a merged launch that drains its own rescue lists ends the scan: ev[3])
+    if (has(6)) HIPCHECK(hipEventElapsedTime(&t67, se.ev[6], has(7) ? se.ev[7] : se.ev[3]));
     if (se.merged) {  // the merged launch: no separate intra span
         t01 = 0;
         t02 = t67;
@@ -2191,6 +2310,14 @@ int sw_get_timing(sw_handle* h, sw_timing* out) {
     std::memset(out, 0, sizeof(*out));
     if (!h->timed || h->nscans == 0) return SW_OK;
     return read_events(h->evpool[h->nscans - 1], out);
+}
+
+int sw_stream_wait_scan(sw_handle* h, void* hip_stream) {
+    if (!h) return fail(SW_E_INVALID, "null handle");
+    if (!h->timed || h->nscans == 0) return SW_OK;  // no scan yet: nothing to wait for
+    HIPCHECK(hipSetDevice(h->device));
+    HIPCHECK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(hip_stream), h->evpool[h->nscans - 1].ev[3], 0));
+    return SW_OK;
 }
 
 const char* sw_last_kernel(sw_handle* h) { return h ? h->last_kernel.c_str() : "none"; }

@@ -31,6 +31,9 @@
 // recurrences equal the int32 ones (sw_kernels.hip) bit for bit.  sw_inter_x2s
 // also runs beyond that bound in guarded mode: lanes that reach kSat16 flag
 // their block for the int32 kernel (see the end of the kernel).
+#include <algorithm>
+
+#include "sw_int32.h"
 #include "sw_intra_x2.h"
 #include "sw_kernels.h"
 
@@ -250,7 +253,7 @@ __device__ __forceinline__ h2 max3h(h2 a, h2 b, h2 c) {
 }
 
 template <int R, int SG, bool AFFINE, bool F16, int CR = 16>
-__device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>& L, int lane);
+__device__ __forceinline__ bool x2s_block(const InterArgs& a, int blk, X2Lds<R>& L, int lane);
 
 // LIST: a rescue stage walking the device-side block list (a separate
 // instantiation, so the list loop costs the scan kernels no registers).
@@ -264,7 +267,7 @@ __global__ __launch_bounds__(256, 2) void sw_inter_x2s(InterArgs a) {
     if constexpr (LIST) {
         const int n = __builtin_amdgcn_readfirstlane(*a.blk_count);
         for (int i = blockIdx.x * kWavesPerWG + wave; i < n; i += gridDim.x * kWavesPerWG)
-            x2s_block<R, SG, AFFINE, F16, CR>(a, __builtin_amdgcn_readfirstlane(a.blk_list[i]), L, lane);
+            x2s_block<R, SG, AFFINE, F16, CR>(a, list_take(a.blk_list, i), L, lane);
         return;
     }
     const int blk = a.blk_first + blockIdx.x * kWavesPerWG + wave;
@@ -346,8 +349,9 @@ __device__ __forceinline__ void trace_block(const InterArgs& a, int blk, uint64_
 // band first — int16: [kSat16, 32767] (or wrapped: negative); fp16:
 // >= a.sat_limit = 2048 - 2 max S, computed exactly — and its block is
 // re-scored from the list by the next stage (int16 packed, then int32).
+// Returns (wave-uniform) whether the block was appended to the rescue list.
 template <bool F16>
-__device__ __forceinline__ void x2s_finish(const InterArgs& a, int blk, int lane, typename PkCell<F16>::V best) {
+__device__ __forceinline__ bool x2s_finish(const InterArgs& a, int blk, int lane, typename PkCell<F16>::V best) {
     int b;
     if constexpr (F16)  // offset removed in integers: true scores go up to ~4096
         b = static_cast<int>(static_cast<float>(__builtin_elementwise_maximum(best.x, best.y))) -
@@ -360,10 +364,12 @@ __device__ __forceinline__ void x2s_finish(const InterArgs& a, int blk, int lane
         const bool sat = F16 ? (b >= a.sat_limit) : (b >= kSat16 || b < 0);
         const uint64_t m = __builtin_amdgcn_ballot_w64(sat);
         if (m && lane == 0) {
-            a.rescue_list[atomicAdd(a.rescue_count, 1)] = blk;
+            list_publish(a.rescue_list, a.rescue_count, blk);
             if (a.rescue_max) atomicMax(a.rescue_max, blk);
         }
+        return m != 0;
     }
+    return false;
 }
 
 
@@ -768,7 +774,7 @@ __device__ __forceinline__ uint32_t block_cols(const InterArgs& a, int blk) {
 }
 
 template <int R, int SG, bool AFFINE, bool F16, int CR>
-__device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>& L, int lane) {
+__device__ __forceinline__ bool x2s_block(const InterArgs& a, int blk, X2Lds<R>& L, int lane) {
     const uint32_t ncols = block_cols(a, blk);
     const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
     Best<F16> best;
@@ -780,8 +786,9 @@ __device__ __forceinline__ void x2s_block(const InterArgs& a, int blk, X2Lds<R>&
         for (int s0 = 0; s0 < a.qpad && ncols > 0; s0 += 2 * R)
             x2s_pass<R, SG, AFFINE, F16, false, CR>(a, L, ncols, base, lane, s0, best, nullptr, nullptr, nullptr);
     }
-    x2s_finish<F16>(a, blk, lane, best.value(a));
+    const bool flagged = x2s_finish<F16>(a, blk, lane, best.value(a));
     trace_block(a, blk, t0, lane, 0);
+    return flagged;
 }
 
 // ---------------------------------------------------------------------------
@@ -857,8 +864,9 @@ struct X2pSmem {
 // only), the next ones blocks [quad_end, npair) by pairs (two per
 // workgroup), and with MERGED the rest blocks [npair, nblocks) one per wave
 // (x2s_block): the dispatcher hands out work widest-first across the forms.
+// Returns (per wave) whether this wave appended a block to the rescue list.
 template <int R, int SG, bool AFFINE, bool F16, bool MERGED, int GMAX>
-__device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, int quad_end, X2pSmem<R, SG, GMAX>& sm) {
+__device__ __forceinline__ bool x2p_wg(const InterArgs& a, int wgi, int quad_end, X2pSmem<R, SG, GMAX>& sm) {
     static_assert(R % 16 == 0 && SG % 4 == 0, "shape");
     static_assert(GMAX == 2 || GMAX == 4, "groups of 2 or 4 waves");
     X2Lds<R>* lds = sm.lds;
@@ -874,8 +882,8 @@ __device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, int quad_end
     const int pwg = qwg + (npair - qend + 1) / 2;          // ... and pair workgroups
     if (MERGED && wgi >= pwg) {
         const int blk = npair + (wgi - pwg) * kWavesPerWG + wave;
-        if (blk < a.nblocks) x2s_block<R, SG, AFFINE, F16, kSingleCR>(a, blk, lds[wave], lane);
-        return;  // workgroup-uniform branch: no barrier below is skipped by part of it
+        // workgroup-uniform branch: no barrier below is skipped by part of it
+        return blk < a.nblocks && x2s_block<R, SG, AFFINE, F16, kSingleCR>(a, blk, lds[wave], lane);
     }
     const bool quad = wgi < qwg;                           // workgroup-uniform
     const int G = quad ? 4 : 2, NG = kWavesPerWG / G;
@@ -914,6 +922,7 @@ __device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, int quad_end
     }
     if (blk < npair && w > 0) part[wave][lane] = P::bits(best.value(a));
     __syncthreads();
+    bool flagged = false;
     if (blk < npair && w == 0) {
         V b = best.value(a);
         for (int u = 1; u < G; ++u) {
@@ -921,9 +930,10 @@ __device__ __forceinline__ void x2p_wg(const InterArgs& a, int wgi, int quad_end
             if constexpr (F16) b = __builtin_elementwise_maximum(b, o);
             else b = max2(b, o);
         }
-        x2s_finish<F16>(a, blk, lane, b);
+        flagged = x2s_finish<F16>(a, blk, lane, b);
         trace_block(a, blk, t0, lane, quad ? 4 : 1);
     }
+    return flagged;
 }
 
 // G = 2: every group block by pairs; G = 4: every group block by quads.
@@ -949,39 +959,126 @@ __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_inter_x2p(InterArgs 
 // so the dispatcher starts the longest work first and fills the end with
 // the shortest (LPT).  LDS: the two kinds' buffers overlap (a workgroup is
 // one kind), so the occupancy stays the inter kernel's 2 workgroups per CU.
+// The drain's shapes: the int16 list form of the two-strips kernel (affine
+// 32x8 with 64-row passes, linear 48x4 with 96-row passes) and the int32
+// inter kernel (affine 32x8, linear 64x8), as the separate rescue launches.
+template <bool AFFINE>
+struct DrainShape {
+    static constexpr int R16 = AFFINE ? 32 : 48, SG16 = AFFINE ? 8 : 4;
+    static constexpr int R32 = AFFINE ? 32 : 64;
+};
+template <bool AFFINE, int RI>
+constexpr size_t drain_smem() {
+    using D = DrainShape<AFFINE>;
+    const size_t x16 = kWavesPerWG * sizeof(X2Lds<D::R16>);
+    const size_t i32 = static_cast<size_t>(kProfileRows) * intra_stride(RI);
+    const size_t a32 = static_cast<size_t>(kWavesPerWG) * kProfileRows * inter_stride(D::R32);
+    const size_t i16 = sizeof(typename ix2::IntraImg<RI, false>::Elem) * ix2::img_elems<RI, false>();
+    return std::max(std::max(x16, i32), std::max(a32, i16));
+}
+
+// The merged launch's own rescue stages (DrainArgs, sw_kernels.h): after its
+// scan work, a workgroup takes entries of the rescue lists until none are
+// left — the int16 pairs of list 1 (a whole workgroup: four waves, one LDS
+// image), up to four blocks of list A (one int16 block per wave), one subject
+// of list 2 (wave 0, int32) or up to four blocks of list B (int32).  A
+// workgroup that finds nothing exits; an entry appended later is taken by the
+// workgroup that appended it (it drains after appending), so nothing waits
+// for other workgroups.  task: 2 + 8 ints of LDS (kind, count, entries).
+template <bool AFFINE, int RI>
+__device__ __forceinline__ void lpt_drain(const DrainArgs* __restrict__ d, char* smem, int* task) {
+    using D = DrainShape<AFFINE>;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    for (;;) {
+        __syncthreads();  // the LDS of the previous work is free, task may be rewritten
+        if (threadIdx.x == 0) {
+            // list 1 first (whole-workgroup work, the longest), then A, 2, B
+            constexpr int kOrder[4] = {2, 0, 3, 1};
+            constexpr int kWant[4] = {2 * kWavesPerWG, kWavesPerWG, 1, kWavesPerWG};
+            int kind = 0, n = 0, start = 0;
+            for (int k = 0; k < 4 && !n; ++k) {
+                const int l = kOrder[k];
+                if ((n = list_claim(d->lists[l], d->heads[l], kWant[k], &start))) kind = l + 1;
+            }
+            int m = 0;
+            for (int i = 0; i < n; ++i) {
+                const int v = list_wait_take(d->lists[kind - 1] + 1, start + i);
+                if (v >= 0) task[2 + m++] = v;
+            }
+            task[0] = m ? kind : (n ? -1 : 0);  // -1: claimed entries never appeared; look again
+            task[1] = m;
+        }
+        __syncthreads();
+        const int kind = task[0], n = task[1];
+        if (kind == 0) return;  // workgroup-uniform
+        if (kind < 0) continue;
+        // the producers' results happen-before the re-scoring's stores
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (kind == 3) {  // list 1: int16 pairs, flagging into list 2
+            IntraArgs y = d->i16;
+            y.subj_list = task + 2;
+            y.list_count = task + 1;
+            ix2::intra_x2_wg<RI, false, true, !AFFINE, false>(y, 0,
+                                                               reinterpret_cast<typename ix2::IntraImg<RI, false>::Elem*>(smem));
+        } else if (kind == 1) {  // list A: int16 blocks, flagging into list B
+            if (wave < n)
+                x2s_block<D::R16, D::SG16, AFFINE, false, 16>(d->a16, task[2 + wave],
+                                                              reinterpret_cast<X2Lds<D::R16>*>(smem)[wave], lane);
+        } else if (kind == 4) {  // list 2: int32 subject (wave 0)
+            if (wave == 0) intra_subject<RI, AFFINE, false>(d->i32, task[2], reinterpret_cast<uint8_t*>(smem));
+        } else {  // list B: int32 blocks
+            if (wave < n)
+                inter_block<D::R32, 8, AFFINE, false>(
+                    d->a32, task[2 + wave],
+                    reinterpret_cast<uint8_t*>(smem) + wave * (kProfileRows * inter_stride(D::R32)), lane);
+        }
+    }
+}
+
 template <int R, int SG, bool AFFINE, int RI>
 __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(InterArgs a, IntraArgs ia,
-                                                                     const int32_t* __restrict__ order) {
+                                                                     const int32_t* __restrict__ order,
+                                                                     const DrainArgs* __restrict__ drain) {
     using Elem = typename ix2::IntraImg<RI, true>::Elem;
     constexpr size_t kInter = sizeof(X2pSmem<R, SG, 4>);
     constexpr size_t kIntra = sizeof(Elem) * ix2::img_elems<RI, true>();
-    __shared__ __attribute__((aligned(16))) char smem[kInter > kIntra ? kInter : kIntra];
+    constexpr size_t kDrain = drain_smem<AFFINE, RI>();
+    constexpr size_t kSmem = std::max(std::max(kInter, kIntra), kDrain);
+    __shared__ __attribute__((aligned(16))) char smem[kSmem];
+    __shared__ int task[2 + 2 * kWavesPerWG];
     const int item = order[blockIdx.x];
     const uint64_t t0 = trace_now();
+    bool flagged;
     if (item >= 0)
-        x2p_wg<R, SG, AFFINE, true, true, 4>(a, item, a.blk_quad, *reinterpret_cast<X2pSmem<R, SG, 4>*>(smem));
+        flagged = x2p_wg<R, SG, AFFINE, true, true, 4>(a, item, a.blk_quad, *reinterpret_cast<X2pSmem<R, SG, 4>*>(smem));
     else
-        ix2::intra_x2_wg<RI, true, false, !AFFINE>(ia, -1 - item, reinterpret_cast<Elem*>(smem));
+        flagged = ix2::intra_x2_wg<RI, true, false, !AFFINE>(ia, -1 - item, reinterpret_cast<Elem*>(smem));
     // per-workgroup timeline (trace builds): after the per-block entries
     if (threadIdx.x == 0) trace_block(a, a.nblocks + blockIdx.x, t0, 0, item >= 0 ? 2 : 3);
+    // Only a workgroup that appended an entry drains (and takes whatever is
+    // listed, its own entries included): every entry is then taken by its
+    // producer at the latest, and the rest of the grid pays one barrier.
+    if (drain && __syncthreads_or(flagged)) lpt_drain<AFFINE, RI>(drain, smem, task);
 }
 
 template <int RI>
 static void launch_lpt_t(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine,
-                         hipStream_t s) {
+                         hipStream_t s, const DrainArgs* drain) {
     if (affine) hipLaunchKernelGGL((sw_scan_lpt<32, 8, true, RI>), dim3(n), dim3(kWavesPerWG * kLanes), 0, s, a, ia,
-                                   order);
-    else hipLaunchKernelGGL((sw_scan_lpt<32, 8, false, RI>), dim3(n), dim3(kWavesPerWG * kLanes), 0, s, a, ia, order);
+                                   order, drain);
+    else hipLaunchKernelGGL((sw_scan_lpt<32, 8, false, RI>), dim3(n), dim3(kWavesPerWG * kLanes), 0, s, a, ia, order,
+                            drain);
 }
 
 bool lpt_supported(int ri) { return ri == 4 || ri == 6 || ri == 8; }
 
 hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri,
-                           hipStream_t s) {
+                           hipStream_t s, const DrainArgs* drain) {
     if (n <= 0) return hipSuccess;
-    if (ri == 4) launch_lpt_t<4>(a, ia, order, n, affine, s);
-    else if (ri == 6) launch_lpt_t<6>(a, ia, order, n, affine, s);
-    else if (ri == 8) launch_lpt_t<8>(a, ia, order, n, affine, s);
+    if (ri == 4) launch_lpt_t<4>(a, ia, order, n, affine, s, drain);
+    else if (ri == 6) launch_lpt_t<6>(a, ia, order, n, affine, s, drain);
+    else if (ri == 8) launch_lpt_t<8>(a, ia, order, n, affine, s, drain);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }

@@ -167,8 +167,12 @@ __host__ __device__ constexpr int img_elems() { return kCodes * IntraImg<RI, F16
 // per row and per step), so h~ = max(max3(H~_left, H~_up, H~_diag + S + 2g),
 // floor): 2 packed ops per cell pair after the diagonal sum instead of the
 // Farrar form's 6 (the two-strips kernel's linear cell, sw_inter_x2.hip).
-template <int RI, bool F16, bool LIST, bool LIN = false>
-__device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typename IntraImg<RI, F16>::Elem* img) {
+// TAKE (LIST): the entries are read from the device list and reset (list_take);
+// otherwise a.subj_list holds plain subject indices (the merged launch's
+// drain passes the entries it took, in LDS).
+// Returns (per wave) whether the wave appended a subject to a.rescue_list.
+template <int RI, bool F16, bool LIST, bool LIN = false, bool TAKE = true>
+__device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typename IntraImg<RI, F16>::Elem* img) {
     static_assert(RI % 2 == 0 && RI <= 16, "rows per lane");
     constexpr int CH = kLanes * RI;  // query rows per chunk
     using C = IntraCell<F16>;
@@ -186,11 +190,16 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
     bool hasA = sa < a.nsubj, hasB = sb < a.nsubj;
     if constexpr (LIST) {
         const int n = __builtin_amdgcn_readfirstlane(*a.list_count);
-        if (wgi * 2 * kWavesPerWG >= n) return;  // workgroup-uniform
+        if (wgi * 2 * kWavesPerWG >= n) return false;  // workgroup-uniform
         hasA = sa < n;
         hasB = sb < n;
-        sa = hasA ? a.subj_list[sa] : 0;
-        sb = hasB ? a.subj_list[sb] : 0;
+        if constexpr (TAKE) {
+            sa = hasA ? list_take(a.subj_list, sa) : 0;
+            sb = hasB ? list_take(a.subj_list, sb) : 0;
+        } else {
+            sa = hasA ? a.subj_list[sa] : 0;
+            sb = hasB ? a.subj_list[sb] : 0;
+        }
     }
     const int LA = hasA ? a.subj_len[sa] : 0;
     const int LB = hasB ? a.subj_len[sb] : 0;
@@ -399,18 +408,26 @@ __device__ __forceinline__ void intra_x2_wg(const IntraArgs& a, int wgi, typenam
         const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(C::bits(best)), off));
         best = C::max2(best, C::from(o));
     }
+    bool flagged = false;
     if (lane == 0) {
         const int ba = C::lo(best) - C::zero_int(a);
         const int bb = C::hi(best) - C::zero_int(a);
         if (hasA) {
             a.scores[a.subj_id[sa]] = ba;
-            if (a.rescue_list && C::flag(a, ba)) a.rescue_list[atomicAdd(a.rescue_count, 1)] = sa;
+            if (a.rescue_list && C::flag(a, ba)) {
+                list_publish(a.rescue_list, a.rescue_count, sa);
+                flagged = true;
+            }
         }
         if (hasB) {
             a.scores[a.subj_id[sb]] = bb;
-            if (a.rescue_list && C::flag(a, bb)) a.rescue_list[atomicAdd(a.rescue_count, 1)] = sb;
+            if (a.rescue_list && C::flag(a, bb)) {
+                list_publish(a.rescue_list, a.rescue_count, sb);
+                flagged = true;
+            }
         }
     }
+    return __builtin_amdgcn_readfirstlane(flagged);
 }
 
 }  // namespace ix2

@@ -133,6 +133,63 @@ struct IntraArgs {
     const int32_t* list_count = nullptr;
 };
 
+// ---- device-side rescue lists: [count, item 0, item 1, ...] --------------
+// A 16-bit kernel appends the blocks / subjects whose values may have left
+// its exact range; the next stage re-scores them.  Entries past the count
+// hold -1: whoever takes an entry resets it, so every list is all -1 past
+// its count when a scan starts (the host fills new lists with -1 and zeroes
+// the counts per scan), and a consumer running in the SAME launch as the
+// producer (sw_scan_lpt's drain) can wait for an entry whose slot a
+// producer has claimed but not yet written.
+#if defined(__HIPCC__)
+// Producer: this wave's results (its scores, its boundary rows) are made
+// visible device-wide before the entry, so a re-scoring stage on another XCD
+// overwrites them, not the reverse.
+__device__ __forceinline__ void list_publish(int32_t* items, int32_t* count, int32_t item) {
+    __threadfence();
+    const int slot = atomicAdd(count, 1);
+    __hip_atomic_store(items + slot, item, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Consumer in a later launch (the entry is written): read entry i, reset it.
+// Wave-uniform.
+__device__ __forceinline__ int32_t list_take(const int32_t* items, int i) {
+    int32_t* p = const_cast<int32_t*>(items) + i;
+    const int32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    __hip_atomic_store(p, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+}
+// Consumer in the producer's launch: wait (bounded) until entry i is written,
+// then reset it.  -1 if it never appears (the caller skips it; a bounded
+// wait, so a wave can never hang here).
+__device__ __forceinline__ int32_t list_wait_take(int32_t* items, int i) {
+    int32_t* p = items + i;
+    int32_t v = -1;
+    for (int spin = 0; spin < (1 << 22); ++spin) {
+        v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v >= 0) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (v >= 0) __hip_atomic_store(p, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+}
+// Claim up to `want` entries [start, start + n) past the list's head; 0 when
+// none are left (or other workgroups keep winning: they drain the rest).
+__device__ __forceinline__ int list_claim(int32_t* count, int32_t* head, int want, int* start) {
+    int h = __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int tries = 0; tries < 256; ++tries) {
+        const int c = __hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (h >= c) return 0;
+        const int nh = h + want < c ? h + want : c;
+        if (__hip_atomic_compare_exchange_strong(head, &h, nh, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+            *start = h;
+            return nh - h;
+        }
+    }
+    return 0;
+}
+#endif
+
 // Strip heights (query rows held in registers per lane) the kernels are
 // instantiated for.
 // Shape of the inter kernel for this gap model.  x2_ok: 2 = the scan is
@@ -179,9 +236,28 @@ hipError_t launch_inter_x2p(const InterArgs& a, bool affine, bool f16, bool merg
 // [blk_quad, blk_first) by pairs), < 0 intra workgroup -1 - order[k] (ia as
 // for launch_intra_x2: 4 subject pairs per workgroup).  Intra rows per lane
 // 4, 6 or 8.
+// drain (nullable, DEVICE memory): the launch also re-scores what its fp16
+// cells flag — each workgroup, after its own work, takes entries of the four
+// rescue lists until none are left: int16 subject pairs of list 1 (i16: the
+// int16 intra form, flagging into list 2), int16 blocks of list A (a16: the
+// x2s list form, flagging into list B), int32 subjects of list 2 (i32:
+// sw_intra's body, rows per lane = ri) and int32 blocks of list B (a32:
+// sw_inter's body) — the four rescue launches that otherwise follow the scan
+// (and their ~5 us each of command-processor time).  The stages use their own
+// boundary rows (the deferred tails' rows).  In device memory, not in the
+// kernel arguments: read from kernel arguments, the compiler kept the drain's
+// values in registers across the scan loops and spilled.
+struct DrainArgs {
+    InterArgs a16;
+    InterArgs a32;
+    IntraArgs i16;
+    IntraArgs i32;
+    int32_t* lists[4];  // list A, B, 1, 2: [count, items...]
+    int32_t* heads[4];  // their dequeue heads (zeroed per scan)
+};
 bool lpt_supported(int ri);
 hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri,
-                           hipStream_t s);
+                           hipStream_t s, const DrainArgs* drain = nullptr);
 // true if the chosen inter kernel has a wave-pair form (two-strips 32x8).
 bool inter_has_pair(bool affine, int x2_ok);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.
@@ -247,8 +323,8 @@ uint64_t synth_hash(uint64_t seed, uint64_t id, uint64_t k);
 //   p16 : the same values as int16 (null: not built)
 //   pin : the int32 intra kernel's lane-slotted image, rows < qpad_intra:
 //         [chunk of 64 ri rows][code][lane][rip] (null: not built)
-// The first launch also zeroes the rescue lists' counters (reset[2] := -1,
-// the largest-flagged-block slot; null pointers skipped).
+// The first launch also zeroes the rescue lists' counters and dequeue heads
+// (reset[2] := -1, the largest-flagged-block slot; null pointers skipped).
 constexpr int kAlphabet = 25;
 constexpr int kProfQueryChunk = 2048;
 struct ProfileArgs {
@@ -260,7 +336,7 @@ struct ProfileArgs {
     int32_t row0, row1;
     int32_t bias;
     int32_t ri, rip, qpad_intra;
-    int32_t* reset[5];
+    int32_t* reset[9];
     int8_t mat[kAlphabet * kAlphabet + 15];
     uint8_t q[kProfQueryChunk];
 };

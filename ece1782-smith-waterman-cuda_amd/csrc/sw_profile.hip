@@ -16,12 +16,9 @@ namespace swk {
 
 // One thread per (code, row) entry of rows [row0, row1).
 __global__ __launch_bounds__(256) void sw_build_profile(ProfileArgs a) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the rescue lists' counters (first launch only)
-        if (a.reset[0]) *a.reset[0] = 0;
-        if (a.reset[1]) *a.reset[1] = 0;
-        if (a.reset[2]) *a.reset[2] = -1;
-        if (a.reset[3]) *a.reset[3] = 0;
-        if (a.reset[4]) *a.reset[4] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 9) {  // the rescue lists' counters and heads (first launch only)
+        int32_t* p = a.reset[threadIdx.x];
+        if (p) *p = threadIdx.x == 2 ? -1 : 0;
     }
     const int n = a.row1 - a.row0;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;

@@ -214,6 +214,11 @@ SW_API int sw_get_timing(sw_handle* h, sw_timing* out);
  * between them (bench.py).                                               */
 SW_API int sw_timing_reset(sw_handle* h);
 SW_API int sw_timing_total(sw_handle* h, sw_timing* out, int32_t* nscans);
+/* Make another stream (hipStream_t, e.g. a top-K exchange stream) wait for
+ * the handle's most recent scan to complete, through the scan's own end
+ * event: no extra event record on the scan's stream (each is a packet the
+ * command processor spends ~5 us on between two kernels).                 */
+SW_API int sw_stream_wait_scan(sw_handle* h, void* hip_stream);
 /* Name of the per-wave inter-sequence kernel the handle's last scan ran,
  * e.g. "sw_inter_x2<16,16,affine>" (packed int16, two subjects per lane) or
  * "sw_inter<32,8,affine>" (int32); "none" before any scan.  Valid until the

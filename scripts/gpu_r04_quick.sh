@@ -1,0 +1,30 @@
+# Round 4 iteration check: the GPU suite (or only tests matching $FIRST
+# first), then the configs in $CONFIGS (default: C2 and its 1/8 share), and
+# with TRACE=1 a rocprofv3 kernel trace of the 1/8 share (per-dispatch start /
+# end: the launches around the merged scan, scripts/step_gaps.py).
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/${RUN:-r04quick}
+mkdir -p $O
+if [ -n "$FIRST" ]; then timeout -k 10 300 python -u -m pytest tests -x -q -m gpu -k "$FIRST" --timeout 200 --timeout-method thread > $O/first_tests.log 2>&1 || { echo FIRST TESTS FAILED; tail -40 $O/first_tests.log; exit 1; }; tail -1 $O/first_tests.log; fi
+if [ -z "$NOSUITE" ]; then timeout -k 10 700 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo TESTS FAILED; tail -40 $O/gpu_tests.log; exit 1; }; tail -1 $O/gpu_tests.log; fi
+b() { tag=$1; shift; timeout -k 10 600 python3 bench.py "$@" > $O/$tag.json 2> $O/$tag.err || { echo "$tag FAILED"; tail -20 $O/$tag.err; exit 1; }; }
+for c in ${CONFIGS:-c2 s8}; do
+  case $c in
+    c2) b c2 --no-cpu-baseline ;;
+    s8) b s8 --shard-of 8 --no-cpu-baseline ;;
+    s4) b s4 --shard-of 4 --no-cpu-baseline ;;
+    s2) b s2 --shard-of 2 --no-cpu-baseline ;;
+    c3) b c3 --config c3 --no-cpu-baseline ;;
+    c5) b c5 --config c5 --no-cpu-baseline ;;
+  esac
+  python3 -c "
+import json
+d=json.loads(open('$O/$c.json').read().strip().split(chr(10))[-1]); r=d.get('reference_scoring',{})
+print('$c', d['value'], d['ms_per_step'], d.get('kernel_ms_per_scan',{}).get('scan_total'), r.get('value'), r.get('ms_per_step'), d.get('parity_sample_ok'), d.get('sustained',{}).get('value') if d.get('sustained') else None)"
+done
+if [ -n "$TRACE" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_s8 -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-verify --no-reference-scoring --shard-of 8 --steps 50 --warmup 2 > $O/kt_s8.json 2> $O/kt_s8.err || { echo TRACE FAILED; tail -5 $O/kt_s8.err; exit 1; }
+  head -12 $(find $O/kt_s8 -name "*kernel_stats.csv") | cut -c1-160
+fi
+echo RC=0

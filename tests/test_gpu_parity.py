@@ -636,10 +636,58 @@ def test_merged_lpt_launch(sw, oracle, handle, monkeypatch, quad_width, scoring)
     for qlen in (200, 375, 500):
         q = q0[:qlen]
         got = db.scan(q, m, go, ge)
-        assert handle.last_kernel().endswith("+lpt"), handle.last_kernel()
+        assert "+lpt" in handle.last_kernel(), handle.last_kernel()
         want = oracle.scan(q, r2, o2, mat=m, gap_open=go, gap_extend=ge)
         assert np.array_equal(got, want), (qlen, np.nonzero(got != want)[0][:10])
         monkeypatch.setenv("SW_LPT", "0")
         assert np.array_equal(db.scan(q, m, go, ge), got)
-        assert not handle.last_kernel().endswith("+lpt")
+        assert "+lpt" not in handle.last_kernel()
         monkeypatch.setenv("SW_LPT", "1")
+
+
+@pytest.mark.parametrize("ri", ["4", "8"])
+@pytest.mark.parametrize("scoring", [(0, 2, 2), (0, 12, 1)])
+def test_merged_launch_drains_rescue_lists(sw, oracle, handle, monkeypatch, ri, scoring):
+    """The merged launch re-scores what its fp16 cells flag inside the same
+    launch (sw_scan_lpt's drain, no rescue launches after it): planted hits
+    of every stage — inter blocks above the fp16 bound (int16 re-score) and
+    above 32767 (int16 flags again -> int32), long subjects likewise (int16
+    pairs -> int32 subjects), in quad, pair and single-wave blocks — equal
+    the oracle and the separate-launch form, twice (the lists' entries are
+    reset by whoever takes them, so the second scan starts clean)."""
+    mid, go, ge = scoring
+    monkeypatch.setenv("SW_LPT", "1")
+    monkeypatch.setenv("SW_INTRA_X2_RI", ri)
+    monkeypatch.setenv("SW_PAIR_WIDTH", "64")
+    # keep the fp16-first order on the second scan (the adaptive routing would
+    # send this many flagged blocks / subjects to int16 first)
+    monkeypatch.setenv("SW_INTER_I16_SPAN", "0")
+    monkeypatch.setenv("SW_INTRA_I16_FIRST", "0")
+    W = sw.encode("W")[0]
+    q = np.full(2300, W, dtype=np.uint8)  # W/W scores 15: 34,500 for a full copy
+    r, o = sw.synth.database(2000, shard=41)
+    rng = np.random.default_rng(41)
+
+    def planted(n, at, k):
+        s = sw.synth.query(n, shard=int(rng.integers(1 << 30)))
+        s[at:at + k] = W
+        return s
+    extra = [np.full(2300, W, np.uint8),   # inter, > 32767: A -> B -> int32
+             planted(600, 100, 400),       # inter, ~6,000: A -> int16
+             planted(2000, 50, 300),       # inter, widest blocks (quads): A -> int16
+             np.full(2600, W, np.uint8),   # long, > 32767: 1 -> 2 -> int32
+             planted(3000, 900, 400),      # long, ~6,000: 1 -> int16
+             planted(2700, 10, 2290)]      # long, ~34,000: 1 -> 2 -> int32
+    r2 = np.concatenate([r] + extra)
+    o2 = np.concatenate([o, o[-1] + np.cumsum([len(x) for x in extra])])
+    db = sw.Database(handle, r2, o2, long_threshold=2500)
+    m = sw.capi.builtin_matrix(mid)
+    want = oracle.scan(q, r2, o2, mat=m, gap_open=go, gap_extend=ge, nthreads=16)
+    assert int(want.max()) > 32767 and int((want > 4096).sum()) >= 6
+    for _ in range(2):
+        got = db.scan(q, m, go, ge)
+        assert handle.last_kernel().endswith("+lpt+drain"), handle.last_kernel()
+        assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    monkeypatch.setenv("SW_LPT", "0")
+    assert np.array_equal(db.scan(q, m, go, ge), want)
+    db.close()
