@@ -369,6 +369,7 @@ struct sw_db {
     // sw_scan_lpt work tables (longest first), per scan shape
     struct LptTable {
         int32_t qpad, qpad_intra, ri, npair, group /* quad blocks */, n;
+        int32_t npipe;  // the longest pairs, in the pipelined form
         int32_t* d_order;
         std::vector<float> cost;  // estimated duration of each entry, longest first
     };
@@ -982,7 +983,10 @@ int32_t pair_blocks(const sw_db* db) {
 // (profiles/r02_strong/traces/).  Only the order matters: the dispatcher
 // starts workgroups in grid order, so the longest work starts first.
 constexpr double kTickUs = 7.4;
-double intra_step_us(int ri) { return 0.157 * (ri * 28.8 + 80.0) / (6 * 28.8 + 80.0); }
+// (0.157 us alone on a SIMD; inside the busy merged grid a step takes ~0.3
+// us, profiles/r04_*/: with the doubled cost the long subjects start early
+// enough, C2's 1/8 share +0.8 %)
+double intra_step_us(int ri) { return 2 * 0.157 * (ri * 28.8 + 80.0) / (6 * 28.8 + 80.0); }
 
 // The widest group blocks of the merged launch run by quads: those at least
 // kQuadFrac x the long threshold wide, whose pair latency would otherwise
@@ -1016,11 +1020,12 @@ double group_ticks_host(int64_t ncols, int passes, int G) {
 
 // The work table of sw_scan_lpt for this scan shape (built once, cached).
 int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad,
-              const int32_t** order, int* n) {
+              const int32_t** order, int* n, int32_t* npipe_out) {
     for (const auto& t : db->lpt_tables)
         if (t.qpad == qpad && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad) {
             *order = t.d_order;
             *n = t.n;
+            *npipe_out = t.npipe;
             return SW_OK;
         }
     const int passes = qpad / 64;
@@ -1045,9 +1050,34 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     for (int64_t g = 0; g < swg; ++g)  // widest first: the workgroup's first block bounds it
         w.emplace_back(single_ticks(width(npair + g * swk::kWavesPerWG), passes) * kTickUs,
                        static_cast<int32_t>(pwg + g));
-    for (int64_t g = 0; g < iwg; ++g)
-        w.emplace_back((db->h_llen[static_cast<size_t>(8 * g)] + swk::kLanes - 1) * nch * intra_step_us(ri),
+    // The longest pairs whose one-wave latency would exceed every inter
+    // item's run in the pipelined form (a 128-row query chunk per wave,
+    // ix2::intra_x2_wg PIPE; at most 4 chunks): a pair of one outlier subject
+    // otherwise sets the launch's span alone (C2's 1/8 share: the 7,429-aa
+    // subject's workgroup 1,275 us, every other one <= 1,224 us; pipelined,
+    // 7,662 -> 8,082 GCUPS on one box, profiles/r04_*/).  They start first.
+    // SW_LPT_PIPE=n forces n pairs (tests).
+    const int nchp = (qpad_intra + 127) / 128;
+    double inter_max = 0;
+    for (const auto& e : w) inter_max = std::max(inter_max, e.first);
+    auto pair_us = [&](int64_t p) { return (db->h_llen[static_cast<size_t>(2 * p)] + swk::kLanes - 1) * nch *
+                                           intra_step_us(ri); };
+    int64_t npipe = 0;
+    if (nchp <= swk::kWavesPerWG) {
+        if (const char* e = std::getenv("SW_LPT_PIPE")) npipe = std::atoll(e);
+        else
+            while (npipe < std::min<int64_t>(npairs, 4) && pair_us(npipe) > inter_max) ++npipe;
+    }
+    npipe = std::min(npipe, npairs);
+    const int64_t npipe_wg = npipe / swk::kWavesPerWG;  // ordinary workgroups left with no pair
+    for (int64_t g = npipe_wg; g < iwg; ++g) {
+        const int64_t first = std::max<int64_t>(8 * g, 2 * npipe);  // its longest subject not pipelined
+        if (first >= db->nlong) continue;
+        w.emplace_back((db->h_llen[static_cast<size_t>(first)] + swk::kLanes - 1) * nch * intra_step_us(ri),
                        static_cast<int32_t>(-1 - g));
+    }
+    // (sw_scan_lpt item -1 - (iwg + pair)), ahead of everything
+    for (int64_t p = 0; p < npipe; ++p) w.emplace_back(1e30 - p, static_cast<int32_t>(-1 - (iwg + p)));
     std::stable_sort(w.begin(), w.end(), [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) {
         return x.first > y.first;
     });
@@ -1057,7 +1087,8 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
         ord[k] = w[k].second;
         cost[k] = static_cast<float>(w[k].first);
     }
-    sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, static_cast<int32_t>(ord.size()), nullptr, cost};
+    sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, static_cast<int32_t>(ord.size()),
+                      static_cast<int32_t>(npipe), nullptr, cost};
     HIPCHECK(hipMalloc(reinterpret_cast<void**>(&t.d_order), ord.size() * sizeof(int32_t)));
     HIPCHECK(hipMemcpy(t.d_order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     db->device_bytes += ord.size() * sizeof(int32_t);
@@ -1068,6 +1099,7 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     db->lpt_tables.push_back(t);
     *order = t.d_order;
     *n = t.n;
+    *npipe_out = t.npipe;
     return SW_OK;
 }
 
@@ -1623,7 +1655,9 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             int nwg = 0;
             const int32_t nquad = lpt_quad_blocks(db, npair);
             a.blk_quad = nquad;
-            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, &order, &nwg))) return rc;
+            int32_t npipe = 0;
+            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, &order, &nwg, &npipe))) return rc;
+            lpt_intra.pipe_pairs = npipe;
             const swk::DrainArgs* dargs = nullptr;
             if (drain) {
                 // the four rescue stages of launch_inter_tail / launch_intra_tail,

@@ -1041,19 +1041,28 @@ __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(InterArgs a
                                                                      const int32_t* __restrict__ order,
                                                                      const DrainArgs* __restrict__ drain) {
     using Elem = typename ix2::IntraImg<RI, true>::Elem;
+    using PElem = typename ix2::IntraImg<2, true>::Elem;
     constexpr size_t kInter = sizeof(X2pSmem<R, SG, 4>);
     constexpr size_t kIntra = sizeof(Elem) * ix2::img_elems<RI, true>();
+    constexpr size_t kPipe = kWavesPerWG * sizeof(PElem) * ix2::img_elems<2, true>();
     constexpr size_t kDrain = drain_smem<AFFINE, RI>();
-    constexpr size_t kSmem = std::max(std::max(kInter, kIntra), kDrain);
+    constexpr size_t kSmem = std::max(std::max(std::max(kInter, kIntra), kDrain), kPipe);
     __shared__ __attribute__((aligned(16))) char smem[kSmem];
     __shared__ int task[2 + 2 * kWavesPerWG];
     const int item = order[blockIdx.x];
     const uint64_t t0 = trace_now();
+    // intra items: -1 - g; g < the launch's intra workgroups (RI rows per
+    // lane, 4 pairs) or, past them, one of the longest pairs in the
+    // pipelined form (2 rows per lane, a chunk per wave)
+    const int niwg = ((ia.nsubj + 1) / 2 + kWavesPerWG - 1) / kWavesPerWG;
     bool flagged;
     if (item >= 0)
         flagged = x2p_wg<R, SG, AFFINE, true, true, 4>(a, item, a.blk_quad, *reinterpret_cast<X2pSmem<R, SG, 4>*>(smem));
-    else
+    else if (-1 - item < niwg)
         flagged = ix2::intra_x2_wg<RI, true, false, !AFFINE>(ia, -1 - item, reinterpret_cast<Elem*>(smem));
+    else
+        flagged = ix2::intra_x2_wg<2, true, false, !AFFINE, true, true>(ia, -1 - item - niwg,
+                                                                       reinterpret_cast<PElem*>(smem));
     // per-workgroup timeline (trace builds): after the per-block entries
     if (threadIdx.x == 0) trace_block(a, a.nblocks + blockIdx.x, t0, 0, item >= 0 ? 2 : 3);
     // Only a workgroup that appended an entry drains (and takes whatever is

@@ -171,8 +171,15 @@ __host__ __device__ constexpr int img_elems() { return kCodes * IntraImg<RI, F16
 // otherwise a.subj_list holds plain subject indices (the merged launch's
 // drain passes the entries it took, in LDS).
 // Returns (per wave) whether the wave appended a subject to a.rescue_list.
-template <int RI, bool F16, bool LIST, bool LIN = false, bool TAKE = true>
+// PIPE (fp16 only, not LIST): ONE subject pair per workgroup (pair wgi), its
+// query chunks (at most kWavesPerWG) pipelined over the waves, each wave with
+// its own image in img (kWavesPerWG images): the longest subjects' latency
+// form for the merged launch, whose span one long pair otherwise sets
+// (chunks x steps on one wave; here ~steps + 2 rounds per extra chunk).
+constexpr int kPipeLag = 2;
+template <int RI, bool F16, bool LIST, bool LIN = false, bool TAKE = true, bool PIPE = false>
 __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typename IntraImg<RI, F16>::Elem* img) {
+    static_assert(!(PIPE && LIST), "the pipelined form takes its pair by index");
     static_assert(RI % 2 == 0 && RI <= 16, "rows per lane");
     constexpr int CH = kLanes * RI;  // query rows per chunk
     using C = IntraCell<F16>;
@@ -185,9 +192,11 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const bool is_last_lane = lane == kLanes - 1;
-    const int p = wgi * kWavesPerWG + wave;  // subject pair
+    const int p = PIPE ? wgi : wgi * kWavesPerWG + wave;  // subject pair
     int sa = 2 * p, sb = 2 * p + 1;
-    bool hasA = sa < a.nsubj, hasB = sb < a.nsubj;
+    // (pairs the merged launch runs in the pipelined form are skipped here)
+    const bool skip = !PIPE && !LIST && p < a.pipe_pairs;
+    bool hasA = !skip && sa < a.nsubj, hasB = !skip && sb < a.nsubj;
     if constexpr (LIST) {
         const int n = __builtin_amdgcn_readfirstlane(*a.list_count);
         if (wgi * 2 * kWavesPerWG >= n) return false;  // workgroup-uniform
@@ -229,173 +238,210 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
     for (int q = 0; q < NACC; ++q) acc[q] = C::from(C::zero(a));
     constexpr uint32_t kPadPair = kPadCode | (kPadCode << 8);
 
-    for (int c0 = 0; c0 < a.qpad; c0 += CH) {
-        const bool first = (c0 == 0);
-        const bool last = (c0 + CH >= a.qpad);
-        __syncthreads();  // the previous chunk's LDS reads are done
-        // stage rows [c0, c0 + CH) of codes 0..25 as fp16 S + 2 ge (the
-        // linear profile is biased by the gap, a.bias)
-        for (int t = static_cast<int>(threadIdx.x); t < kCodes * NQ * kLanes; t += kWavesPerWG * kLanes) {
+    // One chunk pass: rows [c0, c0 + CH) against the pair's columns, its
+    // profile image in cimg; for_blocks(nblk, block) runs block(bk) for the
+    // blocks of 64 steps (in order: at once, or one per round of a pipeline).
+    auto run_chunk = [&](int c0, Elem* cimg, bool first, bool last, auto&& for_blocks) {
+        (void)c0;
+            // state of step -1 (column -1 - lane: H = 0), before step 0's rebase
+            V H[RI], E[LIN ? 1 : RI];
+#pragma unroll
+            for (int r = 0; r < RI; ++r) {
+                H[r] = step(r + NB - 1);
+                if constexpr (!LIN) E[r] = C::from(C::zero(a));
+            }
+            // bottom row (H, F) of this lane one step back, and H of the row above
+            // at the previous column (row 0's diagonal): zeros of step -1
+            uint32_t hl = C::step(a, RI + NB - 2), fl = C::step(a, RI + NB - 1);
+            uint32_t up_prev = C::step(a, NB - 2);
+            uint32_t rc = kPadPair;        // codes (A | B << 8) of this lane's current column
+            uint32_t in_res = kPadPair, in_bh = 0, in_bf = 0;
+            const int nsteps = L + kLanes - 1;
+            // LDS byte address of this lane's element of code 0
+            const uint32_t lrow = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(cimg + lane));
+
+            constexpr uint32_t kCodeBytes = NQ * kLanes * sizeof(Elem);
+            // the profile words of code pair rcx (A | B << 8) for this lane
+            auto read_words = [&](uint32_t rcx, Elem (&wa)[NQ], Elem (&wb)[NQ]) {
+                typename Img::LElem* pa = reinterpret_cast<typename Img::LElem*>(
+                    static_cast<uintptr_t>(lrow + (rcx & 0xffu) * kCodeBytes));
+                typename Img::LElem* pb = reinterpret_cast<typename Img::LElem*>(
+                    static_cast<uintptr_t>(lrow + ((rcx >> 8) & 0xffu) * kCodeBytes));
+#pragma unroll
+                for (int qq = 0; qq < NQ; ++qq) {
+                    wa[qq] = __builtin_bit_cast(Elem, pa[qq * kLanes]);
+                    wb[qq] = __builtin_bit_cast(Elem, pb[qq * kLanes]);
+                }
+            };
+            auto codes_at = [&](int col) {
+                const uint32_t ca = col < LA ? resA[col] : kPadCode;
+                const uint32_t cb = col < LB ? resB[col] : kPadCode;
+                return ca | (cb << 8);
+            };
+            uint32_t in_res_nb = codes_at(lane);  // codes of the next block of 64 steps
+            // profile words, double-buffered by step parity (NB is even, so a
+            // bias period starts on buffer 0): step b reads W[b & 1] and
+            // prefetches the next step's into the other, no register copies
+            Elem W[2][2][NQ];
+            uint32_t rc_n = 0;
+
+            const int nblk = (nsteps + kLanes - 1) / kLanes;
+            auto block = [&](int bk) {
+                const int k0 = bk * kLanes;
+                // lane-0 conveyors for steps k0 .. k0+63 (column k = step); the
+                // first chunk's row -1 is H = 0, F = 0 at the bias lane 0 reads
+                // them with (see the hand-off below)
+                {
+                    const int col = k0 + lane;
+                    in_res = in_res_nb;
+                    in_res_nb = codes_at(col + kLanes);
+                    const int bz = RI - 2 + (col % NB) + ((col % NB) == 0 ? NB : 0);
+                    // (bz ge + zero) computed, not indexed: a lane-varying index
+                    // into the argument table would copy the table to registers
+                    in_bh = (!first && col < L) ? bnd_h[col] : C::pair_of(bz * a.gap_extend + C::zero_int(a));
+                    in_bf = (!first && col < L) ? bnd_f[col] : C::pair_of((bz + 1) * a.gap_extend + C::zero_int(a));
+                }
+                if (kPrefetch && k0 == 0) {
+                    rc_n = shr1u(__builtin_amdgcn_readlane(in_res, 0), rc);
+                    read_words(rc_n, W[0][0], W[0][1]);
+                }
+                // whole bias periods (steps past nsteps run pad columns: harmless)
+                const int mend = min(kLanes, nsteps - k0);
+                for (int m0 = 0; m0 < mend; m0 += NB) {
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) {
+                        const int m = m0 + b;
+                        const uint32_t sbh = __builtin_amdgcn_readlane(in_bh, m);
+                        const uint32_t sbf = LIN ? 0u : __builtin_amdgcn_readlane(in_bf, m);
+                        static_assert(NB % 2 == 0, "buffer parity");
+                        Elem(&wa)[NQ] = W[b & 1][0];
+                        Elem(&wb)[NQ] = W[b & 1][1];
+                        if constexpr (kPrefetch) {
+                            rc = rc_n;
+                            // the next step's codes: lane 0 takes the next column
+                            // (the next block's first at the block's last step)
+                            const bool wrap = (b == NB - 1) && (m0 + NB == kLanes);
+                            const uint32_t sres_n = wrap ? __builtin_amdgcn_readlane(in_res_nb, 0)
+                                                         : __builtin_amdgcn_readlane(in_res, (m + 1) & (kLanes - 1));
+                            rc_n = shr1u(sres_n, rc);
+                            read_words(rc_n, W[(b + 1) & 1][0], W[(b + 1) & 1][1]);
+                        } else {
+                            rc = shr1u(__builtin_amdgcn_readlane(in_res, m), rc);
+                            read_words(rc, wa, wb);
+                        }
+                        // hand-off: the row above's bottom (H, F) from one step back
+                        const V adj = diff(RI - 1 + (b == 0 ? NB : 0));
+                        const uint32_t up0 = C::bits(C::from(shr1u(sbh, hl)) - adj);
+                        V f = LIN ? C::from(0u) : C::from(shr1u(sbf, fl)) - adj;
+                        if (b == 0) {  // rebase: the bias period restarts
+                            const V reb = diff(NB);
+#pragma unroll
+                            for (int r = 0; r < RI; ++r) {
+                                H[r] = H[r] - reb;
+                                if constexpr (!LIN) E[r] = E[r] - reb;
+                            }
+                            up_prev = C::bits(C::from(up_prev) - reb);
+                        }
+                        // H_diag + S for every row first (from the previous
+                        // column's H), so H is then updated in place
+                        V T[RI];
+#pragma unroll
+                        for (int r = 0; r < RI; ++r) {
+                            const uint32_t ua = Img::word(wa, r), ub = Img::word(wb, r);
+                            // low half: subject A's S for row r, high half: subject B's
+                            const V sc = C::from(__builtin_amdgcn_perm(ub, ua, (r & 1) ? 0x07060302u : 0x05040100u));
+                            T[r] = (r == 0 ? C::from(up_prev) : H[r - 1]) + sc;
+                        }
+                        // LIN: row 0's up term is the row above's bottom H (up0)
+                        V up = C::from(up0);
+                        up_prev = up0;
+#pragma unroll
+                        for (int r = 0; r < RI; ++r) {
+                            V h;
+                            if constexpr (LIN) {
+                                h = C::max2(C::max3(H[r], up, T[r]), step(r + b));
+                                up = h;
+                            } else {
+                                h = C::max3(E[r], f, T[r]);
+                                const V mm = h - gog;
+                                E[r] = C::max2(E[r], mm);
+                                f = C::max3(f, mm, step(r + 1 + b));
+                            }
+                            V& ac = acc[r + b];
+                            if (b & 1) {
+                                if (r + 1 < RI) ac = C::max3(ac, h, H[r + 1]);  // H[r + 1]: cell (r + 1, step - 1)
+                                else ac = C::max2(ac, h);
+                            } else if (r == 0) {  // the even steps' other rows are partners above
+                                ac = C::max2(ac, h);
+                            }
+                            H[r] = h;
+                        }
+                        hl = C::bits(H[RI - 1]);
+                        if constexpr (!LIN) fl = C::bits(f);
+                        if (!last) {
+                            // lane 63 finished column k - 63: it stores it for the
+                            // next pass itself (no per-step collection across lanes)
+                            const int oc = k0 + m - (kLanes - 1);
+                            if (oc >= 0 && oc < L && is_last_lane) {
+                                bnd_h[oc] = hl;
+                                if constexpr (!LIN) bnd_f[oc] = fl;
+                            }
+                        }
+                        // pin the maxima at every step (left free, the compiler
+                        // defers the reductions and keeps every h alive)
+#pragma unroll
+                        for (int q = 0; q < NACC; ++q) asm volatile("" : "+v"(acc[q]));
+                    }
+                }
+            };
+            for_blocks(nblk, block);
+    };
+    // stage rows [c0, c0 + CH) of codes 0..25 into image im as fp16 S + 2 ge
+    // (the linear profile is biased by the gap, a.bias), threads [t0, ...)
+    // in steps of `stride`
+    auto stage = [&](Elem* im, int c0, int t0, int stride) {
+        for (int t = t0; t < kCodes * NQ * kLanes; t += stride) {
             const int code = t / (NQ * kLanes);
             const int u = t % (NQ * kLanes);
             const int qq = u / kLanes, ln = u % kLanes;
-            img[t] = Img::load(prof16 + static_cast<size_t>(code) * a.prof_stride + c0 + ln * RI + Img::kRows * qq,
-                               a.bias - 2 * a.gap_extend);
+            im[t] = Img::load(prof16 + static_cast<size_t>(code) * a.prof_stride + c0 + ln * RI + Img::kRows * qq,
+                              a.bias - 2 * a.gap_extend);
         }
+    };
+    const int nch = (a.qpad + CH - 1) / CH;
+    if constexpr (!PIPE) {
+        for (int c0 = 0; c0 < a.qpad; c0 += CH) {
+            __syncthreads();  // the previous chunk's LDS reads are done
+            stage(img, c0, static_cast<int>(threadIdx.x), kWavesPerWG * kLanes);
+            __syncthreads();
+            if (!hasA && !hasB) continue;  // wave-uniform; the barriers above are shared
+            run_chunk(c0, img, c0 == 0, c0 + CH >= a.qpad, [](int nblk, auto& block) {
+                for (int bk = 0; bk < nblk; ++bk) block(bk);
+            });
+        }
+    } else {
+        // PIPE: wave w runs chunk w (nch <= 4 chunks), kPipeLag rounds of 64
+        // steps behind wave w - 1, one workgroup barrier per round: the
+        // boundary row wave w - 1 writes for column c (at its step c + 63)
+        // is read by wave w at the start of block c / 64, >= 1 round later,
+        // and overwritten by wave w (for wave w + 1) only after that read —
+        // one boundary array serves every stage.
+        if (!hasA && !hasB) return false;  // workgroup-uniform (one pair per workgroup)
+        Elem* mine = img + wave * (kCodes * NQ * kLanes);
+        if (wave < nch) stage(mine, wave * CH, lane, kLanes);
         __syncthreads();
-        if (!hasA && !hasB) continue;  // wave-uniform; the barriers above are shared
-
-        // state of step -1 (column -1 - lane: H = 0), before step 0's rebase
-        V H[RI], E[LIN ? 1 : RI];
-#pragma unroll
-        for (int r = 0; r < RI; ++r) {
-            H[r] = step(r + NB - 1);
-            if constexpr (!LIN) E[r] = C::from(C::zero(a));
-        }
-        // bottom row (H, F) of this lane one step back, and H of the row above
-        // at the previous column (row 0's diagonal): zeros of step -1
-        uint32_t hl = C::step(a, RI + NB - 2), fl = C::step(a, RI + NB - 1);
-        uint32_t up_prev = C::step(a, NB - 2);
-        uint32_t rc = kPadPair;        // codes (A | B << 8) of this lane's current column
-        uint32_t in_res = kPadPair, in_bh = 0, in_bf = 0;
-        const int nsteps = L + kLanes - 1;
-        // LDS byte address of this lane's element of code 0
-        const uint32_t lrow = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(img + lane));
-
-        constexpr uint32_t kCodeBytes = NQ * kLanes * sizeof(Elem);
-        // the profile words of code pair rcx (A | B << 8) for this lane
-        auto read_words = [&](uint32_t rcx, Elem (&wa)[NQ], Elem (&wb)[NQ]) {
-            typename Img::LElem* pa = reinterpret_cast<typename Img::LElem*>(
-                static_cast<uintptr_t>(lrow + (rcx & 0xffu) * kCodeBytes));
-            typename Img::LElem* pb = reinterpret_cast<typename Img::LElem*>(
-                static_cast<uintptr_t>(lrow + ((rcx >> 8) & 0xffu) * kCodeBytes));
-#pragma unroll
-            for (int qq = 0; qq < NQ; ++qq) {
-                wa[qq] = __builtin_bit_cast(Elem, pa[qq * kLanes]);
-                wb[qq] = __builtin_bit_cast(Elem, pb[qq * kLanes]);
-            }
-        };
-        auto codes_at = [&](int col) {
-            const uint32_t ca = col < LA ? resA[col] : kPadCode;
-            const uint32_t cb = col < LB ? resB[col] : kPadCode;
-            return ca | (cb << 8);
-        };
-        uint32_t in_res_nb = codes_at(lane);  // codes of the next block of 64 steps
-        // profile words, double-buffered by step parity (NB is even, so a
-        // bias period starts on buffer 0): step b reads W[b & 1] and
-        // prefetches the next step's into the other, no register copies
-        Elem W[2][2][NQ];
-        uint32_t rc_n = 0;
-
-        // blocks of 64 steps
-        const int nblk = (nsteps + kLanes - 1) / kLanes;
-        for (int bk = 0; bk < nblk; ++bk) {
-            const int k0 = bk * kLanes;
-            // lane-0 conveyors for steps k0 .. k0+63 (column k = step); the
-            // first chunk's row -1 is H = 0, F = 0 at the bias lane 0 reads
-            // them with (see the hand-off below)
-            {
-                const int col = k0 + lane;
-                in_res = in_res_nb;
-                in_res_nb = codes_at(col + kLanes);
-                const int bz = RI - 2 + (col % NB) + ((col % NB) == 0 ? NB : 0);
-                // (bz ge + zero) computed, not indexed: a lane-varying index
-                // into the argument table would copy the table to registers
-                in_bh = (!first && col < L) ? bnd_h[col] : C::pair_of(bz * a.gap_extend + C::zero_int(a));
-                in_bf = (!first && col < L) ? bnd_f[col] : C::pair_of((bz + 1) * a.gap_extend + C::zero_int(a));
-            }
-            if (kPrefetch && k0 == 0) {
-                rc_n = shr1u(__builtin_amdgcn_readlane(in_res, 0), rc);
-                read_words(rc_n, W[0][0], W[0][1]);
-            }
-            // whole bias periods (steps past nsteps run pad columns: harmless)
-            const int mend = min(kLanes, nsteps - k0);
-            for (int m0 = 0; m0 < mend; m0 += NB) {
-#pragma unroll
-                for (int b = 0; b < NB; ++b) {
-                    const int m = m0 + b;
-                    const uint32_t sbh = __builtin_amdgcn_readlane(in_bh, m);
-                    const uint32_t sbf = LIN ? 0u : __builtin_amdgcn_readlane(in_bf, m);
-                    static_assert(NB % 2 == 0, "buffer parity");
-                    Elem(&wa)[NQ] = W[b & 1][0];
-                    Elem(&wb)[NQ] = W[b & 1][1];
-                    if constexpr (kPrefetch) {
-                        rc = rc_n;
-                        // the next step's codes: lane 0 takes the next column
-                        // (the next block's first at the block's last step)
-                        const bool wrap = (b == NB - 1) && (m0 + NB == kLanes);
-                        const uint32_t sres_n = wrap ? __builtin_amdgcn_readlane(in_res_nb, 0)
-                                                     : __builtin_amdgcn_readlane(in_res, (m + 1) & (kLanes - 1));
-                        rc_n = shr1u(sres_n, rc);
-                        read_words(rc_n, W[(b + 1) & 1][0], W[(b + 1) & 1][1]);
-                    } else {
-                        rc = shr1u(__builtin_amdgcn_readlane(in_res, m), rc);
-                        read_words(rc, wa, wb);
-                    }
-                    // hand-off: the row above's bottom (H, F) from one step back
-                    const V adj = diff(RI - 1 + (b == 0 ? NB : 0));
-                    const uint32_t up0 = C::bits(C::from(shr1u(sbh, hl)) - adj);
-                    V f = LIN ? C::from(0u) : C::from(shr1u(sbf, fl)) - adj;
-                    if (b == 0) {  // rebase: the bias period restarts
-                        const V reb = diff(NB);
-#pragma unroll
-                        for (int r = 0; r < RI; ++r) {
-                            H[r] = H[r] - reb;
-                            if constexpr (!LIN) E[r] = E[r] - reb;
-                        }
-                        up_prev = C::bits(C::from(up_prev) - reb);
-                    }
-                    // H_diag + S for every row first (from the previous
-                    // column's H), so H is then updated in place
-                    V T[RI];
-#pragma unroll
-                    for (int r = 0; r < RI; ++r) {
-                        const uint32_t ua = Img::word(wa, r), ub = Img::word(wb, r);
-                        // low half: subject A's S for row r, high half: subject B's
-                        const V sc = C::from(__builtin_amdgcn_perm(ub, ua, (r & 1) ? 0x07060302u : 0x05040100u));
-                        T[r] = (r == 0 ? C::from(up_prev) : H[r - 1]) + sc;
-                    }
-                    // LIN: row 0's up term is the row above's bottom H (up0)
-                    V up = C::from(up0);
-                    up_prev = up0;
-#pragma unroll
-                    for (int r = 0; r < RI; ++r) {
-                        V h;
-                        if constexpr (LIN) {
-                            h = C::max2(C::max3(H[r], up, T[r]), step(r + b));
-                            up = h;
-                        } else {
-                            h = C::max3(E[r], f, T[r]);
-                            const V mm = h - gog;
-                            E[r] = C::max2(E[r], mm);
-                            f = C::max3(f, mm, step(r + 1 + b));
-                        }
-                        V& ac = acc[r + b];
-                        if (b & 1) {
-                            if (r + 1 < RI) ac = C::max3(ac, h, H[r + 1]);  // H[r + 1]: cell (r + 1, step - 1)
-                            else ac = C::max2(ac, h);
-                        } else if (r == 0) {  // the even steps' other rows are partners above
-                            ac = C::max2(ac, h);
-                        }
-                        H[r] = h;
-                    }
-                    hl = C::bits(H[RI - 1]);
-                    if constexpr (!LIN) fl = C::bits(f);
-                    if (!last) {
-                        // lane 63 finished column k - 63: it stores it for the
-                        // next pass itself (no per-step collection across lanes)
-                        const int oc = k0 + m - (kLanes - 1);
-                        if (oc >= 0 && oc < L && is_last_lane) {
-                            bnd_h[oc] = hl;
-                            if constexpr (!LIN) bnd_f[oc] = fl;
-                        }
-                    }
-                    // pin the maxima at every step (left free, the compiler
-                    // defers the reductions and keeps every h alive)
-#pragma unroll
-                    for (int q = 0; q < NACC; ++q) asm volatile("" : "+v"(acc[q]));
+        const int nblk = (L + 2 * kLanes - 2) / kLanes;  // = run_chunk's
+        const int rounds = nblk + kPipeLag * (nch - 1);
+        if (wave < nch) {
+            run_chunk(wave * CH, mine, wave == 0, wave == nch - 1, [&](int nb, auto& block) {
+                for (int r = 0; r < rounds; ++r) {
+                    const int bk = r - kPipeLag * wave;
+                    if (bk >= 0 && bk < nb) block(bk);
+                    __syncthreads();
                 }
-            }
+            });
+        } else {
+            for (int r = 0; r < rounds; ++r) __syncthreads();
         }
     }
     // the lane's maximum (bias removed, offset kept: fp16 does not hold the
@@ -407,6 +453,15 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
     for (int off = 32; off > 0; off >>= 1) {
         const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(C::bits(best)), off));
         best = C::max2(best, C::from(o));
+    }
+    if constexpr (PIPE) {
+        // the stages' maxima (each covers its chunk's rows) to wave 0; the
+        // images are free after the last round's barrier
+        uint32_t* part = reinterpret_cast<uint32_t*>(img);
+        if (wave < nch && lane == 0) part[wave] = C::bits(best);
+        __syncthreads();
+        if (wave != 0) return false;
+        for (int w = 1; w < nch; ++w) best = C::max2(best, C::from(part[w]));
     }
     bool flagged = false;
     if (lane == 0) {

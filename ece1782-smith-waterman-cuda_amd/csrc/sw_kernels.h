@@ -131,6 +131,9 @@ struct IntraArgs {
     // sw_intra in list mode: only subjects subj_list[0 .. *list_count)
     const int32_t* subj_list = nullptr;
     const int32_t* list_count = nullptr;
+    // sw_scan_lpt: pairs [0, pipe_pairs) run in the pipelined form; the
+    // launch's ordinary intra workgroups skip them
+    int32_t pipe_pairs = 0;
 };
 
 // ---- device-side rescue lists: [count, item 0, item 1, ...] --------------

@@ -613,17 +613,19 @@ def test_random_scoring_and_shapes(sw, oracle, handle, case):
                                            handle.last_intra_kernel(), np.nonzero(got != want)[0][:10])
 
 
-@pytest.mark.parametrize("quad_width", ["0", "200", "16"])
+@pytest.mark.parametrize("quad_width, pipe", [("0", "0"), ("200", "0"), ("16", "0"), ("200", "2"), ("0", "100")])
 @pytest.mark.parametrize("scoring", [(1, 12, 1), (0, 2, 2)])
-def test_merged_lpt_launch(sw, oracle, handle, monkeypatch, quad_width, scoring):
+def test_merged_lpt_launch(sw, oracle, handle, monkeypatch, quad_width, pipe, scoring):
     """sw_scan_lpt (the inter blocks by quads / pairs / single waves and the
     long subjects' fp16 pass in one launch, longest work first): queries for
     the three intra shapes it supports (4, 6, 8 rows per lane), quads for
-    none, the widest or every group block, planted near-copies in both
-    kernels' halves (rescue chains after the merged launch), against the
-    oracle and the two-launch form."""
+    none, the widest or every group block, the longest pairs in the
+    pipelined form (a query chunk per wave) for none, 8 or every long
+    subject, planted near-copies in both kernels' halves (rescued inside the
+    merged launch), against the oracle and the two-launch form."""
     mid, go, ge = scoring
     monkeypatch.setenv("SW_LPT", "1")
+    monkeypatch.setenv("SW_LPT_PIPE", pipe)
     monkeypatch.setenv("SW_QUAD_WIDTH", quad_width)
     monkeypatch.setenv("SW_PAIR_WIDTH", "64")
     r, o = sw.synth.database(2500, shard=23)
