@@ -445,30 +445,51 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def launch_ranks(n, argv):
+def launch_ranks(n, argv, attempts=2):
     """`bench.py --gpus N` started without a torchrun environment: start N
     ranks as ONE child process (`python -m torch.distributed.run`, one rank per
     GPU, rendezvous on 127.0.0.1), relay rank 0's single JSON line and return
     the child's exit code.  Runs before anything in this process touches HIP
-    (torch is not even imported here) and never replaces this process."""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
-    log("starting %d ranks: %s" % (n, " ".join(cmd)))
-    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, cwd=REPO)
-    lines = []
-    for line in proc.stdout:
-        s = line.strip()
-        if s.startswith("{") and '"metric"' in s:
-            lines.append(s)
-        elif s:
-            print(s, file=sys.stderr, flush=True)
-    rc = proc.wait()
+    (torch is not even imported here) and never replaces this process.  The
+    rendezvous port is picked free just before the launch; if another process
+    takes it in between (the child fails with no JSON line and an address-in-
+    use error), the launch is tried once more on a new port."""
+    for attempt in range(attempts):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+        log("starting %d ranks: %s" % (n, " ".join(cmd)))
+        proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, cwd=REPO)
+        lines, port_taken = [], False
+        for line in proc.stdout:
+            s = line.strip()
+            if s.startswith("{") and '"metric"' in s:
+                lines.append(s)
+            elif s:
+                port_taken = port_taken or "address already in use" in s.lower() or "EADDRINUSE" in s
+                print(s, file=sys.stderr, flush=True)
+        rc = proc.wait()
+        if rc != 0 and not lines and port_taken and attempt + 1 < attempts:
+            log("rendezvous port taken; retrying on another port")
+            continue
+        break
     if rc == 0 and len(lines) != 1:
         log("expected one JSON line from rank 0, got %d" % len(lines))
         rc = 1
     if lines:
         print(lines[-1], flush=True)
     return rc
+
+
+def sustained_summary(elapsed_s, steps, cells_per_step, kernel_ms_total, nscans, world):
+    """The `sustained` object: back-to-back steps for >= --sustained-seconds
+    after the timed region (not part of `value`), so clock droop under
+    continuous load shows, with the scan kernel's HIP-event time beside it."""
+    return {"seconds": round(elapsed_s, 3), "steps": steps, "n_gpus": world,
+            "value": round(cells_per_step * steps / elapsed_s / 1e9, 2), "unit": "GCUPS",
+            "ms_per_step": round(elapsed_s * 1e3 / steps, 4),
+            "kernel_ms_per_scan": round(kernel_ms_total / max(nscans, 1), 4),
+            "note": "outside value: the same step back to back for the stated seconds after the timed region "
+                    "(max over ranks), scan kernel time from the library's HIP events"}
 
 
 def check_world(gpus, env):
@@ -523,6 +544,9 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = rehearse the multi-rank path on one GPU (CPU collectives)")
     ap.add_argument("--device", type=int, default=None, help="override the GPU index (rehearsal)")
+    ap.add_argument("--sustained-seconds", type=float, default=5.0,
+                    help="after the timed steps, run the step back to back this long and report it as "
+                         "`sustained` (outside value; 0 = skip)")
     args = ap.parse_args()
     if args.config == "c1":
         return c1_main(args)
@@ -663,11 +687,12 @@ def main():
 
     cells_rank = float(qtot) * residues
 
-    def timed_loop():
+    def timed_loop(steps=None, warmup=None):
         """W untimed steps, then K timed steps between barrier + sync pairs;
         returns (max-over-ranks seconds, all ranks' cells per step, kernel
         timing, name of the per-wave inter kernel)."""
-        for _ in range(args.warmup):
+        steps = args.steps if steps is None else steps
+        for _ in range(args.warmup if warmup is None else warmup):
             step()
         torch.cuda.synchronize()
         if world > 1:
@@ -675,7 +700,7 @@ def main():
         torch.cuda.synchronize()
         handle.timing_reset()
         t_start = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(steps):
             step()
         t_enq = time.perf_counter() - t_start  # host time to enqueue the K steps
         torch.cuda.synchronize()
@@ -683,7 +708,7 @@ def main():
             tdist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t_start
-        log("rank %d: %d steps in %.3f ms, host enqueue %.3f ms" % (rank, args.steps, elapsed * 1e3, t_enq * 1e3))
+        log("rank %d: %d steps in %.3f ms, host enqueue %.3f ms" % (rank, steps, elapsed * 1e3, t_enq * 1e3))
         kt = handle.timing_total()
         if world > 1:
             t = torch.tensor([elapsed, cells_rank], dtype=torch.float64,
@@ -696,6 +721,13 @@ def main():
 
     elapsed_max, cells_all, kt, (kernel, intra_kernel) = timed_loop()
     st = db.stats()  # the coop split of the timed scans
+    sustained = None
+    if args.sustained_seconds > 0:
+        # back to back for >= the stated seconds (every rank runs the same
+        # count: from the timed region's max-over-ranks step time)
+        n_sus = max(args.steps, int(math.ceil(args.sustained_seconds / (elapsed_max / args.steps))))
+        s_elapsed, s_cells, s_kt, _ = timed_loop(steps=n_sus, warmup=0)
+        sustained = sustained_summary(s_elapsed, n_sus, s_cells, s_kt["wave_ms"], s_kt["scans"], world)
     final_keys = (final if world > 1 else top).cpu().numpy()
     top_ids, top_scores = sw.capi.decode_keys(final_keys[0])
     # the measured run's scores and keys (its last step's buffer), for the parity leg
@@ -860,6 +892,8 @@ def main():
             out["rehearsal"] = "rank %d's share of %d GPUs measured alone on one GPU" % (shard_rank, shard_world)
         if ref is not None:
             out["reference_scoring"] = ref
+        if sustained is not None:
+            out["sustained"] = sustained
         if verify_res is not None:
             out["parity"] = verify_res
             out["parity_sample_ok"] = verify_ok

@@ -1063,12 +1063,14 @@ __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(InterArgs a
     else
         flagged = ix2::intra_x2_wg<2, true, false, !AFFINE, true, true>(ia, -1 - item - niwg,
                                                                        reinterpret_cast<PElem*>(smem));
-    // per-workgroup timeline (trace builds): after the per-block entries
-    if (threadIdx.x == 0) trace_block(a, a.nblocks + blockIdx.x, t0, 0, item >= 0 ? 2 : 3);
     // Only a workgroup that appended an entry drains (and takes whatever is
     // listed, its own entries included): every entry is then taken by its
     // producer at the latest, and the rest of the grid pays one barrier.
-    if (drain && __syncthreads_or(flagged)) lpt_drain<AFFINE, RI>(drain, smem, task);
+    const bool any = __syncthreads_or(flagged);
+    // per-workgroup timeline (trace builds), after the per-block entries:
+    // every wave of the workgroup is done here
+    if (threadIdx.x == 0) trace_block(a, a.nblocks + blockIdx.x, t0, 0, item >= 0 ? 2 : 3);
+    if (drain && any) lpt_drain<AFFINE, RI>(drain, smem, task);
 }
 
 template <int RI>

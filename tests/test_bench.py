@@ -77,3 +77,39 @@ def test_bench_c1_json_line():
         assert k in cb, k
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1
     assert 0 < cb["one_thread"] <= cb["value"] * 1.2
+
+
+def test_bench_sustained_object():
+    """The `sustained` object of the bench line (back-to-back steps after the
+    timed region, outside value): its keys and arithmetic."""
+    sys.path.insert(0, REPO)
+    import bench
+    d = bench.sustained_summary(5.0, 4000, 9.6e9, 4000 * 1.2, 4000, 1)
+    for k in ("seconds", "steps", "n_gpus", "value", "unit", "ms_per_step", "kernel_ms_per_scan", "note"):
+        assert k in d, k
+    assert d["unit"] == "GCUPS" and d["steps"] == 4000
+    assert abs(d["value"] - 9.6e9 * 4000 / 5.0 / 1e9) < 0.01
+    assert abs(d["ms_per_step"] - 1.25) < 1e-9 and abs(d["kernel_ms_per_scan"] - 1.2) < 1e-9
+
+
+def test_bench_rendezvous_retry(monkeypatch):
+    """A rendezvous port taken between picking and binding:
+    the launch is retried once on a new port."""
+    sys.path.insert(0, REPO)
+    import bench
+    calls = []
+
+    class FakeProc:
+        def __init__(self, cmd, **kw):
+            calls.append(cmd[cmd.index("--master-port") + 1])
+            first = len(calls) == 1
+            self.stdout = iter(["RuntimeError: Address already in use\n"] if first else
+                               ['{"metric": "m", "value": 1.0, "n_gpus": 2}\n'])
+            self.rc = 1 if first else 0
+
+        def wait(self):
+            return self.rc
+
+    monkeypatch.setattr(bench.subprocess, "Popen", FakeProc)
+    assert bench.launch_ranks(2, ["--gpus", "2"]) == 0
+    assert len(calls) == 2
