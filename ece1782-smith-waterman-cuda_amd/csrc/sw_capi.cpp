@@ -1569,7 +1569,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         a.residues = db->d_res;
         a.blk_off = db->d_blk_off;
         a.blk_groups = db->d_blk_groups;
-        if (!std::getenv("SW_BLK_COLS16")) a.blk_cols = db->d_blk_cols;
+        a.blk_cols = db->d_blk_cols;
         a.lane_ids = db->d_lane_ids;
         a.nblocks = static_cast<int32_t>(db->nblocks);
         a.prof = P.dev + (x2 ? P.off16 : P.off8);
@@ -1791,6 +1791,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         int64_t res = 0;
         int32_t wmin = 1 << 30, wmax = 0, bmin = 1 << 30, bmax = -1;
         for (int32_t b : ids) {
+            if (b < 0) continue;  // (taken entries are reset to -1: a drained list shows counts only)
             res += db->h_blk_res[b];
             wmin = std::min<int32_t>(wmin, db->h_blk_groups[b] * 16);
             wmax = std::max<int32_t>(wmax, db->h_blk_groups[b] * 16);

@@ -1,36 +1,35 @@
-// sw_inter_x2.hip — inter-sequence Smith-Waterman, packed 16-bit cells
-// (sw_inter_x2s: one subject per lane, two query strips per pass; its wave-
-// pair form sw_inter_x2p).  The first packed form, two SUBJECTS per lane
-// (sw_inter_x2, described below), was measured slower (profiles/r01_x2/) and
-// removed in round 2; its profile-image helpers remain in use.
+// sw_inter_x2.hip — inter-sequence Smith-Waterman in packed 16-bit cells
+// (the reference's f_scoreSequenceTiledCoalesced,
+// SWSolver.cu:201-264): sw_inter_x2s (one subject per lane, TWO query strips
+// per pass, one wave per 64-subject block), its wave-group form sw_inter_x2p
+// (a block's passes split over 2 or 4 waves) and sw_scan_lpt (the whole scan
+// of a small database, inter blocks and long subjects, in one longest-first
+// launch that also re-scores what it flags).
 //
 // Why: the scan is bound by VALU issue.  On gfx950 every 32-bit max/max3 and
 // the SDWA byte add issue at the slow ~4.3-cycle rate, so an int32 affine cell
 // costs ~26 SIMD-cycles per 64 cells (profiles/r01_valu_rate_*.txt); one
-// v_pk_* instruction (also ~4.2 cycles) updates TWO cells.  An affine cell
-// pair is 9 packed instructions (add, 2 max for H, sub for H - go, sub + max
-// for E and for F, max for the running best) plus one fast v_or_b32 that
-// assembles the pair's substitution scores: ~20 cycles per cell.
+// v_pk_* instruction (also ~4.25 cycles) updates TWO cells.
 //
-// Scores for the two subjects' residues come from two images of the query
-// profile that the wave stages in its own LDS slice per strip: `lo` holds
-// S[q_i][c] zero-extended, `hi` holds S[q_i][c] << 16, so
-//     (S[q_i][a] | S[q_i][b] << 16) = lo[a][i] | hi[b][i]
-// with one ds_read_b128 per 4 rows from each image.  (The earlier pair-table
-// form, sw_inter_pk.hip, rebuilt a 676-entry table per strip behind three
-// workgroup barriers; here the waves are independent.)
+// The default cell is fp16 with a bias (x2s_pass): cell (r, jj)
+// of an 8-column sub-group stores H + (r % 16 + jj) ge, so both gap
+// extensions are the drift of the bias and an affine cell pair is 5 packed
+// ops (v_pk_fma_f16 for H_diag + S, v_pk_maximum3_f16 for H, v_pk_add_f16
+// for H - (go - ge), a max for E, a max3 for F with the floor), a linear one
+// 3; the running maxima are kept per anti-diagonal.  The lane's low halves run
+// rows [s0, s0 + 32) at column t, the high halves rows [s0 + 32, s0 + 64) at
+// column t - 8, fed through an 8-entry register delay line, so a 64-row pass
+// hands one dword (H | F << 16) per column to the next pass through HBM.
+// The pair (S_low, S_high) is formed without a combine: the LDS images hold
+// (S, 1) and (1, S) and the fma multiplies them.
 //
-// Layout: wave p handles blocks blk_first + 2p and blk_first + 2p + 1 of the
-// packed database (sw_capi.cpp, widest first): lane l's low half is subject
-// (2p, l), its high half subject (2p+1, l).  Columns past the narrower
-// block's width read as the pad code (score 0).  Strip boundary rows are
-// packed (H, and F for affine) pairs in the wider block's slots of bnd_h/f.
-//
-// Exactness: sw_inter_x2 runs only when (qlen + 2) * (max S + gap open) <
-// 32767, so no H, E, F or H_diag + S can leave int16 and the packed
-// recurrences equal the int32 ones (sw_kernels.hip) bit for bit.  sw_inter_x2s
-// also runs beyond that bound in guarded mode: lanes that reach kSat16 flag
-// their block for the int32 kernel (see the end of the kernel).
+// Exactness: every fp16 value carries the offset -2048 + 2 ge, so true scores
+// up to ~4,000 are exact integers; a lane whose maximum reaches the guard band
+// (a.sat_limit) flags its block, which the int16 form of the same kernel
+// re-scores (x2s_block with F16 = false: up to 32767, guard kSat16), and
+// blocks it flags again go to the int32 kernel (sw_int32.h).  Blocks and
+// subjects are listed on the device (sw_kernels.h list_publish / list_take);
+// no host synchronisation anywhere in the chain.
 #include <algorithm>
 
 #include "sw_int32.h"
@@ -126,6 +125,52 @@ __device__ __forceinline__ void store_pairs(int32_t* p, const uint32_t (&v)[SG])
         *reinterpret_cast<int4*>(p + 4 * q) = make_int4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
 }
 
+// half-word shuffles as one v_perm_b32 each (byte i of the result = byte
+// sel[i] of {src0 : src1}, src1 the low dword): (a.lo, b.lo), (a.hi, b.lo),
+// (a.hi, b.hi)
+__device__ __forceinline__ uint32_t lo_lo(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040100u); }
+__device__ __forceinline__ uint32_t hi_lo(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040302u); }
+__device__ __forceinline__ uint32_t hi_hi(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
+
+// The pass hand-off in HBM, SG columns from index i of the residues' index
+// space: affine (H | F << 16) dwords; linear H alone as 16-bit values (with
+// open = extend the biased cell needs no F: half the bytes).  Per column
+// the value lands in v[q] with H in its low half (even q) or its high half
+// (odd q; col_start picks the matching half).
+template <int SG, bool AFFINE>
+__device__ __forceinline__ void load_bnd(uint32_t (&v)[SG], const uint32_t* bnd, uint64_t i) {
+    if constexpr (AFFINE) {
+        load_pairs<SG>(v, reinterpret_cast<const int32_t*>(bnd) + i);
+    } else {
+        const uint16_t* p = reinterpret_cast<const uint16_t*>(bnd) + i;
+        uint32_t w[SG / 2];
+        if constexpr (SG == 8) {
+            const int4 t = *reinterpret_cast<const int4*>(p);
+            w[0] = t.x; w[1] = t.y; w[2] = t.z; w[3] = t.w;
+        } else {
+            static_assert(SG == 4, "sub-group width");
+            const int2 t = *reinterpret_cast<const int2*>(p);
+            w[0] = t.x; w[1] = t.y;
+        }
+#pragma unroll
+        for (int q = 0; q < SG; ++q) v[q] = w[q / 2];
+    }
+}
+// hb[q]: affine (H | F << 16) of column q; linear H of column q in BOTH halves
+template <int SG, bool AFFINE>
+__device__ __forceinline__ void store_bnd(uint32_t* bnd, uint64_t i, const uint32_t (&hb)[SG]) {
+    if constexpr (AFFINE) {
+        store_pairs<SG>(reinterpret_cast<int32_t*>(bnd) + i, hb);
+    } else {
+        uint16_t* p = reinterpret_cast<uint16_t*>(bnd) + i;
+        uint32_t w[SG / 2];
+#pragma unroll
+        for (int q = 0; q < SG / 2; ++q) w[q] = lo_lo(hb[2 * q], hb[2 * q + 1]);
+        if constexpr (SG == 8) *reinterpret_cast<int4*>(p) = make_int4(w[0], w[1], w[2], w[3]);
+        else *reinterpret_cast<int2*>(p) = make_int2(w[0], w[1]);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // sw_inter_x2s: ONE subject per lane, TWO query strips per pass
 // ---------------------------------------------------------------------------
@@ -192,10 +237,6 @@ __device__ __forceinline__ void stage_x2s(X2Lds<R>& L, const int16_t* __restrict
     }
 }
 
-// half-word shuffles as one v_perm_b32 each (byte i of the result = byte
-// sel[i] of {src0 : src1}, src1 the low dword)
-__device__ __forceinline__ uint32_t lo_lo(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040100u); }
-__device__ __forceinline__ uint32_t hi_lo(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040302u); }
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const v4i lds_int4;
@@ -221,7 +262,6 @@ __device__ __forceinline__ void read_x2a(int4 (&pl)[N], int4 (&ph)[N], uint32_t&
         ph[q] = __builtin_bit_cast(int4, b[q]);
     }
 }
-__device__ __forceinline__ uint32_t hi_hi(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
 
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
@@ -479,7 +519,10 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     uint32_t rc[SG / 4], rp[SG / 4], rn[SG / 4];  // codes: current (low), previous (high), next
 #pragma unroll
     for (int q = 0; q < SG; ++q) {
-        bz[q] = F16 ? lo_lo(a.f16_step[kRowGroup - 1 + q], a.f16_step[kRowGroup + q]) : 0u;
+        // (linear: H of row -1 in both halves, as the 16-bit hand-off loads it)
+        bz[q] = !F16 ? 0u
+                     : AFFINE ? lo_lo(a.f16_step[kRowGroup - 1 + q], a.f16_step[kRowGroup + q])
+                              : lo_lo(a.f16_step[kRowGroup - 1 + q], a.f16_step[kRowGroup - 1 + q]);
         dl_h[q] = F16 ? a.f16_step[kRowGroup - 1 + q] : 0u;
         dl_f[q] = F16 ? a.f16_step[kRowGroup + q] : 0u;
         bin[q] = bz[q];
@@ -490,7 +533,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     load_codes<SG>(rc, a.residues + base, true);
     if (!first) {
         if (PAIR && ring_in) ring_load<SG>(bin, ring_in, 0, lane);
-        else load_pairs<SG>(bin, reinterpret_cast<const int32_t*>(bnd) + base);
+        else load_bnd<SG, AFFINE>(bin, bnd, base);
     }
     int4 PL[2][CQ], PH[2][CQ];
     constexpr uint32_t RB = x2_row_dwords(R) * 4;
@@ -558,7 +601,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
             load_codes<SG>(rn, a.residues + base + noff, next_lo);
             if (!next_first && next_lo) {
                 if (PAIR && ring_in) ring_load<SG>(bin_n, ring_in, (ncol / SG) % kRingSlots, lane);
-                else load_pairs<SG>(bin_n, reinterpret_cast<const int32_t*>(bnd) + base + noff);
+                else load_bnd<SG, AFFINE>(bin_n, bnd, base + noff);
             }
         }
         if constexpr (F16) {
@@ -666,7 +709,8 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
         // high strip from the low strip's bottom row SG steps back (fp16:
         // both from the last row group's bias to row -1's / row 0's)
         auto col_start = [&](V& up, V& diag, V& f, const int jj) {
-            const uint32_t u = lo_lo(bin[jj], dl_h[jj]);
+            // (linear, odd columns: the 16-bit hand-off holds their H in the high half)
+            const uint32_t u = (AFFINE || jj % 2 == 0) ? lo_lo(bin[jj], dl_h[jj]) : hi_lo(bin[jj], dl_h[jj]);
             // fp16: row 0's diagonal keeps the last row group's bias (the
             // profile's row 0 takes it back); the linear cell's up term drops it
             up = P::from(u);
@@ -730,13 +774,13 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
             // boundary out = the high halves of the delay line just written
             uint32_t hb[SG];
 #pragma unroll
-            for (int q = 0; q < SG; ++q) hb[q] = AFFINE ? hi_hi(dl_h[q], dl_f[q]) : (dl_h[q] >> 16);
+            for (int q = 0; q < SG; ++q) hb[q] = AFFINE ? hi_hi(dl_h[q], dl_f[q]) : hi_hi(dl_h[q], dl_h[q]);
             const uint32_t pc = CHAIN ? (lo_c == 0 ? ncols - SG : lo_c - SG) : col0 - SG;
             if (PAIR && ring_out) {
                 ring_store<SG>(ring_out, (pc / SG) % kRingSlots, lane, hb);
             } else {
                 const uint64_t poff = (pc >> 4) * kGroupBytes + (pc & 15);
-                store_pairs<SG>(reinterpret_cast<int32_t*>(bnd) + base + poff, hb);
+                store_bnd<SG, AFFINE>(bnd, base + poff, hb);
             }
         }
         if (has_next) {
@@ -1044,7 +1088,7 @@ __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(InterArgs a
     using PElem = typename ix2::IntraImg<2, true>::Elem;
     constexpr size_t kInter = sizeof(X2pSmem<R, SG, 4>);
     constexpr size_t kIntra = sizeof(Elem) * ix2::img_elems<RI, true>();
-    constexpr size_t kPipe = kWavesPerWG * sizeof(PElem) * ix2::img_elems<2, true>();
+    constexpr size_t kPipe = kWavesPerWG * sizeof(PElem) * ix2::img_elems<2, true>() + kWavesPerWG * sizeof(int);
     constexpr size_t kDrain = drain_smem<AFFINE, RI>();
     constexpr size_t kSmem = std::max(std::max(std::max(kInter, kIntra), kDrain), kPipe);
     __shared__ __attribute__((aligned(16))) char smem[kSmem];

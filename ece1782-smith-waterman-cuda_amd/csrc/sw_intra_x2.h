@@ -173,10 +173,10 @@ __host__ __device__ constexpr int img_elems() { return kCodes * IntraImg<RI, F16
 // Returns (per wave) whether the wave appended a subject to a.rescue_list.
 // PIPE (fp16 only, not LIST): ONE subject pair per workgroup (pair wgi), its
 // query chunks (at most kWavesPerWG) pipelined over the waves, each wave with
-// its own image in img (kWavesPerWG images): the longest subjects' latency
-// form for the merged launch, whose span one long pair otherwise sets
-// (chunks x steps on one wave; here ~steps + 2 rounds per extra chunk).
-constexpr int kPipeLag = 2;
+// its own image in img (kWavesPerWG images, then kWavesPerWG progress ints):
+// the longest subjects' latency form for the merged launch, whose span one
+// long pair otherwise sets (chunks x steps on one wave; here ~steps + 128 per
+// extra chunk).
 template <int RI, bool F16, bool LIST, bool LIN = false, bool TAKE = true, bool PIPE = false>
 __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typename IntraImg<RI, F16>::Elem* img) {
     static_assert(!(PIPE && LIST), "the pipelined form takes its pair by index");
@@ -420,29 +420,46 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
             });
         }
     } else {
-        // PIPE: wave w runs chunk w (nch <= 4 chunks), kPipeLag rounds of 64
-        // steps behind wave w - 1, one workgroup barrier per round: the
-        // boundary row wave w - 1 writes for column c (at its step c + 63)
-        // is read by wave w at the start of block c / 64, >= 1 round later,
-        // and overwritten by wave w (for wave w + 1) only after that read —
-        // one boundary array serves every stage.
+        // PIPE: wave w runs chunk w (nch <= 4 chunks), each at its own pace:
+        // it starts block bk (columns [64 bk, 64 bk + 64)) once wave w - 1 has
+        // finished block bk + 1 (its lane 63 writes the boundary row of column
+        // c at its step c + 63, i.e. in block (c + 63) / 64), told by a
+        // progress count in LDS.  Wave w - 1 writes each column's boundary
+        // value before wave w reads it, and wave w overwrites it (for wave
+        // w + 1) only after reading it: one boundary array serves every
+        // stage, and no wave ever waits for a later one.  (A workgroup barrier
+        // per 64 steps instead tied every stage to the slowest SIMD's pace.)
         if (!hasA && !hasB) return false;  // workgroup-uniform (one pair per workgroup)
+#ifdef SW_PIPE_PRIO
+        __builtin_amdgcn_s_setprio(SW_PIPE_PRIO);
+#endif
         Elem* mine = img + wave * (kCodes * NQ * kLanes);
+        int* prog = reinterpret_cast<int*>(img + kWavesPerWG * (kCodes * NQ * kLanes));
         if (wave < nch) stage(mine, wave * CH, lane, kLanes);
+        if (threadIdx.x < kWavesPerWG) prog[threadIdx.x] = 0;
         __syncthreads();
-        const int nblk = (L + 2 * kLanes - 2) / kLanes;  // = run_chunk's
-        const int rounds = nblk + kPipeLag * (nch - 1);
         if (wave < nch) {
             run_chunk(wave * CH, mine, wave == 0, wave == nch - 1, [&](int nb, auto& block) {
-                for (int r = 0; r < rounds; ++r) {
-                    const int bk = r - kPipeLag * wave;
-                    if (bk >= 0 && bk < nb) block(bk);
-                    __syncthreads();
+                for (int bk = 0; bk < nb; ++bk) {
+                    if (wave > 0) {
+                        const int need = min(bk + 2, nb);
+                        // bounded: wave 0 never waits, so every stage progresses
+                        for (int spin = 0; spin < (1 << 24); ++spin) {
+                            if (__hip_atomic_load(prog + wave - 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >=
+                                need)
+                                break;
+                            __builtin_amdgcn_s_sleep(1);
+                        }
+                    }
+                    block(bk);
+                    // this block's boundary stores before its progress count
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == 0)
+                        __hip_atomic_store(prog + wave, bk + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             });
-        } else {
-            for (int r = 0; r < rounds; ++r) __syncthreads();
         }
+        __syncthreads();  // every stage done (and the images free)
     }
     // the lane's maximum (bias removed, offset kept: fp16 does not hold the
     // true scores above 2048 exactly), then the wave's

@@ -3,7 +3,9 @@ for offline analysis (run with a -DSW_TRACE_BLOCKS build via SW_AMD_LIB and
 SW_TRACE_FILE set).  Writes OUT.npz: trace [entries][start, end, HW_ID,
 XCC_ID | kind << 32] (s_memrealtime, 100 MHz), the block widths, the long
 subjects' lengths and the library's timing of the traced scan.
-usage: exp_share_dump.py SHARD_OF OUT.npz [LONG_THRESHOLD]"""
+usage: exp_share_dump.py SHARD_OF OUT.npz [LONG_THRESHOLD] [ref]
+(ref: the reference's scoring, BLOSUM50 with linear gap 2; default BLOSUM62
+affine 11/1)"""
 import json
 import os
 import sys
@@ -19,6 +21,7 @@ path = os.environ["SW_TRACE_FILE"]
 S = int(sys.argv[1])
 out = sys.argv[2]
 T = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+REF = len(sys.argv) > 4 and sys.argv[4] == "ref"
 res, offs = sw.synth.database(570000, shard=0)
 if S > 1:
     _, res, offs = sw.dist.shard(res, offs, 0, S)
@@ -26,9 +29,10 @@ with open(os.path.join(REPO, "tests", "golden", "queries", "P07327.fasta")) as f
     q = sw.encode("".join(f.read().split("\n")[1:]))
 h = sw.Handle(0)
 db = sw.Database(h, res, offs, long_threshold=(T or None))
-m = sw.builtin_matrix(sw.MATRIX_BLOSUM62)
+m = sw.builtin_matrix(sw.MATRIX_BLOSUM50_REF if REF else sw.MATRIX_BLOSUM62)
+go, ge = (2, 2) if REF else (12, 1)
 for _ in range(4):
-    db.scan(q, matrix=m, gap_open=12, gap_extend=1)
+    db.scan(q, matrix=m, gap_open=go, gap_extend=ge)
 st = db.stats()
 tm = h.timing()
 kernel = h.last_kernel()
