@@ -1329,14 +1329,16 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     db->last_pair_merged = npair != 0;
     // One merged launch for the fp16 scan, longest work first (sw_scan_lpt):
     // the inter groups + single waves and the long subjects' fp16 pass, when
-    // the scan takes exactly that shape, on databases far from filling the
-    // GPU (n < 0.35 kFillSubjects: a rank's share of a strong-scaled
-    // database at N >= 4).  Measured (profiles/r02_strong/lpt/, r02_round/):
-    // C2's 1/8 share 1.92 -> 1.45 ms, 1/4 2.57 -> 2.29, 1/2 4.15 -> 4.29;
-    // the whole C2 database 7.55 -> 7.70 ms, so those keep two concurrent
-    // launches.  SW_LPT=0 / 1 forces either form.
+    // the scan takes exactly that shape.  Measured (profiles/r02_strong/lpt/,
+    // r02_round/): C2's 1/8 share 1.92 -> 1.45 ms, 1/4 2.57 -> 2.29.  On the
+    // whole C2 database it was 2 % slower than two concurrent launches until
+    // the launch drained its own rescue lists (no rescue launches or events
+    // after it): now 7.19 -> 7.12 ms under affine scoring (C3 and C4's share
+    // unchanged), but under linear gaps 4.57 -> 5.03 ms (profiles/r04_*/):
+    // affine scans of every database and linear scans of small ones take
+    // it.  SW_LPT=0 / 1 forces either form.
     const char* lpt_env = std::getenv("SW_LPT");
-    const bool lpt_want = lpt_env ? lpt_env[0] == '1' : static_cast<double>(db->n) < 0.35 * kFillSubjects;
+    const bool lpt_want = lpt_env ? lpt_env[0] == '1' : affine || static_cast<double>(db->n) < 0.35 * kFillSubjects;
     const bool lpt = lpt_want && db->nlong && db->nblocks && intra_x2 && !intra_i16_first &&
                      f16 && rescue && npair && !ncoop && i16_span == 0 &&
                      swk::lpt_supported(ri2);

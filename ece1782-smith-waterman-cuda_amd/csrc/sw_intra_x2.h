@@ -430,9 +430,6 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
         // stage, and no wave ever waits for a later one.  (A workgroup barrier
         // per 64 steps instead tied every stage to the slowest SIMD's pace.)
         if (!hasA && !hasB) return false;  // workgroup-uniform (one pair per workgroup)
-#ifdef SW_PIPE_PRIO
-        __builtin_amdgcn_s_setprio(SW_PIPE_PRIO);
-#endif
         Elem* mine = img + wave * (kCodes * NQ * kLanes);
         int* prog = reinterpret_cast<int*>(img + kWavesPerWG * (kCodes * NQ * kLanes));
         if (wave < nch) stage(mine, wave * CH, lane, kLanes);

@@ -62,5 +62,5 @@ if __name__ == "__main__":
         name, body, vgpr = kernel_lines(lines, sym)
         print(f"{sym}  vgpr={vgpr}")
         for hdr, k in loops(body).items():
-            if k["all"] > 500:
+            if k["all"] > int(__import__("os").environ.get("MINLOOP", "500")):
                 print(f"  loop {hdr}: " + " ".join(f"{n}={k[n]}" for n in ("all", "valu", "v_pk", "s_nop", "lds", "vmem", "barrier")))
