@@ -155,6 +155,12 @@ struct IntraImg {
 #define SW_IX2_PREFETCH 1
 #endif
 constexpr bool kPrefetch = SW_IX2_PREFETCH != 0;
+#ifndef SW_IX2_PIPE_PF
+#define SW_IX2_PIPE_PF 2
+#endif
+#ifndef SW_IX2_PIPE_PF_LIN
+#define SW_IX2_PIPE_PF_LIN 1
+#endif
 
 // The LDS image of one chunk: [code][element][lane] (img_elems(RI) elements).
 template <int RI, bool F16>
@@ -189,6 +195,12 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
     constexpr int NQ = Img::kPer;    // image elements per lane and code
     constexpr int NB = 8;            // steps per bias period (one rebase each)
     constexpr int NACC = RI + NB - 1;
+    // profile prefetch distance in steps: the pipelined form's short affine
+    // steps (RI 2) do not cover an LDS read's latency on a busy CU with one
+    // (C2's 1/8 share +0.6 %; linear steps lost 3 % with 2, 6 % with 3)
+    constexpr int PF = PIPE ? (LIN ? SW_IX2_PIPE_PF_LIN : SW_IX2_PIPE_PF) : 1;
+    constexpr int NBUF = PF == 1 ? 2 : 4;
+    static_assert(PF >= 1 && PF <= NBUF - 1, "prefetch distance");
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const bool is_last_lane = lane == kLanes - 1;
@@ -279,11 +291,13 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
                 return ca | (cb << 8);
             };
             uint32_t in_res_nb = codes_at(lane);  // codes of the next block of 64 steps
-            // profile words, double-buffered by step parity (NB is even, so a
-            // bias period starts on buffer 0): step b reads W[b & 1] and
-            // prefetches the next step's into the other, no register copies
-            Elem W[2][2][NQ];
-            uint32_t rc_n = 0;
+            // profile words, in NBUF buffers by step (NB is a multiple of NBUF,
+            // so a bias period starts on buffer 0): step b reads W[b % NBUF]
+            // and prefetches step b + PF's into another, no register copies
+            Elem W[NBUF][2][NQ];
+            uint32_t rcq[PF];  // codes (lane's column) of steps + 1 .. + PF
+#pragma unroll
+            for (int d = 0; d < PF; ++d) rcq[d] = 0;
 
             const int nblk = (nsteps + kLanes - 1) / kLanes;
             auto block = [&](int bk) {
@@ -302,8 +316,11 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
                     in_bf = (!first && col < L) ? bnd_f[col] : C::pair_of((bz + 1) * a.gap_extend + C::zero_int(a));
                 }
                 if (kPrefetch && k0 == 0) {
-                    rc_n = shr1u(__builtin_amdgcn_readlane(in_res, 0), rc);
-                    read_words(rc_n, W[0][0], W[0][1]);
+#pragma unroll
+                    for (int d = 0; d < PF; ++d) {
+                        rcq[d] = shr1u(__builtin_amdgcn_readlane(in_res, d), d == 0 ? rc : rcq[d > 0 ? d - 1 : 0]);
+                        read_words(rcq[d], W[d][0], W[d][1]);
+                    }
                 }
                 // whole bias periods (steps past nsteps run pad columns: harmless)
                 const int mend = min(kLanes, nsteps - k0);
@@ -313,18 +330,21 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
                         const int m = m0 + b;
                         const uint32_t sbh = __builtin_amdgcn_readlane(in_bh, m);
                         const uint32_t sbf = LIN ? 0u : __builtin_amdgcn_readlane(in_bf, m);
-                        static_assert(NB % 2 == 0, "buffer parity");
-                        Elem(&wa)[NQ] = W[b & 1][0];
-                        Elem(&wb)[NQ] = W[b & 1][1];
+                        static_assert(NB % NBUF == 0, "buffer period");
+                        Elem(&wa)[NQ] = W[b % NBUF][0];
+                        Elem(&wb)[NQ] = W[b % NBUF][1];
                         if constexpr (kPrefetch) {
-                            rc = rc_n;
-                            // the next step's codes: lane 0 takes the next column
-                            // (the next block's first at the block's last step)
-                            const bool wrap = (b == NB - 1) && (m0 + NB == kLanes);
-                            const uint32_t sres_n = wrap ? __builtin_amdgcn_readlane(in_res_nb, 0)
-                                                         : __builtin_amdgcn_readlane(in_res, (m + 1) & (kLanes - 1));
-                            rc_n = shr1u(sres_n, rc);
-                            read_words(rc_n, W[(b + 1) & 1][0], W[(b + 1) & 1][1]);
+                            rc = rcq[0];
+#pragma unroll
+                            for (int d = 0; d + 1 < PF; ++d) rcq[d] = rcq[d + 1];
+                            // step b + PF's codes: lane 0 takes that column
+                            // (the next block's first ones at the block's last steps)
+                            const bool wrap = (b + PF >= NB) && (m0 + NB == kLanes);
+                            const uint32_t sres_n =
+                                wrap ? __builtin_amdgcn_readlane(in_res_nb, (b + PF - NB) & (kLanes - 1))
+                                     : __builtin_amdgcn_readlane(in_res, (m + PF) & (kLanes - 1));
+                            rcq[PF - 1] = shr1u(sres_n, PF > 1 ? rcq[PF > 1 ? PF - 2 : 0] : rc);
+                            read_words(rcq[PF - 1], W[(b + PF) % NBUF][0], W[(b + PF) % NBUF][1]);
                         } else {
                             rc = shr1u(__builtin_amdgcn_readlane(in_res, m), rc);
                             read_words(rc, wa, wb);

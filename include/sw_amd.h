@@ -107,7 +107,11 @@ typedef struct sw_timing {
 } sw_timing;
 /* A scan run as ONE merged longest-first launch (sw_last_kernel ends in
  * "+lpt": inter blocks and the long subjects' fp16 pass in one grid) reports
- * that launch as inter_ms and wave_ms and 0 as intra_ms. */
+ * that launch as inter_ms and wave_ms and 0 as intra_ms.
+ * In a batch (sw_scan_batch*), a query's rescue tail (re-scoring of flagged
+ * subjects) may run on a tail stream beside the next query's scan: its time
+ * is then outside that query's spans and inside a later query's total_ms;
+ * the batch's sum covers all of it. */
 
 typedef struct sw_handle sw_handle;
 typedef struct sw_db sw_db;
