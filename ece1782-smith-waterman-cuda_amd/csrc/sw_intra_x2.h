@@ -183,6 +183,19 @@ __host__ __device__ constexpr int img_elems() { return kCodes * IntraImg<RI, F16
 // the longest subjects' latency form for the merged launch, whose span one
 // long pair otherwise sets (chunks x steps on one wave; here ~steps + 128 per
 // extra chunk).
+// Staging of the chunk's bottom row (intra_x2_wg): kStage slots per wave
+// plus NB scratch slots every lane but 63 writes, 8 bytes each (H, F): one
+// LDS array per kernel, whichever forms of intra_x2_wg it instantiates.
+// (Stored by lane 63 at every step under an exec mask, with the column's
+// range test, the stores cost a lone wave ~16 scalar instructions per step:
+// the reference scoring's 1/8 share 10,986 -> 11,975 GCUPS, C5 8,045 ->
+// 8,177; 1 KB of LDS, so sw_intra_x2<16> still fits 3 workgroups per CU.)
+constexpr int kStage = 32;
+__device__ __forceinline__ uint2* bottom_stage() {
+    __shared__ uint2 slots[kWavesPerWG * kStage + 8];
+    return slots;
+}
+
 template <int RI, bool F16, bool LIST, bool LIN = false, bool TAKE = true, bool PIPE = false>
 __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typename IntraImg<RI, F16>::Elem* img) {
     static_assert(!(PIPE && LIST), "the pipelined form takes its pair by index");
@@ -300,6 +313,28 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
             for (int d = 0; d < PF; ++d) rcq[d] = 0;
 
             const int nblk = (nsteps + kLanes - 1) / kLanes;
+            // lane 63's bottom row (H, F) of each step goes to its wave's
+            // staging slots in LDS (step m: slot m % kStage); every other lane
+            // writes the scratch slots, so the per-step store needs no exec
+            // mask, no range test and no branch; every kStage steps the wave
+            // copies the slots to the boundary row with one coalesced store
+            using Slot = typename std::conditional<LIN, uint32_t, uint2>::type;
+            Slot* const stg = reinterpret_cast<Slot*>(bottom_stage()) + wave * kStage;
+            Slot* const scratch = reinterpret_cast<Slot*>(bottom_stage()) + kWavesPerWG * kStage;
+            auto flush = [&](int k0, int mbase) {  // slots of steps k0 + mbase ..
+                if (lane < kStage) {
+                    const int oc = k0 + mbase + lane - (kLanes - 1);
+                    if (oc >= 0 && oc < L) {
+                        const Slot v = stg[lane];
+                        if constexpr (LIN) {
+                            bnd_h[oc] = v;
+                        } else {
+                            bnd_h[oc] = v.x;
+                            bnd_f[oc] = v.y;
+                        }
+                    }
+                }
+            };
             auto block = [&](int bk) {
                 const int k0 = bk * kLanes;
                 // lane-0 conveyors for steps k0 .. k0+63 (column k = step); the
@@ -325,6 +360,7 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
                 // whole bias periods (steps past nsteps run pad columns: harmless)
                 const int mend = min(kLanes, nsteps - k0);
                 for (int m0 = 0; m0 < mend; m0 += NB) {
+                    Slot* const sp = is_last_lane ? stg + (m0 % kStage) : scratch;
 #pragma unroll
                     for (int b = 0; b < NB; ++b) {
                         const int m = m0 + b;
@@ -398,20 +434,16 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
                         }
                         hl = C::bits(H[RI - 1]);
                         if constexpr (!LIN) fl = C::bits(f);
-                        if (!last) {
-                            // lane 63 finished column k - 63: it stores it for the
-                            // next pass itself (no per-step collection across lanes)
-                            const int oc = k0 + m - (kLanes - 1);
-                            if (oc >= 0 && oc < L && is_last_lane) {
-                                bnd_h[oc] = hl;
-                                if constexpr (!LIN) bnd_f[oc] = fl;
-                            }
-                        }
+                        // lane 63 finished column k - 63 (staged, see flush)
+                        if constexpr (LIN) sp[b] = hl;
+                        else sp[b] = make_uint2(hl, fl);
                         // pin the maxima at every step (left free, the compiler
                         // defers the reductions and keeps every h alive)
 #pragma unroll
                         for (int q = 0; q < NACC; ++q) asm volatile("" : "+v"(acc[q]));
                     }
+                    if (!last && ((m0 + NB) % kStage == 0 || m0 + NB >= mend))
+                        flush(k0, (m0 + NB - 1) / kStage * kStage);
                 }
             };
             for_blocks(nblk, block);
