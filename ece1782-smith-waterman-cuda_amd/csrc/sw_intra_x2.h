@@ -261,7 +261,6 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
     V acc[NACC];
 #pragma unroll
     for (int q = 0; q < NACC; ++q) acc[q] = C::from(C::zero(a));
-    constexpr uint32_t kPadPair = kPadCode | (kPadCode << 8);
 
     // One chunk pass: rows [c0, c0 + CH) against the pair's columns, its
     // profile image in cimg; for_blocks(nblk, block) runs block(bk) for the
@@ -279,19 +278,24 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
             // at the previous column (row 0's diagonal): zeros of step -1
             uint32_t hl = C::step(a, RI + NB - 2), fl = C::step(a, RI + NB - 1);
             uint32_t up_prev = C::step(a, NB - 2);
-            uint32_t rc = kPadPair;        // codes (A | B << 8) of this lane's current column
+            // The code conveyor carries the LDS byte offsets of the two
+            // subjects' profile rows, A | B << 16 (code x the image's bytes per
+            // code, < 2^16): a row address is then one add of a 16-bit field
+            constexpr uint32_t kCodeBytes = NQ * kLanes * sizeof(Elem);
+            static_assert(kCodes * kCodeBytes <= 0x10000u, "16-bit row offsets");
+            constexpr uint32_t kPadPair = kPadCode * kCodeBytes | (kPadCode * kCodeBytes) << 16;
+            uint32_t rc = kPadPair;        // row offsets (A | B << 16) of this lane's current column
             uint32_t in_res = kPadPair, in_bh = 0, in_bf = 0;
             const int nsteps = L + kLanes - 1;
             // LDS byte address of this lane's element of code 0
             const uint32_t lrow = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(cimg + lane));
 
-            constexpr uint32_t kCodeBytes = NQ * kLanes * sizeof(Elem);
-            // the profile words of code pair rcx (A | B << 8) for this lane
+            // the profile words of row offsets rcx (A | B << 16) for this lane
             auto read_words = [&](uint32_t rcx, Elem (&wa)[NQ], Elem (&wb)[NQ]) {
                 typename Img::LElem* pa = reinterpret_cast<typename Img::LElem*>(
-                    static_cast<uintptr_t>(lrow + (rcx & 0xffu) * kCodeBytes));
+                    static_cast<uintptr_t>(lrow + (rcx & 0xffffu)));
                 typename Img::LElem* pb = reinterpret_cast<typename Img::LElem*>(
-                    static_cast<uintptr_t>(lrow + ((rcx >> 8) & 0xffu) * kCodeBytes));
+                    static_cast<uintptr_t>(lrow + (rcx >> 16)));
 #pragma unroll
                 for (int qq = 0; qq < NQ; ++qq) {
                     wa[qq] = __builtin_bit_cast(Elem, pa[qq * kLanes]);
@@ -301,9 +305,9 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
             auto codes_at = [&](int col) {
                 const uint32_t ca = col < LA ? resA[col] : kPadCode;
                 const uint32_t cb = col < LB ? resB[col] : kPadCode;
-                return ca | (cb << 8);
+                return ca * kCodeBytes | (cb * kCodeBytes) << 16;
             };
-            uint32_t in_res_nb = codes_at(lane);  // codes of the next block of 64 steps
+            uint32_t in_res_nb = codes_at(lane);  // row offsets of the next block of 64 steps
             // profile words, in NBUF buffers by step (NB is a multiple of NBUF,
             // so a bias period starts on buffer 0): step b reads W[b % NBUF]
             // and prefetches step b + PF's into another, no register copies
