@@ -418,7 +418,8 @@ class Database:
 
     def align(self, query_codes, ids, matrix=None, gap=2, gap_extend=None):
         """Traceback of the query against the subjects with these result ids
-        (sw_align: cpu.cpp's tie rules, linear gap).  Returns a list of dicts
+        (sw_align: cpu.cpp's tie rules for a linear gap; gap_extend != gap: the
+        affine extension of them, include/sw_amd.h).  Returns a list of dicts
         {score, q_begin, q_end, s_begin, s_end, ops} like the oracle's align."""
         q, qp = _u8(query_codes)
         idv = np.ascontiguousarray(ids, dtype=np.int32)

@@ -2448,7 +2448,6 @@ int sw_align(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen,
     const int8_t* mat;
     int go, ge, rc;
     if ((rc = check_scoring(sc, &mat, &go, &ge))) return rc;
-    if (go != ge) return fail(SW_E_UNSUPPORTED, "sw_align: traceback is implemented for linear gaps only");
     for (int32_t i = 0; i < qlen; ++i)
         if (query[i] >= SW_ALPHABET) return fail(SW_E_INVALID, "query residue code out of range (use sw_encode)");
     if (db->id_index.empty())
@@ -2507,7 +2506,8 @@ int sw_align(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen,
         alloc(&ddoff, m * sizeof(int64_t));
         alloc(&dmat, 625);
         alloc(&ddir, static_cast<size_t>(dacc));
-        alloc(&dh, static_cast<size_t>(m) * 3 * W1 * sizeof(int32_t));
+        // H: three diagonals; affine also two of E and two of F
+        alloc(&dh, static_cast<size_t>(m) * (go != ge ? 7 : 3) * W1 * sizeof(int32_t));
         alloc(&dout, static_cast<size_t>(m) * 6 * sizeof(int32_t));
         if (ops) alloc(&dops, static_cast<size_t>(m) * ops_stride);
         if (e == hipSuccess) e = hipMemcpyAsync(dq, query, qlen, hipMemcpyHostToDevice, h->stream);
@@ -2524,6 +2524,7 @@ int sw_align(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen,
             a.n = m;
             a.mat = dmat;
             a.gap = go;
+            a.gap_extend = ge;
             a.dirs = ddir;
             a.dirs_off = ddoff;
             a.hbuf = dh;

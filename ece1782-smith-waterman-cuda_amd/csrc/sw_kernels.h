@@ -281,7 +281,8 @@ hipError_t launch_intra_x2_list16(const IntraArgs& a, int ri, hipStream_t s);
 hipError_t launch_intra_x2_int16(const IntraArgs& a, int ri, hipStream_t s);
 int intra_x2_rows_for(int qlen, int longest);
 
-// Traceback of chosen hits (sw_align.hip), linear gap, cpu.cpp's tie rules.
+// Traceback of chosen hits (sw_align.hip): cpu.cpp's tie rules for a linear
+// gap (gap == gap_extend), this build's extension of them for affine gaps.
 struct AlignArgs {
     const uint8_t* query;
     int32_t qlen;
@@ -289,7 +290,8 @@ struct AlignArgs {
     const int64_t* subj_off;   // n+1 offsets
     int32_t n;
     const int8_t* mat;         // 25 x 25
-    int32_t gap;
+    int32_t gap;               // gap open (a 1-residue gap)
+    int32_t gap_extend;        // each further residue (== gap: linear)
     uint8_t* dirs;             // per hit: (qlen + slen + 1) x (qlen + 1) direction bytes
     const int64_t* dirs_off;   // per hit offset into dirs
     int32_t* hbuf;             // per hit: 3 x (qlen + 1) int32 diagonal scratch

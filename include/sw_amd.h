@@ -270,8 +270,13 @@ SW_API int sw_topk_device_ids(sw_handle* h, const int32_t* scores_dev, int64_t n
  * the query against that database subject under cpu.cpp's rules — a cell
  * takes left, then up, then diagonal only on a strict improvement over 0,
  * the first strict maximum in row-major order is the end cell, and the walk
- * back stops at a zero cell.  Linear gap only (gap_open == gap_extend;
- * otherwise SW_E_UNSUPPORTED).  Positions are 1-based and inclusive; ops
+ * back stops at a zero cell.  Affine gaps (gap_open != gap_extend) use
+ * this build's extension of those rules (the reference has no affine
+ * traceback): a gap run opens unless extending is STRICTLY better, H takes
+ * the run ending in the row (left), then the column (up), then the
+ * diagonal, and the walk follows a run back to its opening cell; with
+ * gap_open == gap_extend both give the same alignment.  Positions are
+ * 1-based and inclusive; ops
  * (optional, n x ops_stride bytes, not NUL-terminated) spells the path from
  * the begin cell: 'M' an aligned pair, 'I' a query residue against a gap,
  * 'D' a subject residue against a gap; ops_len is the full path length even

@@ -258,6 +258,83 @@ int swo_align_linear(const uint8_t* q, int qlen, const uint8_t* s, int slen,
     return best;
 }
 
+/* Affine traceback (Gotoh).  The reference has no affine path, so its tie
+ * order is this build's own, cpu.cpp's carried over: E(i,j) = H(i,j-1) - go
+ * unless extending, E(i,j-1) - ge, is STRICTLY better (the same for F down
+ * the column); H takes, in order, E (left), F (up), the diagonal, each only
+ * on a strict improvement over the running value that starts at 0; the end
+ * cell is the first strict maximum in row-major order; the walk back from H
+ * follows E / F runs to their opening cell and stops at a zero cell.  With
+ * go == ge every E / F is an opening and this is swo_align_linear exactly.
+ * Direction byte: bits 0-1 H's source (0 none, 1 E, 2 F, 3 diagonal), bit 2
+ * E extends, bit 3 F extends.  Parity unpinned against the reference (it
+ * prints no affine alignment): pinned to swo_score_affine and to the score
+ * of its own path. */
+int swo_align_affine(const uint8_t* q, int qlen, const uint8_t* s, int slen,
+                     const int8_t* mat, int go, int ge, int* q_end, int* s_end,
+                     int* q_begin, int* s_begin, char* ops, int ops_cap,
+                     int* ops_len) {
+    *q_end = *s_end = *q_begin = *s_begin = 0;
+    *ops_len = 0;
+    if (qlen <= 0 || slen <= 0) return 0;
+    const int NEG = -(1 << 29);
+    size_t W = (size_t)slen + 1;
+    size_t cells = ((size_t)qlen + 1) * W;
+    int* H = (int*)calloc(cells, sizeof(int));
+    int* E = (int*)malloc(cells * sizeof(int));
+    int* F = (int*)malloc(cells * sizeof(int));
+    unsigned char* T = (unsigned char*)calloc(cells, 1);
+    for (size_t k = 0; k < cells; ++k) E[k] = F[k] = NEG;
+    int best = 0, bi = 0, bj = 0;
+    for (int i = 1; i <= qlen; ++i) {
+        for (int j = 1; j <= slen; ++j) {
+            unsigned char t = 0;
+            int e = H[i * W + j - 1] - go;
+            if (E[i * W + j - 1] - ge > e) { e = E[i * W + j - 1] - ge; t |= 4; }
+            int f = H[(i - 1) * W + j] - go;
+            if (F[(i - 1) * W + j] - ge > f) { f = F[(i - 1) * W + j] - ge; t |= 8; }
+            int h = 0;
+            if (e > h) { h = e; t = (unsigned char)((t & 12) | 1); }
+            if (f > h) { h = f; t = (unsigned char)((t & 12) | 2); }
+            int d = H[(i - 1) * W + j - 1] + mat[25 * q[i - 1] + s[j - 1]];
+            if (d > h) { h = d; t = (unsigned char)((t & 12) | 3); }
+            if (h > best) { best = h; bi = i; bj = j; }
+            H[i * W + j] = h;
+            E[i * W + j] = e;
+            F[i * W + j] = f;
+            T[i * W + j] = t;
+        }
+    }
+    int i = bi, j = bj, n = 0, state = 0; /* 0: H, 1: in an E run, 2: in an F run */
+    while (i > 0 && j > 0) {
+        unsigned char t = T[i * W + j];
+        char op;
+        if (state == 0) {
+            int src = t & 3;
+            if (src == 0 || H[i * W + j] == 0) break;
+            if (src == 3) { op = 'M'; --i; --j; }
+            else { state = src; continue; }
+        } else if (state == 1) {
+            op = 'D';
+            state = (t & 4) ? 1 : 0;
+            --j;
+        } else {
+            op = 'I';
+            state = (t & 8) ? 2 : 0;
+            --i;
+        }
+        if (n < ops_cap) ops[n] = op;
+        ++n;
+    }
+    int m = n < ops_cap ? n : ops_cap;
+    for (int k = 0; k < m / 2; ++k) { char c = ops[k]; ops[k] = ops[m - 1 - k]; ops[m - 1 - k] = c; }
+    *ops_len = n;
+    *q_end = bi; *s_end = bj;
+    *q_begin = i + 1; *s_begin = j + 1;
+    free(H); free(E); free(F); free(T);
+    return best;
+}
+
 /* ------------------------------------------------------------------ */
 /* Threaded whole-database scan (the CPU baseline).                      */
 /* ------------------------------------------------------------------ */

@@ -77,6 +77,14 @@ int swo_align_linear(const uint8_t* q, int qlen, const uint8_t* s, int slen,
                      int* q_begin, int* s_begin, char* ops, int ops_cap,
                      int* ops_len);
 
+/* The same under affine gaps (Gotoh, a k-gap costs go + (k-1) ge), with the
+ * tie order described at its definition (this build's own: the reference
+ * has no affine traceback).  go == ge gives swo_align_linear's result.   */
+int swo_align_affine(const uint8_t* q, int qlen, const uint8_t* s, int slen,
+                     const int8_t* mat, int go, int ge, int* q_end, int* s_end,
+                     int* q_begin, int* s_begin, char* ops, int ops_cap,
+                     int* ops_len);
+
 #ifdef __cplusplus
 }
 #endif

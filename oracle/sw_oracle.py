@@ -58,6 +58,11 @@ def lib():
                                        ctypes.POINTER(ctypes.c_int8), ctypes.c_int] + \
             [ctypes.POINTER(ctypes.c_int)] * 4 + [ctypes.c_char_p, ctypes.c_int,
                                                   ctypes.POINTER(ctypes.c_int)]
+        L.swo_align_affine.restype = ctypes.c_int
+        L.swo_align_affine.argtypes = [u8p, ctypes.c_int, u8p, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_int8), ctypes.c_int, ctypes.c_int] + \
+            [ctypes.POINTER(ctypes.c_int)] * 4 + [ctypes.c_char_p, ctypes.c_int,
+                                                  ctypes.POINTER(ctypes.c_int)]
         _LIB = L
     return _LIB
 
@@ -196,8 +201,10 @@ def scan(q, residues, offsets, mat=None, gap_open=2, gap_extend=2, nthreads=0):
     return out
 
 
-def align(q, s, mat=None, gap=2):
-    """Score + traceback under cpu.cpp's tie rules. Returns dict."""
+def align(q, s, mat=None, gap=2, gap_extend=None):
+    """Score + traceback under cpu.cpp's tie rules (oracle/sw_oracle.c
+    swo_align_linear, cpu.cpp:47-108); with gap_extend != gap the affine
+    traceback swo_align_affine (this build's tie order).  Returns dict."""
     mat = matrix() if mat is None else mat
     q, qp = _u8(q)
     s, sp = _u8(s)
@@ -205,9 +212,12 @@ def align(q, s, mat=None, gap=2):
     ints = [ctypes.c_int() for _ in range(5)]
     cap = len(q) + len(s) + 1
     buf = ctypes.create_string_buffer(cap)
-    best = lib().swo_align_linear(qp, len(q), sp, len(s), mp, gap,
-                                  *[ctypes.byref(x) for x in ints[:4]], buf, cap,
-                                  ctypes.byref(ints[4]))
+    refs = [ctypes.byref(x) for x in ints[:4]]
+    if gap_extend is None or gap_extend == gap:
+        best = lib().swo_align_linear(qp, len(q), sp, len(s), mp, gap, *refs, buf, cap, ctypes.byref(ints[4]))
+    else:
+        best = lib().swo_align_affine(qp, len(q), sp, len(s), mp, gap, gap_extend, *refs, buf, cap,
+                                      ctypes.byref(ints[4]))
     return {"score": best, "q_end": ints[0].value, "s_end": ints[1].value,
             "q_begin": ints[2].value, "s_begin": ints[3].value,
             "ops": buf.raw[: ints[4].value].decode()}

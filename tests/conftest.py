@@ -42,3 +42,25 @@ def read_query(name):
 def read_golden(name):
     with open(os.path.join(GOLDEN, name)) as f:
         return [int(x) for x in f.read().split()]
+
+
+def path_score(q, s, mat, go, ge, al):
+    """Score of an alignment's path (ops from (q_begin, s_begin)) under a gap
+    of go for its first residue and ge for each further one: equal to the
+    reported score whatever the tie rules, so it checks a traceback without
+    trusting them."""
+    i, j, sc, prev = al["q_begin"] - 1, al["s_begin"] - 1, 0, None
+    for op in al["ops"]:
+        if op == "M":
+            sc += int(mat[q[i]][s[j]])
+            i += 1
+            j += 1
+        else:
+            sc -= ge if prev == op else go
+            if op == "I":
+                i += 1
+            else:
+                j += 1
+        prev = op
+    assert (i, j) == (al["q_end"], al["s_end"]), "the path ends at the end cell"
+    return sc

@@ -4,7 +4,7 @@ import json
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, read_golden, read_query
+from conftest import GOLDEN, path_score, read_golden, read_query
 
 
 def subset(oracle):
@@ -90,6 +90,45 @@ def test_affine_reduces_to_linear(oracle):
         s = rng.integers(0, 25, size=rng.integers(1, 60)).astype(np.uint8)
         for g in (1, 2, 5):
             assert oracle.score(q, s, m, g, g) == oracle.score(q, s, m, g, g, force_affine=True)
+
+
+def test_affine_traceback(oracle):
+    """The affine traceback (swo_align_affine, this build's tie order): its
+    score is Gotoh's (swo_score_affine), its path scores exactly that under
+    open / extend, and with open == extend it is the linear traceback of
+    cpu.cpp's rules, alignment for alignment."""
+    rng = np.random.default_rng(8)
+    m = oracle.matrix(oracle.MATRIX_BLOSUM62)
+    for _ in range(40):
+        q = rng.integers(0, 25, size=rng.integers(1, 80)).astype(np.uint8)
+        s = rng.integers(0, 25, size=rng.integers(1, 80)).astype(np.uint8)
+        if rng.random() < 0.5:  # a planted copy with indels: long gaps worth opening
+            s = np.concatenate([s[:10], q[5:30], s[10:14], q[34:60]]).astype(np.uint8)
+        for go, ge in ((12, 1), (11, 2), (5, 5)):
+            al = oracle.align(q, s, m, go, ge)
+            assert al["score"] == oracle.score(q, s, m, go, ge)
+            if al["score"] > 0:
+                assert path_score(q, s, m, go, ge, al) == al["score"]
+                assert al["ops"][0] == "M" and al["ops"][-1] == "M"
+        for g in (1, 2, 5):
+            # force the affine routine with open == extend through the C entry
+            assert oracle.align(q, s, m, g, g) == _affine_equal(oracle, q, s, m, g)
+
+
+def _affine_equal(oracle, q, s, m, g):
+    import ctypes
+    q8 = np.ascontiguousarray(q, dtype=np.uint8)
+    s8 = np.ascontiguousarray(s, dtype=np.uint8)
+    mm = np.ascontiguousarray(m, dtype=np.int8)
+    ints = [ctypes.c_int() for _ in range(5)]
+    cap = len(q) + len(s) + 1
+    buf = ctypes.create_string_buffer(cap)
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    best = oracle.lib().swo_align_affine(q8.ctypes.data_as(u8p), len(q8), s8.ctypes.data_as(u8p), len(s8),
+                                         mm.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)), g, g,
+                                         *[ctypes.byref(x) for x in ints[:4]], buf, cap, ctypes.byref(ints[4]))
+    return {"score": best, "q_end": ints[0].value, "s_end": ints[1].value,
+            "q_begin": ints[2].value, "s_begin": ints[3].value, "ops": buf.raw[: ints[4].value].decode()}
 
 
 def test_matrices(oracle):
