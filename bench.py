@@ -96,7 +96,7 @@ VALU_MODEL = {
 # cycles of conveyor work (3 DPP moves, 3 readlanes, 2 hand-off adjusts, the
 # profile addresses, lane 63's boundary store; hipcc -S of sw_intra_x2.hip;
 # SQ_INSTS_VALU on C5 at RI = 16: 130 per lane-step, profiles/r02_sq/)
-for _ri in (4, 8, 12, 16):
+for _ri in (4, 6, 8, 10, 12, 16, 20):
     VALU_MODEL["sw_intra_x2<%d>" % _ri] = (_ri * (6.78 * 4.25) + 80.0) / (128 * _ri)
 MATRICES = {"blosum50": 0, "blosum62": 1}
 SEED = 1782

@@ -1210,7 +1210,11 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // (SW_INTRA_X2=0: int32 only).
     const char* ix = std::getenv("SW_INTRA_X2");
     const bool intra_x2 = db->nlong && x2_ok >= 1 && !(ix && ix[0] == '0');
-    const int ri2 = intra_x2 ? swk::intra_x2_rows_for(qlen, db->long_max) : 0;
+    // (20 rows per lane only where no merged launch can take the scan: no
+    // inter blocks; where the fp16 bias of row 19 fits, as f16_fits; and by
+    // the cost model for affine gaps only, see intra_x2_rows_for)
+    const bool ri2_wide = db->nblocks == 0 && 2 * max_s + (swk::intra_bias_rows(swk::kIntraX2MaxRI) + 1) * ge + go < 1024;
+    const int ri2 = intra_x2 ? swk::intra_x2_rows_for(qlen, db->long_max, ri2_wide ? (affine ? 2 : 1) : 0) : 0;
     // The intra chain's order.  Linear scoring with cheap gaps makes random
     // pairs' scores grow with their lengths, so on long subjects the fp16
     // pass can flag many of them and its time on those is wasted.  Once a
@@ -1513,7 +1517,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         // offset by zero = -2048 + 2 ge as the inter cell's (the lowest value
         // an addition reads is a rebased row -1 H of bias -2 ge: exact)
         const int zero = -kF16Span + 2 * ge;
-        x.sat_limit = kF16Span - zero - 2 * std::max(max_s, 1) - 26 * ge;
+        x.sat_limit = kF16Span - zero - 2 * std::max(max_s, 1) - swk::intra_bias_rows(ri2) * ge;
         for (int j = 0; j < 32; ++j) x.f16_step[j] = f16_pair(j * ge + zero);
         x.f16_zero = f16_pair(zero);
         x.f16_gog = f16_pair(go - ge);

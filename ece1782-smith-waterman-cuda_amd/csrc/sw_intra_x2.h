@@ -58,8 +58,8 @@ __device__ __forceinline__ uint32_t shr1u(uint32_t old, uint32_t src) {
 constexpr int kCodes = kPadCode + 1;  // residue codes 0..24 and the pad code
 
 // fp16 pair of two int16 profile entries minus `b`
-__device__ __forceinline__ uint32_t f16x2_of(uint32_t w, int b) {
-    return f16_bits(static_cast<int16_t>(w & 0xffffu) - b) | (f16_bits(static_cast<int16_t>(w >> 16) - b) << 16);
+__device__ __forceinline__ uint32_t f16x2_of(uint32_t w, int b0, int b1) {
+    return f16_bits(static_cast<int16_t>(w & 0xffffu) - b0) | (f16_bits(static_cast<int16_t>(w >> 16) - b1) << 16);
 }
 
 typedef short s2 __attribute__((ext_vector_type(2)));
@@ -86,9 +86,10 @@ struct IntraCell {
         return static_cast<int>(static_cast<float>(__builtin_bit_cast(h2, a.f16_zero).x));
     }
     static __device__ __forceinline__ uint32_t pair_of(int v) { const uint32_t b = f16_bits(v); return b | (b << 16); }
-    static __device__ __forceinline__ uint32_t convert(uint32_t w, int b) { return f16x2_of(w, b); }
+    static __device__ __forceinline__ uint32_t convert(uint32_t w, int b0, int b1) { return f16x2_of(w, b0, b1); }
     static __device__ __forceinline__ int lo(V x) { return static_cast<int>(static_cast<float>(x.x)); }
     static __device__ __forceinline__ int hi(V x) { return static_cast<int>(static_cast<float>(x.y)); }
+    template <int RI>
     static __device__ __forceinline__ bool flag(const IntraArgs& a, int b) { return b >= a.sat_limit; }
 };
 template <>
@@ -106,15 +107,17 @@ struct IntraCell<false> {
         const uint32_t b = static_cast<uint16_t>(v);
         return b | (b << 16);
     }
-    static __device__ __forceinline__ uint32_t convert(uint32_t w, int b) {
-        return static_cast<uint16_t>(static_cast<int16_t>(w & 0xffffu) - b) |
-               (static_cast<uint32_t>(static_cast<uint16_t>(static_cast<int16_t>(w >> 16) - b)) << 16);
+    static __device__ __forceinline__ uint32_t convert(uint32_t w, int b0, int b1) {
+        return static_cast<uint16_t>(static_cast<int16_t>(w & 0xffffu) - b0) |
+               (static_cast<uint32_t>(static_cast<uint16_t>(static_cast<int16_t>(w >> 16) - b1)) << 16);
     }
     static __device__ __forceinline__ int lo(V x) { return x.x; }
     static __device__ __forceinline__ int hi(V x) { return x.y; }
-    // the int16 guard band (the biased values sit up to 26 ge above the true)
+    // the int16 guard band (the biased values sit up to max(26, RI + 10) ge
+    // above the true ones)
+    template <int RI>
     static __device__ __forceinline__ bool flag(const IntraArgs& a, int b) {
-        return b >= kSat16 - 26 * a.gap_extend || b < 0;
+        return b >= kSat16 - intra_bias_rows(RI) * a.gap_extend || b < 0;
     }
 };
 
@@ -133,14 +136,15 @@ struct IntraImg {
         else return w[r >> 1];
     }
     // staging: the element of rows [4q, 4q + 4) or [2q, 2q + 2) of a lane
-    static __device__ __forceinline__ Elem load(const int16_t* p, int b) {
+    // (b0: the first row's drop, b the others')
+    static __device__ __forceinline__ Elem load(const int16_t* p, int b0, int b) {
         using C = IntraCell<F16>;
         if constexpr (kRows == 4) {
             const int2 v = *reinterpret_cast<const int2*>(p);
-            return make_int2(static_cast<int>(C::convert(static_cast<uint32_t>(v.x), b)),
-                             static_cast<int>(C::convert(static_cast<uint32_t>(v.y), b)));
+            return make_int2(static_cast<int>(C::convert(static_cast<uint32_t>(v.x), b0, b)),
+                             static_cast<int>(C::convert(static_cast<uint32_t>(v.y), b, b)));
         } else {
-            return C::convert(*reinterpret_cast<const uint32_t*>(p), b);
+            return C::convert(*reinterpret_cast<const uint32_t*>(p), b0, b);
         }
     }
 };
@@ -196,10 +200,24 @@ __device__ __forceinline__ uint2* bottom_stage() {
     return slots;
 }
 
-template <int RI, bool F16, bool LIST, bool LIN = false, bool TAKE = true, bool PIPE = false>
+// CONV: lane 0's conveyor inputs of each step (the boundary row's H and F,
+// the code row offsets) come from LDS, one broadcast ds_read_b32 each,
+// instead of a v_readlane of the block's register and a v_mov of it back to
+// a VGPR for the DPP shift (6 VALU per step): per wave 256 words, [H 64][F
+// 64][codes of this block 64][of the next 64], written at each 64-step
+// block's start.
+constexpr int kConvWords = 256;
+__device__ __forceinline__ uint32_t* conv_area() {
+    __shared__ uint32_t w[kWavesPerWG * kConvWords];
+    return w;
+}
+
+template <int RI, bool F16, bool LIST, bool LIN = false, bool TAKE = true, bool PIPE = false,
+          bool CONV = false>
 __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typename IntraImg<RI, F16>::Elem* img) {
     static_assert(!(PIPE && LIST), "the pipelined form takes its pair by index");
-    static_assert(RI % 2 == 0 && RI <= 16, "rows per lane");
+    static_assert(!CONV || kPrefetch, "the LDS conveyor serves the prefetching step");
+    static_assert(RI % 2 == 0 && RI <= kIntraX2MaxRI, "rows per lane");
     constexpr int CH = kLanes * RI;  // query rows per chunk
     using C = IntraCell<F16>;
     using V = typename C::V;
@@ -277,12 +295,14 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
             // bottom row (H, F) of this lane one step back, and H of the row above
             // at the previous column (row 0's diagonal): zeros of step -1
             uint32_t hl = C::step(a, RI + NB - 2), fl = C::step(a, RI + NB - 1);
-            uint32_t up_prev = C::step(a, NB - 2);
+            // (affine: up_prev is held (RI - 1) ge high, the drop the row-0
+            // profile words carry instead, see the hand-off below)
+            uint32_t up_prev = C::step(a, LIN ? NB - 2 : NB - 2 + RI - 1);
             // The code conveyor carries the LDS byte offsets of the two
             // subjects' profile rows, A | B << 16 (code x the image's bytes per
             // code, < 2^16): a row address is then one add of a 16-bit field
             constexpr uint32_t kCodeBytes = NQ * kLanes * sizeof(Elem);
-            static_assert(kCodes * kCodeBytes <= 0x10000u, "16-bit row offsets");
+            static_assert((kCodes - 1) * kCodeBytes < 0x10000u, "16-bit row offsets");
             constexpr uint32_t kPadPair = kPadCode * kCodeBytes | (kPadCode * kCodeBytes) << 16;
             uint32_t rc = kPadPair;        // row offsets (A | B << 16) of this lane's current column
             uint32_t in_res = kPadPair, in_bh = 0, in_bf = 0;
@@ -325,6 +345,7 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
             using Slot = typename std::conditional<LIN, uint32_t, uint2>::type;
             Slot* const stg = reinterpret_cast<Slot*>(bottom_stage()) + wave * kStage;
             Slot* const scratch = reinterpret_cast<Slot*>(bottom_stage()) + kWavesPerWG * kStage;
+            uint32_t* const cv = CONV ? conv_area() + wave * kConvWords : nullptr;
             auto flush = [&](int k0, int mbase) {  // slots of steps k0 + mbase ..
                 if (lane < kStage) {
                     const int oc = k0 + mbase + lane - (kLanes - 1);
@@ -353,6 +374,12 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
                     // into the argument table would copy the table to registers
                     in_bh = (!first && col < L) ? bnd_h[col] : C::pair_of(bz * a.gap_extend + C::zero_int(a));
                     in_bf = (!first && col < L) ? bnd_f[col] : C::pair_of((bz + 1) * a.gap_extend + C::zero_int(a));
+                    if constexpr (CONV) {  // (the previous block's reads are done: one wave, in order)
+                        cv[lane] = in_bh;
+                        if constexpr (!LIN) cv[kLanes + lane] = in_bf;
+                        cv[2 * kLanes + lane] = in_res;
+                        cv[3 * kLanes + lane] = in_res_nb;
+                    }
                 }
                 if (kPrefetch && k0 == 0) {
 #pragma unroll
@@ -368,8 +395,8 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
 #pragma unroll
                     for (int b = 0; b < NB; ++b) {
                         const int m = m0 + b;
-                        const uint32_t sbh = __builtin_amdgcn_readlane(in_bh, m);
-                        const uint32_t sbf = LIN ? 0u : __builtin_amdgcn_readlane(in_bf, m);
+                        const uint32_t sbh = CONV ? cv[m] : __builtin_amdgcn_readlane(in_bh, m);
+                        const uint32_t sbf = LIN ? 0u : CONV ? cv[kLanes + m] : __builtin_amdgcn_readlane(in_bf, m);
                         static_assert(NB % NBUF == 0, "buffer period");
                         Elem(&wa)[NQ] = W[b % NBUF][0];
                         Elem(&wb)[NQ] = W[b % NBUF][1];
@@ -381,8 +408,9 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
                             // (the next block's first ones at the block's last steps)
                             const bool wrap = (b + PF >= NB) && (m0 + NB == kLanes);
                             const uint32_t sres_n =
-                                wrap ? __builtin_amdgcn_readlane(in_res_nb, (b + PF - NB) & (kLanes - 1))
-                                     : __builtin_amdgcn_readlane(in_res, (m + PF) & (kLanes - 1));
+                                CONV ? cv[2 * kLanes + m + PF]
+                                : wrap ? __builtin_amdgcn_readlane(in_res_nb, (b + PF - NB) & (kLanes - 1))
+                                       : __builtin_amdgcn_readlane(in_res, (m + PF) & (kLanes - 1));
                             rcq[PF - 1] = shr1u(sres_n, PF > 1 ? rcq[PF > 1 ? PF - 2 : 0] : rc);
                             read_words(rcq[PF - 1], W[(b + PF) % NBUF][0], W[(b + PF) % NBUF][1]);
                         } else {
@@ -391,7 +419,14 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
                         }
                         // hand-off: the row above's bottom (H, F) from one step back
                         const V adj = diff(RI - 1 + (b == 0 ? NB : 0));
-                        const uint32_t up0 = C::bits(C::from(shr1u(sbh, hl)) - adj);
+                        // affine: the row above's H is only row 0's next
+                        // diagonal, so its (RI - 1) ge drop rides in the row-0
+                        // profile words (staged with it) and only a rebase
+                        // step's NB ge is subtracted here
+                        const uint32_t up_raw = shr1u(sbh, hl);
+                        const uint32_t up0 = LIN ? C::bits(C::from(up_raw) - adj)
+                                                 : b == 0 ? C::bits(C::from(up_raw) - diff(NB))
+                                                          : up_raw;
                         V f = LIN ? C::from(0u) : C::from(shr1u(sbf, fl)) - adj;
                         if (b == 0) {  // rebase: the bias period restarts
                             const V reb = diff(NB);
@@ -460,8 +495,9 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
             const int code = t / (NQ * kLanes);
             const int u = t % (NQ * kLanes);
             const int qq = u / kLanes, ln = u % kLanes;
+            const int b = a.bias - 2 * a.gap_extend;
             im[t] = Img::load(prof16 + static_cast<size_t>(code) * a.prof_stride + c0 + ln * RI + Img::kRows * qq,
-                              a.bias - 2 * a.gap_extend);
+                              (!LIN && qq == 0) ? b + (RI - 1) * a.gap_extend : b, b);
         }
     };
     const int nch = (a.qpad + CH - 1) / CH;
@@ -539,14 +575,14 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
         const int bb = C::hi(best) - C::zero_int(a);
         if (hasA) {
             a.scores[a.subj_id[sa]] = ba;
-            if (a.rescue_list && C::flag(a, ba)) {
+            if (a.rescue_list && C::template flag<RI>(a, ba)) {
                 list_publish(a.rescue_list, a.rescue_count, sa);
                 flagged = true;
             }
         }
         if (hasB) {
             a.scores[a.subj_id[sb]] = bb;
-            if (a.rescue_list && C::flag(a, bb)) {
+            if (a.rescue_list && C::template flag<RI>(a, bb)) {
                 list_publish(a.rescue_list, a.rescue_count, sb);
                 flagged = true;
             }

@@ -5,23 +5,33 @@
 
 #include <cstdlib>
 
+#ifndef SW_IX2_CONV
+#define SW_IX2_CONV 1
+#endif
+
 namespace swk {
 
+// The LDS conveyor (ix2 CONV: 1 KB per wave) wherever it leaves the
+// occupancy as it is: every shape but RI 16, whose 53 KB image leaves no room
+// for it at 3 workgroups per CU.
 template <int RI, bool F16, bool LIST, bool LIN>
-__global__ __launch_bounds__(256) void sw_intra_x2(IntraArgs a) {
+__global__ __launch_bounds__(kWavesPerWG * kLanes) void sw_intra_x2(IntraArgs a) {
     __shared__ typename ix2::IntraImg<RI, F16>::Elem img[ix2::img_elems<RI, F16>()];
-    ix2::intra_x2_wg<RI, F16, LIST, LIN>(a, blockIdx.x, img);
+    constexpr bool kConv = SW_IX2_CONV && RI != 16;
+    ix2::intra_x2_wg<RI, F16, LIST, LIN, true, false, kConv>(a, blockIdx.x, img);
 }
 
-int intra_x2_rows_for(int qlen, int longest) {
+int intra_x2_rows_for(int qlen, int longest, int wide) {
     // chunks x steps x (cell pairs per lane-step + conveyor/hand-off overhead)
     if (const char* e = std::getenv("SW_INTRA_X2_RI")) {  // tests: force a shape
         const int ri = std::atoi(e);
         if (ri == 4 || ri == 6 || ri == 8 || ri == 10 || ri == 12 || ri == 16) return ri;
+        if (ri == kIntraX2MaxRI && wide >= 1) return ri;
     }
     int best_ri = 16;
     double best_cost = 1e300;
-    for (int ri : {4, 6, 8, 10, 12, 16}) {
+    for (int ri : {4, 6, 8, 10, 12, 16, kIntraX2MaxRI}) {
+        if (ri == kIntraX2MaxRI && wide < 2) continue;
         const int chunk = kLanes * ri;
         const int nch = (qlen + chunk - 1) / chunk;
         // SIMD cycles per lane-step: ri rows x 6.8 ops x 4.25 + ~80 of conveyor
@@ -45,6 +55,7 @@ static hipError_t launch_intra_x2_t(const IntraArgs& a, int ri, hipStream_t s) {
         case 10: hipLaunchKernelGGL((sw_intra_x2<10, F16, LIST, LIN>), grid, block, 0, s, a); break;
         case 12: hipLaunchKernelGGL((sw_intra_x2<12, F16, LIST, LIN>), grid, block, 0, s, a); break;
         case 16: hipLaunchKernelGGL((sw_intra_x2<16, F16, LIST, LIN>), grid, block, 0, s, a); break;
+        case kIntraX2MaxRI: hipLaunchKernelGGL((sw_intra_x2<kIntraX2MaxRI, F16, LIST, LIN>), grid, block, 0, s, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -265,6 +265,16 @@ hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_
 bool inter_has_pair(bool affine, int x2_ok);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.
 constexpr int kSat16 = 32767 - 1152;
+// The two-subjects intra kernel's biased cell stores values up to this many
+// gap extensions above the true ones at RI rows per lane (row RI - 1 at the
+// last step of a bias period, + 2 ge in the profile, + the F floor's step).
+constexpr int intra_bias_rows(int ri) { return ri + 10 > 26 ? ri + 10 : 26; }
+// Its widest shape: 20 rows per lane, in the same 4-wave workgroups: the
+// 26-code image of 1,280 rows (66.5 KB) leaves two workgroups per CU, 2
+// waves per SIMD.  (Measured on C5: 6-wave workgroups did not fit two per CU,
+// 2 + 2 + 1 + 1 waves per SIMD each: 5,550 GCUPS; 12-wave ones, one per CU,
+// left whole CUs idle in the last round: 7,475; 4-wave: 8,892.)
+constexpr int kIntraX2MaxRI = 20;
 // true if the chosen inter kernel may flag blocks for int32 re-scoring
 // (16-bit kernels beyond the static int16 bound).
 bool inter_needs_rescue(bool affine, int x2_ok);
@@ -273,13 +283,19 @@ bool inter_needs_rescue(bool affine, int x2_ok);
 int rescue_rows(bool affine);
 hipError_t launch_inter_rescue(const InterArgs& a, bool affine, hipStream_t s);
 hipError_t launch_intra(const IntraArgs& a, int ri, bool affine, hipStream_t s);
-// Two subjects per wave, packed fp16 (sw_intra_x2.hip); rows per lane 4..16.
+// Two subjects per wave, packed fp16 (sw_intra_x2.hip); rows per lane 4..16,
+// and 20 when intra_x2_rows_for allows it.
 hipError_t launch_intra_x2(const IntraArgs& a, int ri, hipStream_t s);
 // its int16 form over the device-side list a.subj_list / a.list_count
 hipError_t launch_intra_x2_list16(const IntraArgs& a, int ri, hipStream_t s);
 // ... and over every subject (the chain's first stage when fp16 would flag most)
 hipError_t launch_intra_x2_int16(const IntraArgs& a, int ri, hipStream_t s);
-int intra_x2_rows_for(int qlen, int longest);
+// wide: 0 = rows per lane 4..16; 1 = 20 too when a test forces it
+// (SW_INTRA_X2_RI); 2 = 20 by the cost model too.  The host allows 20 only
+// where no merged launch can take the scan (no inter blocks) and the fp16
+// bias of row 19 fits, and picks it only for affine gaps (the linear cell
+// lost 35 % at 20 on C5: its cheaper steps need the third wave per SIMD).
+int intra_x2_rows_for(int qlen, int longest, int wide = 0);
 
 // Traceback of chosen hits (sw_align.hip): cpu.cpp's tie rules for a linear
 // gap (gap == gap_extend), this build's extension of them for affine gaps.

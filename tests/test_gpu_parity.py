@@ -462,12 +462,14 @@ def test_wave_pair_kernel(sw, oracle, handle, monkeypatch, variant, width, group
             assert want.max() > 4096  # the fp16 guard band is crossed
 
 
-@pytest.mark.parametrize("packed,ri", [("1", ""), ("1", "6"), ("1", "10"), ("0", "")])
+@pytest.mark.parametrize("packed,ri", [("1", ""), ("1", "6"), ("1", "10"), ("1", "20"), ("0", "")])
 def test_intra_two_subjects_per_wave(sw, oracle, handle, monkeypatch, packed, ri):
     """sw_intra_x2 (two long subjects per wave, packed fp16; SW_INTRA_X2=0:
-    int32 sw_intra only): rows per lane 4..16 by the cost model (query lengths
+    int32 sw_intra only): rows per lane 4..20 by the cost model (query lengths
     40..2100, one to several chunk passes) or forced to the 2-row-element
-    shapes 6 and 10, an odd number of long subjects, pairs of unequal length,
+    shapes 6 and 10 and to the widest, 20 rows by 6-wave workgroups (this
+    database has no inter blocks, so no merged launch can take the scan), an
+    odd number of long subjects, pairs of unequal length,
     linear and affine scoring, and planted near-copies of the query whose fp16
     maxima cross the fp16 bound (~4,000: cells offset by -2048 + 2 ge;
     re-scored by sw_intra in list mode)."""
@@ -490,6 +492,8 @@ def test_intra_two_subjects_per_wave(sw, oracle, handle, monkeypatch, packed, ri
         got = db.scan(q, m, go, ge)
         want = oracle.scan(q, r, o, mat=m, gap_open=go, gap_extend=ge)
         assert np.array_equal(got, want), (qlen, mid, go, ge, np.nonzero(got != want)[0][:10])
+        if packed == "1" and ri:
+            assert handle.last_intra_kernel().startswith("sw_intra_x2<%s" % ri), handle.last_intra_kernel()
         if qlen >= 1500:
             assert want.max() > 4096
 
