@@ -1006,6 +1006,16 @@ __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_inter_x2p(InterArgs 
 // The drain's shapes: the int16 list form of the two-strips kernel (affine
 // 32x8 with 64-row passes, linear 48x4 with 96-row passes) and the int32
 // inter kernel (affine 32x8, linear 64x8), as the separate rescue launches.
+// The intra forms of the merged launch read lane 0's conveyor inputs from
+// LDS under affine gaps (ix2 CONV, 4 KB beside the launch's 57 KB; C2's 1/8
+// share +0.6 %; the linear steps, shorter, lost 0.4 % with it and keep the
+// readlane form: profiles/r04_ab_lptconv/; SW_LPT_CONV=0: readlane
+// everywhere, for A/B builds)
+#ifndef SW_LPT_CONV
+#define SW_LPT_CONV 1
+#endif
+constexpr bool kLptConv = SW_LPT_CONV != 0;
+
 template <bool AFFINE>
 struct DrainShape {
     static constexpr int R16 = AFFINE ? 32 : 48, SG16 = AFFINE ? 8 : 4;
@@ -1103,10 +1113,11 @@ __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(InterArgs a
     if (item >= 0)
         flagged = x2p_wg<R, SG, AFFINE, true, true, 4>(a, item, a.blk_quad, *reinterpret_cast<X2pSmem<R, SG, 4>*>(smem));
     else if (-1 - item < niwg)
-        flagged = ix2::intra_x2_wg<RI, true, false, !AFFINE>(ia, -1 - item, reinterpret_cast<Elem*>(smem));
+        flagged = ix2::intra_x2_wg<RI, true, false, !AFFINE, true, false, kLptConv && AFFINE>(ia, -1 - item,
+                                                                                 reinterpret_cast<Elem*>(smem));
     else
-        flagged = ix2::intra_x2_wg<2, true, false, !AFFINE, true, true>(ia, -1 - item - niwg,
-                                                                       reinterpret_cast<PElem*>(smem));
+        flagged = ix2::intra_x2_wg<2, true, false, !AFFINE, true, true, kLptConv && AFFINE>(ia, -1 - item - niwg,
+                                                                                 reinterpret_cast<PElem*>(smem));
     // Only a workgroup that appended an entry drains (and takes whatever is
     // listed, its own entries included): every entry is then taken by its
     // producer at the latest, and the rest of the grid pays one barrier.
