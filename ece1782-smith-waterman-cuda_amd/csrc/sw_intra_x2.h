@@ -24,9 +24,12 @@
 // free whatever code each lane reads.  The waves stage each chunk together
 // and meet at one barrier per chunk (their subjects have near-equal lengths).
 //
-// Exactness: fp16 holds every integer up to 2048.  H grows by at most max S
-// per cell, so a subject whose running maximum reaches a.sat_limit =
-// 2048 − 2·max S − 26·ge (computed exactly) is appended to a.rescue_list.
+// Exactness: fp16 holds every integer up to 2048 (the cells are offset by
+// -2048 + 2 ge, so stored values span 4096).  H grows by at most max S per
+// cell and the biased values sit up to intra_bias_rows(RI) = max(26, RI + 10)
+// ge above the true ones, so a subject whose running maximum reaches
+// a.sat_limit = 4096 − 2 ge − 2·max S − intra_bias_rows(RI)·ge (computed
+// exactly) is appended to a.rescue_list.
 // The same kernel in int16 (IntraCell<false>, LIST) re-scores that list and
 // appends subjects near 32767 to a second list for the int32 sw_intra; when
 // the fp16 pass would flag most subjects (cheap linear gaps on long pairs)
