@@ -990,11 +990,17 @@ double intra_step_us(int ri) { return 2 * 0.157 * (ri * 28.8 + 80.0) / (6 * 28.8
 
 // The widest group blocks of the merged launch run by quads: those at least
 // kQuadFrac x the long threshold wide, whose pair latency would otherwise
-// exceed the long subjects' (SW_QUAD_WIDTH=w: at least w columns; 0: none).
+// exceed the long subjects' (SW_QUAD_WIDTH=w: at least w columns; 0: none)
+// — on databases of fewer than kQuadMaxFill x kFillSubjects subjects only.
+// Measured (profiles/r04_sweep_quads/): without quads C2 +1.0 %, its 1/2
+// share +2.5 %, 1/4 +1.8 %, C3 unchanged, but the 1/8 share -19.6 % (its
+// widest blocks' pair latency sets the span there).
 constexpr double kQuadFrac = 0.67;
+constexpr double kQuadMaxFill = 0.2;
 
 int32_t lpt_quad_blocks(const sw_db* db, int32_t npair) {
     int64_t wmin = static_cast<int64_t>(kQuadFrac * db->long_threshold);
+    if (static_cast<double>(db->n) >= kQuadMaxFill * kFillSubjects) wmin = 0;
     if (const char* e = std::getenv("SW_QUAD_WIDTH")) wmin = std::atoll(e);
     if (wmin <= 0) return 0;
     int32_t n = 0;
