@@ -27,7 +27,7 @@
 #include <unordered_map>
 #include <vector>
 
-#include "../../include/sw_amd.h"
+#include "sw_amd.h"
 #include "sw_kernels.h"
 
 namespace {

@@ -37,7 +37,7 @@
 #include <thread>
 #include <vector>
 
-#include "../../include/sw_amd.h"
+#include "sw_amd.h"
 #include "sw_kernels.h"
 
 namespace {
