@@ -25,7 +25,8 @@ MATRIX_BLOSUM50_CHAR = 3  # the _char path's table as its lookup reads it ('*' =
 EXPORTED = (
     "sw_version", "sw_build_id", "sw_last_error", "sw_encode", "sw_builtin_matrix",
     "sw_create", "sw_destroy", "sw_stream", "sw_set_stream",
-    "sw_db_create", "sw_db_free", "sw_db_get_stats", "sw_db_set_long_threshold",
+    "sw_opts_init", "sw_opts_from_env", "sw_set_opts", "sw_get_opts",
+    "sw_db_create", "sw_db_free", "sw_db_get_stats", "sw_db_set_long_threshold", "sw_db_reset_adaptive",
     "sw_scan", "sw_scan_device", "sw_scan_batch", "sw_scan_batch_device", "sw_get_timing",
     "sw_timing_reset", "sw_timing_total", "sw_stream_wait_scan", "sw_last_kernel", "sw_last_intra_kernel",
     "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_topk_device_ids", "sw_scan_topk", "sw_score_pair",
@@ -59,6 +60,30 @@ class DbStats(ctypes.Structure):
 class Alignment(ctypes.Structure):
     _fields_ = [("score", ctypes.c_int32), ("q_begin", ctypes.c_int32), ("q_end", ctypes.c_int32),
                 ("s_begin", ctypes.c_int32), ("s_end", ctypes.c_int32), ("ops_len", ctypes.c_int32)]
+
+
+class Opts(ctypes.Structure):
+    """sw_opts (include/sw_amd.h): kernel-form overrides, -1 = the library's
+    choice.  Field names are the header's; the SW_* variable each mirrors
+    is listed there."""
+    INT_FIELDS = ("lpt", "lpt_pipe", "quad_width", "pair_width", "pair_group", "coop_width", "coop_skew",
+                  "intra_x2", "intra_x2_rows", "intra_i16_first", "inter_i16_span", "int16_guard",
+                  "rescue_stats")
+    _fields_ = [("size", ctypes.c_int32)] + [(f, ctypes.c_int32) for f in INT_FIELDS] + \
+        [("inter_variant", ctypes.c_char * 16), ("trace_file", ctypes.c_char * 256)]
+
+    def as_dict(self):
+        d = {f: getattr(self, f) for f in self.INT_FIELDS}
+        d["inter_variant"] = self.inter_variant.decode()
+        d["trace_file"] = self.trace_file.decode()
+        return d
+
+
+def opts_from_env():
+    """sw_opts from the SW_* environment (sw_opts_from_env)."""
+    o = Opts()
+    _check(lib().sw_opts_from_env(ctypes.byref(o)))
+    return o
 
 
 class Timing(ctypes.Structure):
@@ -104,6 +129,11 @@ def lib():
         "sw_destroy": (ctypes.c_int, [vp]),
         "sw_stream": (vp, [vp]),
         "sw_set_stream": (ctypes.c_int, [vp, vp]),
+        "sw_opts_init": (ctypes.c_int, [ctypes.POINTER(Opts)]),
+        "sw_opts_from_env": (ctypes.c_int, [ctypes.POINTER(Opts)]),
+        "sw_set_opts": (ctypes.c_int, [vp, ctypes.POINTER(Opts)]),
+        "sw_get_opts": (ctypes.c_int, [vp, ctypes.POINTER(Opts)]),
+        "sw_db_reset_adaptive": (ctypes.c_int, [vp]),
         "sw_db_create": (ctypes.c_int, [vp, u8p, i64p, i64, i32p, ctypes.POINTER(vp)]),
         "sw_db_free": (ctypes.c_int, [vp]),
         "sw_db_get_stats": (ctypes.c_int, [vp, ctypes.POINTER(DbStats)]),
@@ -211,14 +241,46 @@ class _ScoringArg:
 
 
 class Handle:
-    """One device + one HIP stream (sw_create)."""
+    """One device + one HIP stream (sw_create).  env_opts: start from the
+    SW_* environment (sw_opts_from_env: measurement scripts set kernel-form
+    overrides that way); otherwise the library's own choices."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, env_opts=True):
         h = ctypes.c_void_p()
         _check(lib().sw_create(device, ctypes.byref(h)))
         self._h = h
         self.device = device
         self._dbs = weakref.WeakSet()  # databases must be freed before the handle
+        if env_opts:
+            _check(lib().sw_set_opts(h, ctypes.byref(opts_from_env())))
+
+    def get_opts(self):
+        o = Opts()
+        _check(lib().sw_get_opts(self._h, ctypes.byref(o)))
+        return o
+
+    def set_opts(self, opts=None, **fields):
+        """sw_set_opts: `opts` (an Opts; default the handle's current ones)
+        with `fields` changed, e.g. set_opts(lpt=1, quad_width=0)."""
+        o = Opts()
+        if opts is None:
+            o = self.get_opts()
+        else:
+            ctypes.memmove(ctypes.byref(o), ctypes.byref(opts), ctypes.sizeof(Opts))
+        for k, v in fields.items():
+            if k in ("inter_variant", "trace_file"):
+                setattr(o, k, (v or "").encode())
+            elif k in Opts.INT_FIELDS:
+                setattr(o, k, -1 if v is None else int(v))
+            else:
+                raise TypeError("unknown sw_opts field %r" % k)
+        _check(lib().sw_set_opts(self._h, ctypes.byref(o)))
+
+    def reset_opts(self):
+        """Every override off (sw_opts_init: the library's own choices)."""
+        o = Opts()
+        _check(lib().sw_opts_init(ctypes.byref(o)))
+        _check(lib().sw_set_opts(self._h, ctypes.byref(o)))
 
     @property
     def ptr(self):
@@ -384,6 +446,11 @@ class Database:
 
     def set_long_threshold(self, t):
         _check(lib().sw_db_set_long_threshold(self._d, int(t)))
+
+    def reset_adaptive(self):
+        """Forget the int16-first routing learned from earlier scans
+        (sw_db_reset_adaptive): the next scan runs as on a fresh database."""
+        _check(lib().sw_db_reset_adaptive(self._d))
 
     def stats(self):
         s = DbStats()

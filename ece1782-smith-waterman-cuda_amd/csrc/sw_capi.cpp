@@ -222,6 +222,19 @@ struct ScanEvents {
     bool merged = false;  // one merged launch (sw_scan_lpt): ev6..ev7 is the whole scan's fp16 pass
 };
 
+namespace {
+sw_opts default_opts() {
+    sw_opts o;
+    std::memset(&o, 0, sizeof o);
+    o.size = static_cast<int32_t>(sizeof o);
+    for (int32_t* f : {&o.lpt, &o.lpt_pipe, &o.quad_width, &o.pair_width, &o.pair_group, &o.coop_width,
+                       &o.coop_skew, &o.intra_x2, &o.intra_x2_rows, &o.intra_i16_first, &o.inter_i16_span,
+                       &o.int16_guard, &o.rescue_stats})
+        *f = -1;
+    return o;
+}
+}  // namespace
+
 struct sw_handle {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -289,7 +302,25 @@ struct sw_handle {
     bool timed = false;
     bool had_intra = false;
     int launches = 0;
+    // host-mapped fault word (swk::DrainArgs::fault): set by a kernel that
+    // had to skip work it could not do (list_wait_take's timeout); the next
+    // call on the handle fails with SW_E_DEVICE instead of returning scores
+    int32_t* h_fault = nullptr;
+    int32_t* d_fault = nullptr;
+    int open_slot = -1;  // profile slot pending on an ev[3] this scan has not recorded yet
+    sw_opts opts = default_opts();  // kernel-form overrides (sw_set_opts); all -1 = the library's choice
 };
+
+// A kernel of this handle reported a fault since the last check (sw_kernels.h
+// list_wait_take): fail loudly, once.
+static int check_fault(sw_handle* h) {
+    if (h && h->h_fault && __atomic_load_n(h->h_fault, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(h->h_fault, 0, __ATOMIC_RELEASE);
+        return fail(SW_E_DEVICE, "sw_scan_lpt: a claimed rescue-list entry never appeared; the handle's scans "
+                                 "since the last successful call may hold unrescued scores");
+    }
+    return SW_OK;
+}
 
 struct sw_db {
     sw_handle* h = nullptr;
@@ -358,7 +389,7 @@ struct sw_db {
     };
     std::vector<SpanObs> i16_span;
     int32_t last_i16_span = 0;
-    uint64_t* h_trace = nullptr;         // SW_TRACE_FILE: host-mapped block timeline
+    uint64_t* h_trace = nullptr;         // sw_opts trace_file: host-mapped block timeline
     size_t trace_entries = 0;            // ... its entries: per block, then per merged-launch workgroup
     std::vector<uint32_t> h_blk_groups;  // block widths (16-column groups), widest first
     std::vector<int64_t> h_blk_res;      // unpadded residues per block
@@ -370,6 +401,7 @@ struct sw_db {
     struct LptTable {
         int32_t qpad, qpad_intra, ri, npair, group /* quad blocks */, n;
         int32_t npipe;  // the longest pairs, in the pipelined form
+        int32_t pipe_opt;  // sw_opts lpt_pipe the table was built under
         int32_t* d_order;
         std::vector<float> cost;  // estimated duration of each entry, longest first
     };
@@ -527,6 +559,7 @@ double norm_quantile(double p) {
 struct SynthTables {
     int32_t len[4096];     // log-normal length quantiles: median 290, sigma 0.657, in [5, 35213]
     uint8_t lut[65536];    // uniform u16 -> residue code
+    uint8_t lut_stored[65536];  // ... as stored on the device (swk::kStored)
     SynthTables() {
         for (int k = 0; k < 4096; ++k) {
             const double z = norm_quantile((k + 0.5) / 4096.0);
@@ -545,6 +578,7 @@ struct SynthTables {
         for (int v = 0; v < 65536; ++v) {
             while (c < 19 && edges[c] <= v) ++c;
             lut[v] = static_cast<uint8_t>(c);
+            lut_stored[v] = swk::kStored[c];
         }
     }
 };
@@ -671,7 +705,11 @@ int build_db(sw_db* db) {
             if (db->synthetic) lane_len[b * swk::kLanes + l] = static_cast<int32_t>(len(src));
         }
     });
-    // one block's bytes: [group][lane][16 codes], kPadCode past each subject
+    // one block's bytes: [group][lane][16 codes], kPadCode past each subject;
+    // codes are stored as swk::kStored (the profile rows follow it)
+    auto stored = [](uint8_t* d, const uint8_t* p, int64_t m) {
+        for (int64_t j = 0; j < m; ++j) d[j] = swk::kStored[p[j]];
+    };
     auto fill_block = [&](int64_t b, uint8_t* dst) {
         std::memset(dst, swk::kPadCode, static_cast<size_t>(blk_groups[b]) * swk::kGroupBytes);
         for (int l = 0; l < swk::kLanes; ++l) {
@@ -681,15 +719,14 @@ int build_db(sw_db* db) {
             const uint8_t* p = db->h_residues.data() + db->h_offsets[src];
             uint8_t* d = dst + l * swk::kGroupCols;
             int64_t j = 0;
-            for (; j + swk::kGroupCols <= L; j += swk::kGroupCols, d += swk::kGroupBytes)
-                std::memcpy(d, p + j, swk::kGroupCols);
-            if (j < L) std::memcpy(d, p + j, static_cast<size_t>(L - j));
+            for (; j + swk::kGroupCols <= L; j += swk::kGroupCols, d += swk::kGroupBytes) stored(d, p + j, swk::kGroupCols);
+            if (j < L) stored(d, p + j, L - j);
         }
     };
     auto fill_long = [&](int64_t k, uint8_t* dst) {
         const int64_t src = order[k];
         std::memset(dst, swk::kPadCode, loff[k + 1] - loff[k]);
-        std::memcpy(dst, db->h_residues.data() + db->h_offsets[src], static_cast<size_t>(len(src)));
+        stored(dst, db->h_residues.data() + db->h_offsets[src], len(src));
     };
     blk_off.pop_back();
 
@@ -729,8 +766,8 @@ int build_db(sw_db* db) {
         size_t tmp = 0;
         if ((rc = upload(&d_lane_len, lane_len, s, &tmp))) return rc;
         const SynthTables& T = synth_tables();
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&d_lut), sizeof T.lut));
-        HIPCHECK(hipMemcpyAsync(d_lut, T.lut, sizeof T.lut, hipMemcpyHostToDevice, s));
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&d_lut), sizeof T.lut_stored));
+        HIPCHECK(hipMemcpyAsync(d_lut, T.lut_stored, sizeof T.lut_stored, hipMemcpyHostToDevice, s));
         swk::SynthFill f{};
         f.res = db->d_res;
         f.blk_off = db->d_blk_off;
@@ -921,6 +958,7 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     }
     S.last_end = h->ev[3];  // recorded at the end of this scan (scan_impl)
     S.pending = true;
+    h->open_slot = P->slot;  // until ev[3] is recorded (scan_impl cleans up if it fails first)
     return SW_OK;
 }
 
@@ -929,15 +967,16 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
 // block costs ~W*qpad*3.5 VALU instructions at ~8.4 cycles each (2 waves per
 // SIMD); the scan costs ~16 cycles per 64 cells over 1024 SIMDs.  Measured on
 // C2 (2.05e8 residues, profiles/r01_tune_coop.jsonl): width 384 with long
-// threshold 2048 is best, i.e. W ~ sum(residues) / 530000.  SW_COOP_WIDTH
-// overrides (tuning); 0 disables.
+// threshold 2048 is best, i.e. W ~ sum(residues) / 530000.  sw_opts
+// coop_width overrides (tuning); 0 disables.
 int32_t coop_blocks(const sw_db* db, int divisor) {
     // divisor from the inter kernel's shape (swk::inter_coop_divisor): the
     // two-subjects-per-lane kernel wants a wider cut-off than int32 (measured
     // on C2: 1024 beats 386 and 640, profiles/r01_x2/); 0 = no coop kernel
-    if (divisor <= 0 && !std::getenv("SW_COOP_WIDTH")) return 0;
+    const int32_t forced = db->h->opts.coop_width;
+    if (divisor <= 0 && forced < 0) return 0;
     int64_t wmin = divisor > 0 ? std::max<int64_t>(128, db->residues / divisor) : 0;
-    if (const char* e = std::getenv("SW_COOP_WIDTH")) wmin = std::atoll(e);
+    if (forced >= 0) wmin = forced;
     if (wmin <= 0) return 0;
     int32_t n = 0;
     while (n < static_cast<int32_t>(db->h_blk_groups.size()) &&
@@ -949,24 +988,21 @@ int32_t coop_blocks(const sw_db* db, int divisor) {
 // Leading (widest) blocks of a two-strips scan handled by wave pairs
 // (sw_inter_x2p): blocks at least `width` columns wide, width =
 // residues / kPairDivisor (1024 on C2: with the biased cell 1,024 beat 256,
-// 512 and none by 2-4 %, profiles/r01_tail2/; SW_PAIR_WIDTH overrides; 0
-// disables).
+// 512 and none by 2-4 %, profiles/r01_tail2/; sw_opts pair_width
+// overrides; 0 disables).
 constexpr int64_t kPairDivisor = 200000;
 
-// Waves per group for those blocks: pairs; SW_PAIR_GROUP=4 runs quads.
+// Waves per group for those blocks: pairs; sw_opts pair_group = 4 runs quads.
 // Measured on C2's 1/8 share (profiles/r02_strong/): the inter kernel alone
 // is fastest with quads over every block >= 64 wide (1.08 ms vs 1.29 for
 // pairs), but beside the concurrent long-subject kernel, whose workgroups
 // are dispatched first, a quad waits for a whole free workgroup slot and the
 // scan is slower (2.21 vs 1.77 ms).
-int pair_group(const sw_db*) {
-    if (const char* e = std::getenv("SW_PAIR_GROUP")) return std::atoi(e) == 4 ? 4 : 2;
-    return 2;
-}
+int pair_group(const sw_db* db) { return db->h->opts.pair_group == 4 ? 4 : 2; }
 
 int32_t pair_blocks(const sw_db* db) {
     int64_t wmin = std::max<int64_t>(256, db->residues / kPairDivisor);
-    if (const char* e = std::getenv("SW_PAIR_WIDTH")) wmin = std::atoll(e);
+    if (db->h->opts.pair_width >= 0) wmin = db->h->opts.pair_width;
     if (wmin <= 0) return 0;
     int32_t n = 0;
     while (n < static_cast<int32_t>(db->h_blk_groups.size()) &&
@@ -990,7 +1026,7 @@ double intra_step_us(int ri) { return 2 * 0.157 * (ri * 28.8 + 80.0) / (6 * 28.8
 
 // The widest group blocks of the merged launch run by quads: those at least
 // kQuadFrac x the long threshold wide, whose pair latency would otherwise
-// exceed the long subjects' (SW_QUAD_WIDTH=w: at least w columns; 0: none)
+// exceed the long subjects' (sw_opts quad_width w: at least w columns; 0: none)
 // — on databases of fewer than kQuadMaxFill x kFillSubjects subjects only.
 // Measured (profiles/r04_sweep_quads/): without quads C2 +1.0 %, its 1/2
 // share +2.5 %, 1/4 +1.8 %, C3 unchanged, but the 1/8 share -19.6 % (its
@@ -1001,7 +1037,7 @@ constexpr double kQuadMaxFill = 0.2;
 int32_t lpt_quad_blocks(const sw_db* db, int32_t npair) {
     int64_t wmin = static_cast<int64_t>(kQuadFrac * db->long_threshold);
     if (static_cast<double>(db->n) >= kQuadMaxFill * kFillSubjects) wmin = 0;
-    if (const char* e = std::getenv("SW_QUAD_WIDTH")) wmin = std::atoll(e);
+    if (db->h->opts.quad_width >= 0) wmin = db->h->opts.quad_width;
     if (wmin <= 0) return 0;
     int32_t n = 0;
     while (n < npair && static_cast<int64_t>(db->h_blk_groups[n]) * swk::kGroupCols >= wmin) ++n;
@@ -1028,7 +1064,8 @@ double group_ticks_host(int64_t ncols, int passes, int G) {
 int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad,
               const int32_t** order, int* n, int32_t* npipe_out) {
     for (const auto& t : db->lpt_tables)
-        if (t.qpad == qpad && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad) {
+        if (t.qpad == qpad && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad &&
+            t.pipe_opt == db->h->opts.lpt_pipe) {
             *order = t.d_order;
             *n = t.n;
             *npipe_out = t.npipe;
@@ -1070,7 +1107,7 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
                                            intra_step_us(ri); };
     int64_t npipe = 0;
     if (nchp <= swk::kWavesPerWG) {
-        if (const char* e = std::getenv("SW_LPT_PIPE")) npipe = std::atoll(e);
+        if (db->h->opts.lpt_pipe >= 0) npipe = db->h->opts.lpt_pipe;
         else
             while (npipe < std::min<int64_t>(npairs, 4) && pair_us(npipe) > inter_max) ++npipe;
     }
@@ -1094,7 +1131,7 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
         cost[k] = static_cast<float>(w[k].first);
     }
     sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, static_cast<int32_t>(ord.size()),
-                      static_cast<int32_t>(npipe), nullptr, cost};
+                      static_cast<int32_t>(npipe), db->h->opts.lpt_pipe, nullptr, cost};
     HIPCHECK(hipMalloc(reinterpret_cast<void**>(&t.d_order), ord.size() * sizeof(int32_t)));
     HIPCHECK(hipMemcpy(t.d_order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     db->device_bytes += ord.size() * sizeof(int32_t);
@@ -1171,12 +1208,13 @@ int next_events(sw_handle* h) {
 // defer: another scan follows on this handle before the caller waits (the
 // queries of a batch but the last): this scan's rescue tail may run on the
 // tail stream beside the next scan's fp16 passes (sw_handle::tail).
-int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen, const sw_scoring* sc,
+int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen, const sw_scoring* sc,
               int32_t* scores_dev, bool defer = false) {
     sw_db* db = const_cast<sw_db*>(cdb);
     if (!h || !db || (!query && qlen > 0) || qlen < 0 || !scores_dev) return fail(SW_E_INVALID, "null argument");
     const int8_t* mat;
     int go, ge, rc;
+    if ((rc = check_fault(h))) return rc;
     if ((rc = check_scoring(sc, &mat, &go, &ge))) return rc;
     // The linear kernels keep S + gap in an int8 profile; if that does not
     // fit, score with the affine kernels (open == extend is the same DP).
@@ -1206,7 +1244,8 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                       : (static_cast<int64_t>(qlen) + 2) * (max_s + go) < 32767 ? 2
                       : (max_s + go < 1000 && ge < 1000)                       ? 1
                                                                                : 0;
-    const int R = swk::inter_rows(affine, x2_ok);
+    const swk::InterShape shape = swk::inter_shape(affine, x2_ok, h->opts);
+    const int R = shape.R;
     const int32_t qpad_inter = static_cast<int32_t>(round_up(qlen, R));
     // (the merged launch's drain takes the int32 rows per lane from ri2, below)
     int ri = db->nlong ? swk::intra_rows_for(qlen, db->long_max) : 0;
@@ -1214,13 +1253,14 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // Long subjects: two per wave in packed fp16 (sw_intra_x2) when the guard
     // applies, with the int32 sw_intra re-scoring the subjects it flags
     // (SW_INTRA_X2=0: int32 only).
-    const char* ix = std::getenv("SW_INTRA_X2");
-    const bool intra_x2 = db->nlong && x2_ok >= 1 && !(ix && ix[0] == '0');
+    const sw_opts& O = h->opts;
+    const bool intra_x2 = db->nlong && x2_ok >= 1 && O.intra_x2 != 0;
     // (20 rows per lane only where no merged launch can take the scan: no
     // inter blocks; where the fp16 bias of row 19 fits, as f16_fits; and by
     // the cost model for affine gaps only, see intra_x2_rows_for)
     const bool ri2_wide = db->nblocks == 0 && 2 * max_s + (swk::intra_bias_rows(swk::kIntraX2MaxRI) + 1) * ge + go < 1024;
-    const int ri2 = intra_x2 ? swk::intra_x2_rows_for(qlen, db->long_max, ri2_wide ? (affine ? 2 : 1) : 0) : 0;
+    const int ri2 =
+        intra_x2 ? swk::intra_x2_rows_for(qlen, db->long_max, ri2_wide ? (affine ? 2 : 1) : 0, O.intra_x2_rows) : 0;
     // The intra chain's order.  Linear scoring with cheap gaps makes random
     // pairs' scores grow with their lengths, so on long subjects the fp16
     // pass can flag many of them and its time on those is wasted.  Once a
@@ -1228,7 +1268,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // subjects at a query no longer than this one, the int16 form runs
     // first, over all of them (the int16 cell costs ~1.4x the fp16 one, so
     // fp16 first + int16 over the flagged fraction p wins while p < ~0.3).
-    // SW_INTRA_I16_FIRST=0 / 1: never / always.
+    // sw_opts intra_i16_first 0 / 1: never / always.
     uint64_t skey = 1469598103934665603ull;  // FNV-1a of the scoring
     for (int k = 0; k < 625; ++k) skey = (skey ^ static_cast<uint8_t>(mat[k])) * 1099511628211ull;
     skey = ((skey ^ static_cast<uint32_t>(go)) * 1099511628211ull ^ static_cast<uint32_t>(ge)) * 1099511628211ull;
@@ -1250,10 +1290,9 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             if (!seen) db->i16_first.emplace_back(db->lcount_key, db->lcount_qlen);
         }
     }
-    const char* i16f = std::getenv("SW_INTRA_I16_FIRST");
     bool intra_i16_first = false;
-    if (i16f && (i16f[0] == '0' || i16f[0] == '1')) {
-        intra_i16_first = i16f[0] == '1';
+    if (O.intra_i16_first == 0 || O.intra_i16_first == 1) {
+        intra_i16_first = O.intra_i16_first == 1;
     } else {
         for (const auto& e : db->i16_first)
             if (e.first == skey && e.second <= qlen) intra_i16_first = true;
@@ -1265,7 +1304,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // every pass in turn) takes longer than the whole scan.  A scan with the
     // same scoring whose fp16 pass flagged most of blocks [0, span) makes
     // later queries at least as long run those blocks in int16, by wave pairs
-    // beside the fp16 launch.  SW_INTER_I16_SPAN=n forces n blocks (0: off).
+    // beside the fp16 launch.  sw_opts inter_i16_span n forces n blocks (0: off).
     if (db->icount_pending && hipEventQuery(db->icount_ev) == hipSuccess) {
         db->icount_pending = false;
         db->icount_seen = true;
@@ -1295,8 +1334,8 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         }
     }
     int32_t i16_span = 0;
-    if (const char* e = std::getenv("SW_INTER_I16_SPAN")) {
-        i16_span = std::atoi(e);
+    if (O.inter_i16_span >= 0) {
+        i16_span = O.inter_i16_span;
     } else {
         for (const auto& o : db->i16_span)
             if (o.key == skey && o.qlen <= qlen) i16_span = std::max(i16_span, o.span);
@@ -1320,10 +1359,10 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         return SW_OK;
     }
     Profiles P;
-    const bool x2 = swk::inter_uses_x2(affine, x2_ok);
+    const bool x2 = shape.x2s;
     // int32 re-scoring of blocks a 16-bit kernel flags near saturation
-    const bool rescue = swk::inter_needs_rescue(affine, x2_ok);
-    const bool f16 = swk::inter_uses_f16(affine, x2_ok);
+    const bool rescue = swk::inter_needs_rescue(shape, x2_ok);
+    const bool f16 = shape.f16;
     const int32_t qpad_rescue = rescue ? static_cast<int32_t>(round_up(qlen, swk::rescue_rows(affine))) : 0;
     // fp16 chain stage 2 (the int16 two-strips 32x8 kernel): 64-row passes
     // (the linear list kernel is the 48x4 shape: 96-row passes)
@@ -1331,9 +1370,9 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // widest blocks first, one cooperative workgroup each (int32, int8-profile paths)
     // two-strips scans: the widest blocks by wave pairs (at least two passes)
     const int32_t npair =
-        (db->nblocks && swk::inter_has_pair(affine, x2_ok) && qpad_inter > R) ? pair_blocks(db) : 0;
+        (db->nblocks && swk::inter_has_pair(shape) && qpad_inter > R) ? pair_blocks(db) : 0;
     const int32_t ncoop =
-        (!npair && db->nblocks) ? coop_blocks(db, swk::inter_coop_divisor(affine, x2_ok)) : 0;
+        (!npair && db->nblocks) ? coop_blocks(db, swk::inter_coop_divisor(shape)) : 0;
     db->last_ncoop = ncoop;
     db->last_npair = npair;
     db->last_pair_merged = npair != 0;
@@ -1346,9 +1385,8 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // after it): now 7.19 -> 7.12 ms under affine scoring (C3 and C4's share
     // unchanged), but under linear gaps 4.57 -> 5.03 ms (profiles/r04_*/):
     // affine scans of every database and linear scans of small ones take
-    // it.  SW_LPT=0 / 1 forces either form.
-    const char* lpt_env = std::getenv("SW_LPT");
-    const bool lpt_want = lpt_env ? lpt_env[0] == '1' : affine || static_cast<double>(db->n) < 0.35 * kFillSubjects;
+    // it.  sw_opts lpt 0 / 1 forces either form.
+    const bool lpt_want = O.lpt >= 0 ? O.lpt == 1 : affine || static_cast<double>(db->n) < 0.35 * kFillSubjects;
     const bool lpt = lpt_want && db->nlong && db->nblocks && intra_x2 && !intra_i16_first &&
                      f16 && rescue && npair && !ncoop && i16_span == 0 &&
                      swk::lpt_supported(ri2);
@@ -1390,6 +1428,11 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         HIPCHECK(hipStreamWaitEvent(h->stream, h->tail_done[par], 0));
         h->tail_pending[par] = false;
     }
+    // The drain re-scores on the deferred tails' boundary rows (d_rbnd_*,
+    // d_rlbnd_*): a non-merged scan just before this one (a longer query
+    // routed int16-first, say) may still be running its tail on those rows,
+    // so the merged launch starts after every pending tail.
+    if (drain && (rc = join_tails(h))) return rc;
     int32_t* const listA = db->d_rescue ? db->d_rescue + par * rstride : nullptr;  // [count, ids...]
     int32_t* const listB = listA ? listA + db->nblocks + 1 : nullptr;
     int32_t* const maxA = listA ? listA + 2 * (db->nblocks + 1) : nullptr;
@@ -1592,7 +1635,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
         a.bnd_h = db->d_bnd_h;
         a.bnd_f = db->d_bnd_f;
         a.scores = scores_dev;
-        if (std::getenv("SW_TRACE_FILE")) {
+        if (O.trace_file[0]) {
             if (!db->h_trace) {
                 // one entry per block, then one per workgroup of a merged
                 // launch (at most nblocks inter + nlong / 8 intra workgroups)
@@ -1634,7 +1677,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             c.prof = P.dev + P.off8;  // the coop kernel reads the int8 profile
             HIPCHECK(hipStreamWaitEvent(h->side2, h->ev[0], 0));
             MARK(4, h->side2);
-            HIPCHECK(swk::launch_inter_coop(c, ncoop, affine, h->side2));
+            HIPCHECK(swk::launch_inter_coop(c, ncoop, affine, h->opts.coop_skew != 0, h->side2));
             MARK(5, h->side2);
             HIPCHECK(hipEventRecord(h->coop_done, h->side2));
             ++h->launches;
@@ -1708,6 +1751,7 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                 d.heads[1] = headA + 1;
                 d.heads[2] = head1;
                 d.heads[3] = head1 + 1;
+                d.fault = h->d_fault;
                 const std::vector<uint64_t> key = {
                     reinterpret_cast<uint64_t>(P.dev), P.off8, P.off16, P.intra_off, static_cast<uint64_t>(par),
                     reinterpret_cast<uint64_t>(scores_dev), static_cast<uint64_t>(qlen), skey,
@@ -1725,9 +1769,9 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
             a.blk_first = std::max(npair, nr);
             HIPCHECK(swk::launch_inter_x2p(a, affine, f16, true, pair_group(db), h->stream));
         } else {
-            HIPCHECK(swk::launch_inter(a, affine, x2_ok, h->stream));
+            HIPCHECK(swk::launch_inter(a, affine, shape, h->stream));
         }
-        h->last_kernel = swk::inter_kernel_name(affine, x2_ok);
+        h->last_kernel = swk::inter_kernel_name(shape, affine);
         if (npair) h->last_kernel.replace(0, std::strlen("sw_inter_x2s"), "sw_inter_x2p");  // + wave pairs
         if (nr) h->last_kernel += "+int16[0," + std::to_string(nr) + ")";
         if (lpt) h->last_kernel += drain ? "+lpt+drain" : "+lpt";
@@ -1783,9 +1827,10 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
     // the scan completes on the handle's stream: so do earlier deferred tails
     if (!deferred && (rc = join_tails(h))) return rc;
     MARK(3, h->stream);
+    h->open_slot = -1;
     h->evpool[h->nscans - 1].launches = h->launches;
     h->timed = true;
-    if (std::getenv("SW_RESCUE_STATS")) {  // diagnostics: what the guard bands flagged (synchronises)
+    if (O.rescue_stats == 1) {  // diagnostics: what the guard bands flagged (synchronises)
         HIPCHECK(hipStreamSynchronize(h->stream));
         HIPCHECK(hipStreamSynchronize(h->tail));
         int32_t cA = 0, cB = 0, l1 = 0, l2 = 0;
@@ -1818,6 +1863,22 @@ int scan_impl(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen
                      static_cast<long long>(db->nlong), l2);
     }
     return SW_OK;
+}
+
+// A scan that fails after its profiles were built leaves the profile slot
+// pending on an end event it never recorded: a later scan reusing the slot
+// would not wait for the kernels this one queued.  Drain the handle's streams
+// and release the slot instead.
+int scan_impl(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen, const sw_scoring* sc,
+              int32_t* scores_dev, bool defer = false) {
+    const int rc = scan_impl_body(h, db, query, qlen, sc, scores_dev, defer);
+    if (h && h->open_slot >= 0) {
+        for (hipStream_t st : {h->stream, h->side, h->side2, h->tail})
+            if (st) (void)hipStreamSynchronize(st);
+        h->prof[h->open_slot].pending = false;
+        h->open_slot = -1;
+    }
+    return rc;
 }
 
 int ensure_scores(sw_handle* h, size_t n) {
@@ -1931,6 +1992,11 @@ int sw_create(int32_t device, sw_handle** out) {
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->coop_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->fork2, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&h->h_fault), sizeof(int32_t), hipHostMallocMapped);
+    if (e == hipSuccess) {
+        *h->h_fault = 0;
+        e = hipHostGetDevicePointer(reinterpret_cast<void**>(&h->d_fault), h->h_fault, 0);
+    }
     for (auto& ev : h->stage_ev)
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (e != hipSuccess) { delete h; return fail(SW_E_HIP, hipGetErrorString(e)); }
@@ -1965,12 +2031,66 @@ int sw_destroy(sw_handle* h) {
         if (ev) (void)hipEventDestroy(ev);
     if (h->coop_done) (void)hipEventDestroy(h->coop_done);
     if (h->fork2) (void)hipEventDestroy(h->fork2);
+    if (h->h_fault) (void)hipHostFree(h->h_fault);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return SW_OK;
 }
 
 void* sw_stream(sw_handle* h) { return h ? reinterpret_cast<void*>(h->stream) : nullptr; }
+
+int sw_opts_init(sw_opts* o) {
+    if (!o) return fail(SW_E_INVALID, "null argument");
+    *o = default_opts();
+    return SW_OK;
+}
+
+// The one place the library reads its SW_* variables (tests and A/B scripts
+// call it; the scan path reads the handle's sw_opts only).
+int sw_opts_from_env(sw_opts* o) {
+    int rc;
+    if ((rc = sw_opts_init(o))) return rc;
+    const struct {
+        const char* name;
+        int32_t* field;
+    } ints[] = {{"SW_LPT", &o->lpt},
+                {"SW_LPT_PIPE", &o->lpt_pipe},
+                {"SW_QUAD_WIDTH", &o->quad_width},
+                {"SW_PAIR_WIDTH", &o->pair_width},
+                {"SW_PAIR_GROUP", &o->pair_group},
+                {"SW_COOP_WIDTH", &o->coop_width},
+                {"SW_COOP_SKEW", &o->coop_skew},
+                {"SW_INTRA_X2", &o->intra_x2},
+                {"SW_INTRA_X2_RI", &o->intra_x2_rows},
+                {"SW_INTRA_I16_FIRST", &o->intra_i16_first},
+                {"SW_INTER_I16_SPAN", &o->inter_i16_span},
+                {"SW_INT16_GUARD", &o->int16_guard},
+                {"SW_RESCUE_STATS", &o->rescue_stats}};
+    for (const auto& k : ints)
+        if (const char* e = std::getenv(k.name); e && e[0]) *k.field = std::atoi(e);
+    if (const char* e = std::getenv("SW_INTER_VARIANT"))
+        std::snprintf(o->inter_variant, sizeof o->inter_variant, "%s", e);
+    if (const char* e = std::getenv("SW_TRACE_FILE")) std::snprintf(o->trace_file, sizeof o->trace_file, "%s", e);
+    return SW_OK;
+}
+
+int sw_set_opts(sw_handle* h, const sw_opts* o) {
+    if (!h || !o) return fail(SW_E_INVALID, "null argument");
+    if (o->size != static_cast<int32_t>(sizeof(sw_opts)))
+        return fail(SW_E_INVALID, "sw_opts.size mismatch (initialise with sw_opts_init)");
+    if (o->pair_group != -1 && o->pair_group != 2 && o->pair_group != 4)
+        return fail(SW_E_INVALID, "sw_opts.pair_group must be -1, 2 or 4");
+    h->opts = *o;
+    h->opts.inter_variant[sizeof h->opts.inter_variant - 1] = 0;
+    h->opts.trace_file[sizeof h->opts.trace_file - 1] = 0;
+    return SW_OK;
+}
+
+int sw_get_opts(const sw_handle* h, sw_opts* o) {
+    if (!h || !o) return fail(SW_E_INVALID, "null argument");
+    *o = h->opts;
+    return SW_OK;
+}
 
 int sw_set_stream(sw_handle* h, void* hip_stream) {
     if (!h) return fail(SW_E_INVALID, "null handle");
@@ -2191,7 +2311,7 @@ int sw_db_free(sw_db* db) {
     if (db->h->side) (void)hipStreamSynchronize(db->h->side);
     if (db->h->tail) (void)hipStreamSynchronize(db->h->tail);
     if (db->h_trace) {  // the last scan's block timeline (tail analysis builds)
-        if (const char* path = std::getenv("SW_TRACE_FILE"))
+        if (const char* path = db->h->opts.trace_file; path[0])
             if (FILE* f = std::fopen(path, "wb")) {
                 std::fwrite(db->h_trace, 32, db->trace_entries, f);
                 std::fclose(f);
@@ -2203,6 +2323,19 @@ int sw_db_free(sw_db* db) {
     if (db->icount_ev) (void)hipEventDestroy(db->icount_ev);
     free_dev(db);
     delete db;
+    return SW_OK;
+}
+
+int sw_db_reset_adaptive(sw_db* db) {
+    if (!db) return fail(SW_E_INVALID, "null argument");
+    // a readback still in flight lands in the same pinned words later, in
+    // stream order before any readback a later scan issues: ignoring it is safe
+    db->lcount_pending = false;
+    db->lcount_seen = false;
+    db->i16_first.clear();
+    db->icount_pending = false;
+    db->icount_seen = false;
+    db->i16_span.clear();
     return SW_OK;
 }
 
@@ -2259,7 +2392,7 @@ int sw_scan(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen, c
     if ((rc = scan_impl(h, db, query, qlen, sc, h->d_scores))) return rc;
     HIPCHECK(hipMemcpyAsync(scores_host, h->d_scores, n * 4, hipMemcpyDeviceToHost, h->stream));
     HIPCHECK(hipStreamSynchronize(h->stream));
-    return SW_OK;
+    return check_fault(h);
 }
 
 namespace {
@@ -2315,6 +2448,7 @@ int sw_scan_batch(sw_handle* h, const sw_db* db, const uint8_t* queries, const i
         if ((rc = sw_scan_batch_device(h, db, queries, qoffsets + k0, m, sc, h->d_scores))) return rc;
         HIPCHECK(hipMemcpyAsync(scores_host + k0 * n, h->d_scores, m * n * 4, hipMemcpyDeviceToHost, h->stream));
         HIPCHECK(hipStreamSynchronize(h->stream));
+        if ((rc = check_fault(h))) return rc;
     }
     return SW_OK;
 }
@@ -2446,7 +2580,7 @@ int sw_scan_topk(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t q
     HIPCHECK(hipMemcpyAsync(keys_host, keys_dev, static_cast<size_t>(k) * sizeof(int64_t), hipMemcpyDeviceToHost,
                             h->stream));
     HIPCHECK(hipStreamSynchronize(h->stream));
-    return SW_OK;
+    return check_fault(h);
 }
 
 int sw_align(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen, const sw_scoring* sc,

@@ -1057,7 +1057,7 @@ __device__ __forceinline__ void lpt_drain(const DrainArgs* __restrict__ d, char*
             }
             int m = 0;
             for (int i = 0; i < n; ++i) {
-                const int v = list_wait_take(d->lists[kind - 1] + 1, start + i);
+                const int v = list_wait_take(d->lists[kind - 1] + 1, start + i, d->fault);
                 if (v >= 0) task[2 + m++] = v;
             }
             task[0] = m ? kind : (n ? -1 : 0);  // -1: claimed entries never appeared; look again

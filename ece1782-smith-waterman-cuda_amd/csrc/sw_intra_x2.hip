@@ -21,10 +21,10 @@ __global__ __launch_bounds__(kWavesPerWG * kLanes) void sw_intra_x2(IntraArgs a)
     ix2::intra_x2_wg<RI, F16, LIST, LIN, true, false, kConv>(a, blockIdx.x, img);
 }
 
-int intra_x2_rows_for(int qlen, int longest, int wide) {
+int intra_x2_rows_for(int qlen, int longest, int wide, int forced) {
     // chunks x steps x (cell pairs per lane-step + conveyor/hand-off overhead)
-    if (const char* e = std::getenv("SW_INTRA_X2_RI")) {  // tests: force a shape
-        const int ri = std::atoi(e);
+    if (forced > 0) {  // sw_opts intra_x2_rows (tests: force a shape)
+        const int ri = forced;
         if (ri == 4 || ri == 6 || ri == 8 || ri == 10 || ri == 12 || ri == 16) return ri;
         if (ri == kIntraX2MaxRI && wide >= 1) return ri;
     }

@@ -7,6 +7,8 @@
 
 #include <string>
 
+#include "sw_amd.h"  // sw_opts: the kernel-form overrides the shape choices below read
+
 namespace swk {
 
 // Record `msg` as this thread's sw_last_error() text and return `code`
@@ -18,6 +20,23 @@ constexpr int kGroupCols = 16;    // residue columns per packed group
 constexpr int kGroupBytes = kLanes * kGroupCols;  // 1 KiB: [lane][16 residues]
 constexpr int kProfileRows = 32;  // profile codes: 25 residues + PAD (25) + unused
 constexpr int kPadCode = 25;      // residue code used for padding (scores 0)
+// The byte a residue code is stored as in the device database (the profile
+// rows follow it: row kStored[c] holds code c's scores).  The two-strips
+// kernel reads its profile images with ds_read_b128 at 144 bytes (9 x 16)
+// per code row; a 16-lane bank group spans 16 such slots, so stored bytes
+// equal mod 16 share a slot with different addresses (one extra LDS cycle
+// per group that holds both).  With 26 codes some pairs alias under any row
+// stride; this order makes them rare ones: the six most frequent residues
+// (L A G V E S) alone on slots 10-15, I beside the pad, K R D T P beside the
+// codes a protein database does not hold (B J Z X *), and the eight rarest
+// standard residues paired rarest with most frequent.  Modelled on C2's
+// blocks (scripts/lds_conflict_model.py): 3.07 -> 1.48 extra LDS cycles per
+// image read (the profiled launch measured 2.90 per LDS instruction with the
+// alphabetical order).  The pad is stored as itself.
+//                       A   R  N  D  C   Q  E   G   H   I  L   K  M   F  P  S   T  W   Y  V   B   J   Z   X   *   pad
+constexpr uint8_t kStored[26] = {11, 1, 5, 2, 22, 6, 14, 12, 23, 9, 10, 0, 24, 7, 4, 15, 3, 21, 8, 13, 16, 17, 18, 19, 20, 25};
+// ... and its inverse: the code a stored byte stands for
+constexpr uint8_t kCodeOf[26] = {11, 1, 3, 16, 14, 2, 5, 13, 18, 9, 10, 0, 7, 19, 6, 15, 20, 21, 22, 23, 24, 17, 4, 8, 12, 25};
 constexpr int kWavesPerWG = 4;
 
 // Shared by the inter kernels: one wave's residues for SG columns.
@@ -161,10 +180,13 @@ __device__ __forceinline__ int32_t list_take(const int32_t* items, int i) {
     __hip_atomic_store(p, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return v;
 }
-// Consumer in the producer's launch: wait (bounded) until entry i is written,
-// then reset it.  -1 if it never appears (the caller skips it; a bounded
-// wait, so a wave can never hang here).
-__device__ __forceinline__ int32_t list_wait_take(int32_t* items, int i) {
+// Consumer in the producer's launch: wait until entry i is written, then
+// reset it.  The producer stores the entry right after its atomicAdd and a
+// wave is not preempted, so the entry appears within microseconds; the wait
+// is still bounded (about 0.1 s) so a wave can never hang here, and a timeout
+// is not silent: it sets *fault (host-visible, mapped), the library fails the
+// next call on that handle (SW_E_DEVICE) and the caller skips the entry.
+__device__ __forceinline__ int32_t list_wait_take(int32_t* items, int i, int32_t* fault) {
     int32_t* p = items + i;
     int32_t v = -1;
     for (int spin = 0; spin < (1 << 22); ++spin) {
@@ -172,7 +194,10 @@ __device__ __forceinline__ int32_t list_wait_take(int32_t* items, int i) {
         if (v >= 0) break;
         __builtin_amdgcn_s_sleep(1);
     }
-    if (v >= 0) __hip_atomic_store(p, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v >= 0)
+        __hip_atomic_store(p, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (fault)
+        __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return v;
 }
 // Claim up to `want` entries [start, start + n) past the list's head; 0 when
@@ -193,37 +218,44 @@ __device__ __forceinline__ int list_claim(int32_t* count, int32_t* head, int wan
 }
 #endif
 
-// Strip heights (query rows held in registers per lane) the kernels are
-// instantiated for.
-// Shape of the inter kernel for this gap model.  x2_ok: 2 = the scan is
+// Shape of the inter kernel for this gap model: R query rows per strip x SG
+// columns per software-pipelined sub-group; x2s: the packed two-strips
+// kernel (int16 profile), f16: its fp16 form.  x2_ok: 2 = the scan is
 // provably int16-safe (any packed kernel may run); 1 = a guarded packed
 // kernel may run (saturating blocks are re-scored at int32); 0 = int32 only.
-int inter_rows(bool affine, int x2_ok);
-// true if the packed two-strips kernel is used (int16 profile).
-bool inter_uses_x2(bool affine, int x2_ok);
+// o.int16_guard / o.inter_variant override the choice (tests, A/B).
+struct InterShape {
+    int R, SG;
+    bool x2s = false;
+    bool f16 = false;
+};
+InterShape inter_shape(bool affine, int x2_ok, const sw_opts& o);
+// true if the chosen inter kernel may flag blocks for int32 re-scoring
+// (16-bit kernels beyond the static int16 bound).
+inline bool inter_needs_rescue(const InterShape& v, int x2_ok) { return v.f16 || (v.x2s && x2_ok != 2); }
+// true if the chosen inter kernel has a wave-pair form (two-strips 32x8).
+inline bool inter_has_pair(const InterShape& v) { return v.x2s && v.R == 64 && v.SG == 8; }
 // Wide-block cut-off for the cooperative kernel: residues / divisor columns
-// (0 = the chosen inter kernel does not use it).
-int inter_coop_divisor(bool affine, int x2_ok);
-// Name of the per-wave inter kernel launch_inter() runs, e.g. "sw_inter_x2<16,16,affine>".
-const char* inter_kernel_name(bool affine, int x2_ok);
+// (0 = the chosen inter kernel does not use it: one subject per lane with two
+// strips per pass has no long single-wave tail, coop on/off within 1 %).
+inline int inter_coop_divisor(const InterShape& v) { return v.x2s ? 0 : 530000; }
+// Name of the per-wave inter kernel launch_inter() runs, e.g. "sw_inter_x2s<32,8,affine,fp16>".
+const char* inter_kernel_name(const InterShape& v, bool affine);
 // Query rows per lane the intra kernel uses for this query (2..16, even).
 int intra_rows_for(int qlen, int longest);
 // Bytes of one intra profile chunk (64*ri query rows, 32 codes).
 int intra_chunk_bytes(int ri);
 __host__ __device__ constexpr int intra_rip(int RI) { return (RI + 3) / 4 * 4; }
 
-hipError_t launch_inter(const InterArgs& a, bool affine, int x2_ok, hipStream_t s);
+hipError_t launch_inter(const InterArgs& a, bool affine, const InterShape& v, hipStream_t s);
 // Wide blocks [0, ncoop): one 4-wave workgroup per block, the waves pipelined
-// over query strips (linear gap).  Returns the strip height it uses.
-hipError_t launch_inter_coop(const InterArgs& a, int ncoop, bool affine, hipStream_t s);
+// over query strips (skew: strip k+1 one sub-group behind strip k).
+hipError_t launch_inter_coop(const InterArgs& a, int ncoop, bool affine, bool skew, hipStream_t s);
 int inter_coop_rows();
 // One subject per lane, two R-row query strips per pass in the two int16
 // halves (sw_inter_x2.hip); qpad is a multiple of 2R; boundary rows are
 // (H | F << 16) dwords in bnd_h.
 hipError_t launch_inter_x2s(const InterArgs& a, int R, int SG, bool affine, bool f16, hipStream_t s);
-// true if the chosen inter kernel computes in fp16 (affine, guarded; its
-// flagged blocks go to the int16 packed kernel in list mode, then int32).
-bool inter_uses_f16(bool affine, int x2_ok);
 // The int16 packed kernel in list mode (blk_list / blk_count set): the
 // second stage of the fp16 rescue chain.
 hipError_t launch_inter_x2s_list(const InterArgs& a, bool affine, hipStream_t s);
@@ -257,12 +289,11 @@ struct DrainArgs {
     IntraArgs i32;
     int32_t* lists[4];  // list A, B, 1, 2: [count, items...]
     int32_t* heads[4];  // their dequeue heads (zeroed per scan)
+    int32_t* fault;     // host-mapped word: a claimed entry never appeared (list_wait_take)
 };
 bool lpt_supported(int ri);
 hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri,
                            hipStream_t s, const DrainArgs* drain = nullptr);
-// true if the chosen inter kernel has a wave-pair form (two-strips 32x8).
-bool inter_has_pair(bool affine, int x2_ok);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.
 constexpr int kSat16 = 32767 - 1152;
 // The two-subjects intra kernel's biased cell stores values up to this many
@@ -275,9 +306,6 @@ constexpr int intra_bias_rows(int ri) { return ri + 10 > 26 ? ri + 10 : 26; }
 // 2 + 2 + 1 + 1 waves per SIMD each: 5,550 GCUPS; 12-wave ones, one per CU,
 // left whole CUs idle in the last round: 7,475; 4-wave: 8,892.)
 constexpr int kIntraX2MaxRI = 20;
-// true if the chosen inter kernel may flag blocks for int32 re-scoring
-// (16-bit kernels beyond the static int16 bound).
-bool inter_needs_rescue(bool affine, int x2_ok);
 // int32 re-scoring of the blocks a 16-bit kernel listed (device-side count);
 // strips of rescue_rows(affine) query rows.
 int rescue_rows(bool affine);
@@ -290,12 +318,12 @@ hipError_t launch_intra_x2(const IntraArgs& a, int ri, hipStream_t s);
 hipError_t launch_intra_x2_list16(const IntraArgs& a, int ri, hipStream_t s);
 // ... and over every subject (the chain's first stage when fp16 would flag most)
 hipError_t launch_intra_x2_int16(const IntraArgs& a, int ri, hipStream_t s);
-// wide: 0 = rows per lane 4..16; 1 = 20 too when a test forces it
-// (SW_INTRA_X2_RI); 2 = 20 by the cost model too.  The host allows 20 only
+// wide: 0 = rows per lane 4..16; 1 = 20 too when forced (sw_opts
+// intra_x2_rows, > 0: a forced shape); 2 = 20 by the cost model too.  The host allows 20 only
 // where no merged launch can take the scan (no inter blocks) and the fp16
 // bias of row 19 fits, and picks it only for affine gaps (the linear cell
 // lost 35 % at 20 on C5: its cheaper steps need the third wave per SIMD).
-int intra_x2_rows_for(int qlen, int longest, int wide = 0);
+int intra_x2_rows_for(int qlen, int longest, int wide, int forced);
 
 // Traceback of chosen hits (sw_align.hip): cpu.cpp's tie rules for a linear
 // gap (gap == gap_extend), this build's extension of them for affine gaps.
@@ -310,7 +338,7 @@ struct AlignArgs {
     int32_t gap_extend;        // each further residue (== gap: linear)
     uint8_t* dirs;             // per hit: (qlen + slen + 1) x (qlen + 1) direction bytes
     const int64_t* dirs_off;   // per hit offset into dirs
-    int32_t* hbuf;             // per hit: 3 x (qlen + 1) int32 diagonal scratch
+    int32_t* hbuf;             // per hit: 3 x (qlen + 1) int32 diagonal scratch for linear gaps, 7 x (qlen + 1) when gap_extend != gap (sw_align_affine: H x3, E x2, F x2)
     int32_t* out;              // per hit: score, q_begin, q_end, s_begin, s_end, ops_len
     char* ops;                 // per hit: ops_stride bytes (may be null)
     int64_t ops_stride;

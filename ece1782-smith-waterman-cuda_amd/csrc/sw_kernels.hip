@@ -174,15 +174,9 @@ __global__ __launch_bounds__(256) void sw_inter_coop(InterArgs a) {
 constexpr int kCoopRows = 32;
 int inter_coop_rows() { return kCoopRows; }
 
-static bool coop_skew() {
-    const char* e = std::getenv("SW_COOP_SKEW");
-    return !(e && e[0] == '0');
-}
-
-hipError_t launch_inter_coop(const InterArgs& a, int ncoop, bool affine, hipStream_t s) {
+hipError_t launch_inter_coop(const InterArgs& a, int ncoop, bool affine, bool sk, hipStream_t s) {
     if (ncoop <= 0 || a.qpad <= 0) return hipSuccess;
     const dim3 grid(ncoop), block(kWavesPerWG * kLanes);
-    const bool sk = coop_skew();
     if (affine && sk) hipLaunchKernelGGL((sw_inter_coop<kCoopRows, true, true>), grid, block, 0, s, a);
     else if (affine) hipLaunchKernelGGL((sw_inter_coop<kCoopRows, true, false>), grid, block, 0, s, a);
     else if (sk) hipLaunchKernelGGL((sw_inter_coop<kCoopRows, false, true>), grid, block, 0, s, a);
@@ -208,10 +202,9 @@ __global__ __launch_bounds__(64) void sw_intra(IntraArgs a) {
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-// Inter-kernel shape: R query rows per strip x SG columns per software-
-// pipelined sub-group.  SW_INTER_VARIANT="RxSG" overrides (tuning only).
-struct InterShape { int R, SG; bool x2s = false; bool f16 = false; };
-static InterShape inter_shape(bool affine, int x2_ok) {
+// Inter-kernel shape (sw_kernels.h InterShape); o.inter_variant "RxSG"
+// overrides (tuning only).
+InterShape inter_shape(bool affine, int x2_ok, const sw_opts& o) {
     // measured on MI355X (scripts/tune_inter.py, profiles/r01_tune_inter*.jsonl,
     // r01_x2s/): int16-safe scans (the common case) run the packed two-strips-
     // per-lane kernel sw_inter_x2s, one subject per lane, in its fp16 form
@@ -219,17 +212,15 @@ static InterShape inter_shape(bool affine, int x2_ok) {
     // always guarded (rescue chain fp16 -> int16 -> int32).  Otherwise int32:
     // affine 32x8, linear 64x8 (+ the cooperative kernel for wide blocks).
     // Beyond the static int16 bound the packed kernel runs guarded (blocks
-    // reaching kSat16 are re-scored at int32); SW_INT16_GUARD=0 disables that.
-    // x2_ok: 2 = int16 provably exact, 1 = guarded int16 allowed, 0 = int32 only
+    // reaching kSat16 are re-scored at int32); o.int16_guard = 0 disables that.
     // (Measured slower and removed in round 2: 16-bit-value and int32-profile
     // one-subject kernels, pair-table packing, two subjects per lane, the
     // column-skewed int32 kernel; their numbers are in profiles/r01_tune_*.)
-    const char* ge = std::getenv("SW_INT16_GUARD");
-    const bool y_ok = x2_ok == 2 || (x2_ok == 1 && !(ge && ge[0] == '0'));
+    const bool y_ok = x2_ok == 2 || (x2_ok == 1 && o.int16_guard != 0);
     InterShape v = y_ok ? InterShape{64, 8, true, true} : InterShape{affine ? 32 : 64, 8};
-    // SW_INTER_VARIANT (tests / A-B only): "RxSG" int32 (32x8, 64x8),
+    // o.inter_variant (tests / A-B only): "RxSG" int32 (32x8, 64x8),
     // "y32x8" the int16 two-strips kernel, "f32x8" / "f32x4" its fp16 form
-    if (const char* e = std::getenv("SW_INTER_VARIANT")) {
+    if (const char* e = o.inter_variant; e[0]) {
         int r = 0, g = 0;
         if (std::sscanf(e, "f%dx%d", &r, &g) == 2 && y_ok && r == 32 && (g == 8 || (g == 4 && affine)))
             v = InterShape{2 * r, g, true, true};
@@ -241,32 +232,7 @@ static InterShape inter_shape(bool affine, int x2_ok) {
     return v;
 }
 
-int inter_rows(bool affine, int x2_ok) { return inter_shape(affine, x2_ok).R; }
-bool inter_uses_x2(bool affine, int x2_ok) { return inter_shape(affine, x2_ok).x2s; }
-
-bool inter_needs_rescue(bool affine, int x2_ok) {
-    const InterShape v = inter_shape(affine, x2_ok);
-    return v.f16 || (v.x2s && x2_ok != 2);
-}
-
-bool inter_uses_f16(bool affine, int x2_ok) { return inter_shape(affine, x2_ok).f16; }
-
-bool inter_has_pair(bool affine, int x2_ok) {
-    const InterShape v = inter_shape(affine, x2_ok);
-    return v.x2s && v.R == 64 && v.SG == 8;
-}
-
-
-
-int inter_coop_divisor(bool affine, int x2_ok) {
-    // blocks at least residues / divisor columns wide go to the cooperative
-    // kernel; 0 = none.  One subject per lane with two strips per pass has
-    // no long single-wave tail (measured: coop on/off within 1 %).
-    return inter_shape(affine, x2_ok).x2s ? 0 : 530000;
-}
-
-const char* inter_kernel_name(bool affine, int x2_ok) {
-    const InterShape v = inter_shape(affine, x2_ok);
+const char* inter_kernel_name(const InterShape& v, bool affine) {
     if (v.x2s) {
         static thread_local char b2[64];
         std::snprintf(b2, sizeof b2, "sw_inter_x2s<%d,%d,%s%s>", v.R / 2, v.SG, affine ? "affine" : "linear",
@@ -308,11 +274,10 @@ int intra_rows_for(int qlen, int longest) {
 
 int intra_chunk_bytes(int ri) { return kProfileRows * kLanes * intra_rip(ri); }
 
-hipError_t launch_inter(const InterArgs& a, bool affine, int x2_ok, hipStream_t s) {
+hipError_t launch_inter(const InterArgs& a, bool affine, const InterShape& v, hipStream_t s) {
     if (a.nblocks - a.blk_first <= 0 || a.qpad <= 0) return hipSuccess;
     const dim3 grid((a.nblocks - a.blk_first + kWavesPerWG - 1) / kWavesPerWG);
     const dim3 block(kWavesPerWG * kLanes);
-    const InterShape v = inter_shape(affine, x2_ok);
     if (v.x2s) return launch_inter_x2s(a, v.R / 2, v.SG, affine, v.f16, s);
 #define SW_LAUNCH_INTER(R_, SG_)                                                                         \
     if (v.R == R_ && v.SG == SG_) {                                                                      \

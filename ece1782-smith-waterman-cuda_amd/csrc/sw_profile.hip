@@ -4,7 +4,8 @@
 // The reference builds nothing per query: its kernel reads the BLOSUM50 table
 // and the query from __constant__ memory (SWSolver.cu:54-81, 296-299, 246),
 // one lookup per cell.  Here every scan kernel reads a per-query profile
-// (prof[code][row] = S[q_row][code], + the gap for the linear kernels), so a
+// (prof[stored code][row] = S[q_row][code], + the gap for the linear kernels;
+// the database stores code c as kStored[c], sw_kernels.h), so a
 // scan starts by building it.  Built on the host and copied, each scan paid
 // an H2D copy on the DMA engine plus the compute queue's wait for it, ~30-40
 // us between two scans (rocprofv3 trace of C2's 1/8 share, profiles/r03_trace/);
@@ -23,9 +24,10 @@ __global__ __launch_bounds__(256) void sw_build_profile(ProfileArgs a) {
     const int n = a.row1 - a.row0;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
     if (tid >= kProfileRows * n) return;
-    const int c = tid / n;
+    const int c = tid / n;  // the profile row: a STORED code (sw_kernels.h kStored)
     const int i = a.row0 + tid % n;
-    const int v = (c >= kAlphabet || i >= a.qlen) ? a.bias : a.mat[kAlphabet * a.q[i - a.row0] + c] + a.bias;
+    const int v =
+        (c >= kAlphabet || i >= a.qlen) ? a.bias : a.mat[kAlphabet * a.q[i - a.row0] + kCodeOf[c]] + a.bias;
     if (i < a.stride) {
         const size_t k = static_cast<size_t>(c) * a.stride + i;
         a.p8[k] = static_cast<int8_t>(v);

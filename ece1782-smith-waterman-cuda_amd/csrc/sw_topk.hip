@@ -3,24 +3,31 @@
 //
 // Hits are ordered by score descending, then global id ascending; both fold
 // into one int64 key (score << 32 | (2^31 - 1 - id)) sorted descending.
-// Radix select: a workgroup holds a chunk of 16,384 keys in registers (1,024
-// threads x 16), finds its k-th largest key with 8-bit digit histograms in
+// Radix select: a workgroup holds a chunk of keys in registers (16 per
+// thread: 4,096 keys for 256 threads, 16,384 for 1,024), finds its k-th largest key with 8-bit digit histograms in
 // LDS — starting at the highest bit where the chunk's keys differ, stopping
 // as soon as the keys left at the chosen digit are exactly the ones still
 // needed — and writes the k keys at or above it (equal keys, i.e. padding,
 // by ticket).  The stage repeats on the survivors (chunks x k keys) until one
 // chunk remains, whose workgroup also sorts its k keys (bitonic in LDS).  No
-// host synchronisation: every stage's size is known from n and k.  For C2
-// (570k scores, k = 100) that is 2 launches of ~4 passes each, where the
-// previous bitonic sort of 2,048-key chunks took 3 launches x 39 us.
+// host synchronisation: every stage's size is known from n and k.
+//
+// Workgroup size: the ranking runs beside the next scan (bench.py's exchange
+// stream), whose workgroups hold every CU with 2 waves per SIMD at 256 VGPRs
+// each.  A 1,024-thread workgroup (4 waves per SIMD at 66 VGPRs, 72 with the
+// allocation granule) fits nowhere until the scan's grid has drained: its
+// kernel traces showed the ranking's first stage taking a whole scan (6.15 ms
+// on C2).  For k <= 1,024 the stages run 256-thread workgroups (one wave per
+// SIMD), which fit in the registers one finished scan workgroup leaves:
+// C2 (570k scores, k = 100) ranks in 3 launches (140 chunks, 4, 1); larger k
+// keeps 1,024 threads (a stage must keep fewer keys than it reads).
 #include "sw_kernels.h"
 
 namespace swk {
 
-constexpr int kTopkThreads = 1024;
-constexpr int kTopkPer = 16;                             // keys per thread
-constexpr int kTopkChunk = kTopkThreads * kTopkPer;      // keys per workgroup
+constexpr int kTopkPer = 16;      // keys per thread
 constexpr int kTopkMaxK = 4096;
+constexpr int kTopkSmallK = 1024;  // k up to this: 256-thread workgroups (4,096-key chunks)
 constexpr int64_t kKeyPad = INT64_MIN;
 
 __device__ __forceinline__ int64_t make_key(int32_t score, int64_t id) {
@@ -41,7 +48,7 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
 // database holds scattered global ids; BY_ID: entry i is scores[ids[i]], the
 // score array of a scan, indexed by result id); otherwise they come from
 // in_keys.  FINAL: one workgroup, sorted output.
-template <bool FINAL, bool BY_ID = false>
+template <int kTopkThreads, bool FINAL, bool BY_ID = false>
 __global__ __launch_bounds__(kTopkThreads) void sw_topk_select(const int32_t* __restrict__ in_scores,
                                                               const int64_t* __restrict__ in_keys, int64_t n,
                                                               int64_t id_base, const int32_t* __restrict__ ids,
@@ -50,6 +57,7 @@ __global__ __launch_bounds__(kTopkThreads) void sw_topk_select(const int32_t* __
     __shared__ uint64_t red[2][kTopkThreads / 64];
     __shared__ int ctl[5];  // digit, keys above it, keys at it, output slot, tie ticket
     __shared__ int64_t sorted[FINAL ? kTopkMaxK : 1];
+    constexpr int kTopkChunk = kTopkThreads * kTopkPer;  // keys per workgroup
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int64_t start = static_cast<int64_t>(blockIdx.x) * kTopkChunk;
     const int m = static_cast<int>(min(static_cast<int64_t>(kTopkChunk), n - start));  // keys in this chunk
@@ -189,33 +197,37 @@ __global__ __launch_bounds__(kTopkThreads) void sw_topk_select(const int32_t* __
     }
 }
 
+static int64_t topk_chunk(int k) { return (k <= kTopkSmallK ? 256 : 1024) * kTopkPer; }
+
 // Workspace bytes sw_topk_device needs for n inputs and k outputs.
 size_t topk_workspace_bytes(int64_t n, int k) {
     size_t total = 0;
     int64_t cur = n;
-    while (cur > kTopkChunk) {
-        const int64_t chunks = (cur + kTopkChunk - 1) / kTopkChunk;
+    const int64_t chunk = topk_chunk(k);
+    while (cur > chunk) {
+        const int64_t chunks = (cur + chunk - 1) / chunk;
         cur = chunks * k;
         total += static_cast<size_t>(cur) * sizeof(int64_t);
     }
     return total + 256;
 }
 
-hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, const int32_t* ids,
-                       int k, int64_t* out, int64_t* work, hipStream_t s, bool by_id) {
-    if (k <= 0 || k > kTopkMaxK || (by_id && (!scores || !ids))) return hipErrorInvalidValue;
+template <int T>
+static hipError_t launch_topk_t(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base,
+                                const int32_t* ids, int k, int64_t* out, int64_t* work, hipStream_t s, bool by_id) {
+    constexpr int64_t chunk = T * kTopkPer;
     const int32_t* sc = scores;
     const int64_t* kin = keys;
     int64_t cur = n;
     int64_t* w = work;
-    while (cur > kTopkChunk) {  // each stage keeps k of every 16,384 keys (k <= 4,096)
-        const int64_t chunks = (cur + kTopkChunk - 1) / kTopkChunk;
+    while (cur > chunk) {  // each stage keeps k of every chunk's keys (k <= chunk / 4)
+        const int64_t chunks = (cur + chunk - 1) / chunk;
         if (sc && by_id)
-            hipLaunchKernelGGL((sw_topk_select<false, true>), dim3(static_cast<unsigned>(chunks)), dim3(kTopkThreads),
-                               0, s, sc, kin, cur, id_base, ids, k, w);
+            hipLaunchKernelGGL((sw_topk_select<T, false, true>), dim3(static_cast<unsigned>(chunks)), dim3(T), 0, s, sc,
+                               kin, cur, id_base, ids, k, w);
         else
-            hipLaunchKernelGGL((sw_topk_select<false>), dim3(static_cast<unsigned>(chunks)), dim3(kTopkThreads), 0, s,
-                               sc, kin, cur, id_base, ids, k, w);
+            hipLaunchKernelGGL((sw_topk_select<T, false>), dim3(static_cast<unsigned>(chunks)), dim3(T), 0, s, sc, kin,
+                               cur, id_base, ids, k, w);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         sc = nullptr;
@@ -224,12 +236,18 @@ hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, in
         w += cur;
     }
     if (sc && by_id)
-        hipLaunchKernelGGL((sw_topk_select<true, true>), dim3(1), dim3(kTopkThreads), 0, s, sc, kin, cur, id_base, ids,
-                           k, out);
+        hipLaunchKernelGGL((sw_topk_select<T, true, true>), dim3(1), dim3(T), 0, s, sc, kin, cur, id_base, ids, k, out);
     else
-        hipLaunchKernelGGL((sw_topk_select<true>), dim3(1), dim3(kTopkThreads), 0, s, sc, kin, cur, id_base,
+        hipLaunchKernelGGL((sw_topk_select<T, true>), dim3(1), dim3(T), 0, s, sc, kin, cur, id_base,
                            sc ? ids : nullptr, k, out);
     return hipGetLastError();
+}
+
+hipError_t launch_topk(const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base, const int32_t* ids,
+                       int k, int64_t* out, int64_t* work, hipStream_t s, bool by_id) {
+    if (k <= 0 || k > kTopkMaxK || (by_id && (!scores || !ids))) return hipErrorInvalidValue;
+    return k <= kTopkSmallK ? launch_topk_t<256>(scores, keys, n, id_base, ids, k, out, work, s, by_id)
+                            : launch_topk_t<1024>(scores, keys, n, id_base, ids, k, out, work, s, by_id);
 }
 
 }  // namespace swk

@@ -34,7 +34,7 @@ _HANDLE = None
 def default_handle():
     global _HANDLE
     if _HANDLE is None:
-        _HANDLE = capi.Handle(0)
+        _HANDLE = capi.Handle(0, env_opts=False)
     return _HANDLE
 
 

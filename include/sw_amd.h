@@ -52,6 +52,9 @@ extern "C" {
 #define SW_E_NODEVICE -4  /* no HIP device / kernel image for this GPU */
 #define SW_E_UNSUPPORTED -5 /* valid request this build does not implement */
 #define SW_E_IO -6          /* file could not be read / written / validated */
+#define SW_E_DEVICE -7      /* a kernel reported an internal fault: the scores of the
+                               handle's scans since the last successful call are not
+                               trusted (see sw_last_error) */
 
 #define SW_ALPHABET 25    /* residue codes 0..24 */
 #define SW_CODE_STAR 24
@@ -136,6 +139,51 @@ SW_API void* sw_stream(sw_handle* h);
 /* Use an external stream (e.g. torch's current stream); NULL = own stream. */
 SW_API int sw_set_stream(sw_handle* h, void* hip_stream);
 
+/* ---- kernel-form overrides ------------------------------------------------
+ * The reference fixes every algorithm parameter at compile time (#defines,
+ * SWSolver.cu:7,43-50).  This library chooses its kernel forms per scan from
+ * the query, the database and the scoring; sw_opts overrides those choices
+ * for tests and A/B measurements.  Scores never depend on it: every form is
+ * bit-exact.  Every field is -1 (the library's own choice) after
+ * sw_opts_init; a handle starts with those values.  The library reads no
+ * environment variable on its scan path: sw_opts_from_env is the one place
+ * the SW_* variables are read (test and measurement scripts call it).    */
+typedef struct sw_opts {
+    int32_t size;             /* sizeof(sw_opts), set by sw_opts_init (ABI check) */
+    int32_t lpt;              /* 1: one merged longest-first launch (sw_scan_lpt)
+                                 whenever the scan's shape allows it; 0: never  SW_LPT */
+    int32_t lpt_pipe;         /* long-subject pairs the merged launch runs in the
+                                 pipelined form (query chunk per wave)          SW_LPT_PIPE */
+    int32_t quad_width;       /* inter blocks at least this wide run by wave quads
+                                 in the merged launch (0: none)                SW_QUAD_WIDTH */
+    int32_t pair_width;       /* ... by wave pairs (0: none)                   SW_PAIR_WIDTH */
+    int32_t pair_group;       /* waves per group (2 or 4) of the separate pair
+                                 launch                                        SW_PAIR_GROUP */
+    int32_t coop_width;       /* blocks at least this wide go to the cooperative
+                                 int32 kernel (int32 scans)                    SW_COOP_WIDTH */
+    int32_t coop_skew;        /* 0: the cooperative kernel without its skew    SW_COOP_SKEW */
+    int32_t intra_x2;         /* 0: long subjects in int32 only                SW_INTRA_X2 */
+    int32_t intra_x2_rows;    /* rows per lane of the packed intra kernel
+                                 (4, 6, 8, 10, 12, 16, 20)                     SW_INTRA_X2_RI */
+    int32_t intra_i16_first;  /* 0 / 1: never / always run the long subjects'
+                                 int16 form first (default: adaptive)          SW_INTRA_I16_FIRST */
+    int32_t inter_i16_span;   /* the widest n blocks in int16 first (0: none;
+                                 default: adaptive)                            SW_INTER_I16_SPAN */
+    int32_t int16_guard;      /* 0: int32 beyond the static int16 bound        SW_INT16_GUARD */
+    int32_t rescue_stats;     /* 1: print what the guard bands flagged per scan
+                                 (synchronises)                                SW_RESCUE_STATS */
+    char inter_variant[16];   /* inter kernel shape: "" (auto), "32x8", "64x8"
+                                 (int32), "y32x8" (int16 two-strips), "f32x8",
+                                 "f32x4" (its fp16 form)                       SW_INTER_VARIANT */
+    char trace_file[256];     /* per-workgroup timeline of the merged launch
+                                 (builds with -DSW_TRACE_BLOCKS only; "" off)  SW_TRACE_FILE */
+} sw_opts;
+SW_API int sw_opts_init(sw_opts* o);
+/* sw_opts_init, then every field whose SW_* variable (above) is set. */
+SW_API int sw_opts_from_env(sw_opts* o);
+SW_API int sw_set_opts(sw_handle* h, const sw_opts* o);
+SW_API int sw_get_opts(const sw_handle* h, sw_opts* o);
+
 /* ---- database -----------------------------------------------------------
  * Replaces the per-call packing loop SWSolver.cu:301-371 (longest-first
  * 32-lane interleave into managed memory, re-done on every query): the
@@ -180,6 +228,14 @@ SW_API int sw_db_subjects(const sw_db* db, int64_t* lengths, int32_t* ids);
  * under 64,000 subjects with a mean length >= 256 (too few 64-subject blocks
  * to fill the GPU).  May be changed between scans (re-packs the database). */
 SW_API int sw_db_set_long_threshold(sw_db* db, int32_t threshold);
+/* A database learns from the flagged counts its scans read back (without
+ * waiting) which work to run in int16 first: the widest blocks and the long
+ * subjects, per scoring and query length (sw_opts inter_i16_span and
+ * intra_i16_first override it).  Scores never depend on that state; which
+ * kernels a scan runs does.  This forgets it (and any readback in flight),
+ * so the next scan runs as on a fresh database: a caller can time a cold
+ * and a warm scan deliberately.                                            */
+SW_API int sw_db_reset_adaptive(sw_db* db);
 
 /* ---- scans ---------------------------------------------------------------
  * Replaces smith_waterman_cuda (SWSolver.cu:266-404): score the encoded

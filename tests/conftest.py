@@ -29,9 +29,28 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def handle(sw):
-    h = sw.Handle(0)
+    # the library's own kernel choices, whatever SW_* variables are set
+    h = sw.Handle(0, env_opts=False)
     yield h
     h.close()
+
+
+@pytest.fixture
+def knobs(handle):
+    """knobs(field=value, ...): sw_opts overrides on the session handle for
+    one test (include/sw_amd.h field names; a string value is converted,
+    "" = the library's choice), restored afterwards."""
+    saved = handle.get_opts()
+
+    def set_(**kw):
+        conv = {}
+        for k, v in kw.items():
+            if isinstance(v, str) and k not in ("inter_variant", "trace_file"):
+                v = int(v) if v.strip() else -1
+            conv[k] = v
+        handle.set_opts(**conv)
+    yield set_
+    handle.set_opts(saved)
 
 
 def read_query(name):

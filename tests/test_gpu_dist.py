@@ -27,7 +27,7 @@ def _worker(rank, world, port, q):
     sw = _swpkg.load()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    h = sw.Handle(0)
+    h = sw.Handle(0, env_opts=False)
     qc = sw.encode(read_query(QUERY))
     mat = sw.capi.builtin_matrix(1)
     r, o = _db(sw)

@@ -17,11 +17,11 @@ def test_overlapped_scan_and_topk(sw, oracle, scoring):
     dev = torch.device("cuda", 0)
     res, offs = sw.synth.database(8000, shard=31)
     n = len(offs) - 1
-    h = sw.Handle(0)
+    h = sw.Handle(0, env_opts=False)
     stream = torch.cuda.Stream(dev)
     h.set_stream(stream.cuda_stream)
     xstream = torch.cuda.Stream(dev, priority=-1)
-    xh = sw.Handle(0)
+    xh = sw.Handle(0, env_opts=False)
     xh.set_stream(xstream.cuda_stream)
     db = sw.Database(h, res, offs)
     m = sw.capi.builtin_matrix(mid)

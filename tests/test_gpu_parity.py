@@ -164,7 +164,7 @@ def test_long_query_self_hit_int32(sw, oracle, handle):
 @pytest.mark.parametrize("mid,go,ge,ww,reps", [(0, 2, 2, 15, 2100), (0, 2, 2, 15, 2190), (0, 2, 2, 15, 2300),
                                               (1, 12, 1, 11, 2870), (1, 12, 1, 11, 2990), (1, 12, 1, 11, 3100)])
 @pytest.mark.parametrize("variant", ["", "f32x8"])
-def test_int16_saturation_rescue(sw, oracle, handle, monkeypatch, mid, go, ge, ww, reps, variant):
+def test_int16_saturation_rescue(sw, oracle, handle, knobs, mid, go, ge, ww, reps, variant):
     """Scores at/above the 16-bit kernels' saturation guard are re-scored at
     int32 (block-level rescue), next to ordinary subjects in the same block;
     linear (BLOSUM50, W-W = 15) and affine (BLOSUM62, W-W = 11) scoring."""
@@ -217,12 +217,15 @@ def test_device_topk(sw, handle, n, k):
 
 
 @pytest.mark.parametrize("n,k,dist", [(2_000_000, 4096, "ties"), (200_000, 300, "wide"), (50_000, 100, "equal"),
-                                      (16_384, 100, "ties"), (16_385, 4096, "wide"), (1, 1, "ties")])
+                                      (16_384, 100, "ties"), (16_385, 4096, "wide"), (1, 1, "ties"),
+                                      (4_096, 100, "ties"), (4_097, 1024, "wide"), (570_000, 100, "ties"),
+                                      (300_000, 1024, "ties"), (300_000, 1025, "equal")])
 def test_device_topk_radix_select(sw, handle, n, k, dist):
     """The radix select's corners: scores over the whole int32 range
     ("wide"), one score for every subject ("equal": the order is the ids
-    alone), many ties; chunk-size boundaries (16,384 keys per workgroup), the
-    largest k, three stages (2M scores)."""
+    alone), many ties; chunk-size boundaries (4,096 keys per 256-thread
+    workgroup for k <= 1,024, 16,384 per 1,024-thread workgroup above), the
+    largest k, three stages (2M scores; C2's 570,000 at k = 100)."""
     import torch
     rng = np.random.default_rng(n ^ k)
     if dist == "wide":
@@ -251,13 +254,13 @@ INTER_VARIANTS = ["32x8", "64x8", "y32x8", "f32x8", "f32x4"]
 
 @pytest.mark.parametrize("variant", INTER_VARIANTS)
 @pytest.mark.parametrize("coop", ["0", "128:0", "128:1"])
-def test_inter_variants_vs_oracle(sw, oracle, handle, monkeypatch, variant, coop):
+def test_inter_variants_vs_oracle(sw, oracle, handle, knobs, variant, coop):
     """Every inter-kernel shape with the cooperative wide-block kernel off /
     on (plain) / on (skewed), linear and affine."""
     width, _, skew = coop.partition(":")
-    monkeypatch.setenv("SW_INTER_VARIANT", variant)
-    monkeypatch.setenv("SW_COOP_WIDTH", width)
-    monkeypatch.setenv("SW_COOP_SKEW", skew or "1")
+    knobs(inter_variant=variant)
+    knobs(coop_width=width)
+    knobs(coop_skew=skew or "1")
     r, o = sw.synth.database(900, shard=11)
     db = sw.Database(handle, r, o, long_threshold=1500)
     for qlen, mid, go, ge in [(375, 0, 2, 2), (150, 1, 12, 1), (97, 1, 11, 2)]:
@@ -270,13 +273,13 @@ def test_inter_variants_vs_oracle(sw, oracle, handle, monkeypatch, variant, coop
 
 @pytest.mark.parametrize("guard", ["1", "0"])
 @pytest.mark.parametrize("variant", ["", "y32x8"])
-def test_long_query_int16_guard(sw, oracle, handle, monkeypatch, variant, guard):
+def test_long_query_int16_guard(sw, oracle, handle, knobs, variant, guard):
     """A query long enough that (qlen + 2) * (max S + gap open) >= 32767: the
-    two-strips kernel runs guarded (SW_INT16_GUARD unset / 1) or the int32
-    kernel runs (SW_INT16_GUARD=0).  Scores stay exact either way."""
-    monkeypatch.setenv("SW_INT16_GUARD", guard)
+    two-strips kernel runs guarded (sw_opts int16_guard auto / 1) or the
+    int32 kernel runs (int16_guard 0).  Scores stay exact either way."""
+    knobs(int16_guard=guard)
     if variant:
-        monkeypatch.setenv("SW_INTER_VARIANT", variant)
+        knobs(inter_variant=variant)
     r, o = sw.synth.database(300, shard=5)
     q = sw.synth.query(2400, shard=9)
     # plant the query itself as a subject so one score is large
@@ -296,7 +299,7 @@ def test_long_query_int16_guard(sw, oracle, handle, monkeypatch, variant, guard)
             assert k.startswith("sw_inter_x2s"), k
 
 
-def test_default_kernel_selection(sw, handle, monkeypatch):
+def test_default_kernel_selection(sw, handle, knobs):
     """int16-safe scans run the packed two-strips-per-lane kernel; longer
     queries run it guarded; gaps too large for the guard band, or the guard
     switched off, run the int32 kernels."""
@@ -313,7 +316,7 @@ def test_default_kernel_selection(sw, handle, monkeypatch):
     # max S + gap open >= 1000: int32
     db.scan(q, sw.capi.builtin_matrix(0), 1000, 1)
     assert handle.last_kernel() == "sw_inter<32,8,affine>"
-    monkeypatch.setenv("SW_INT16_GUARD", "0")
+    knobs(int16_guard="0")
     db.scan(q, sw.capi.builtin_matrix(0), 100, 100)
     assert handle.last_kernel() == "sw_inter<64,8,linear>"
 
@@ -401,7 +404,7 @@ def test_db_save_load_roundtrip(sw, oracle, handle, tmp_path):
 
 @pytest.mark.parametrize("scoring", [(1, 12, 1), (0, 2, 2), (1, 14, 3), (0, 5, 5)])
 @pytest.mark.parametrize("qlen,selfhit", [(375, True), (900, True), (2400, False)])
-def test_fp16_guard_band(sw, oracle, handle, monkeypatch, qlen, selfhit, scoring):
+def test_fp16_guard_band(sw, oracle, handle, knobs, qlen, selfhit, scoring):
     """The fp16 kernels (biased cells: stored values sit up to 26 ge above
     the true ones, all of them offset by -2048 + 2 ge) are exact below
     4096 - 2 ge - 2 max S - 26 ge and flag their block otherwise: subjects
@@ -410,7 +413,7 @@ def test_fp16_guard_band(sw, oracle, handle, monkeypatch, qlen, selfhit, scoring
     4,655-5,932) next to ordinary ones, affine (BLOSUM62 11/1 and 13/3) and
     linear (BLOSUM50, gap 2 and 5) against the oracle."""
     mid, go, ge = scoring
-    monkeypatch.setenv("SW_INTER_VARIANT", "f32x8")
+    knobs(inter_variant="f32x8")
     r, o = sw.synth.database(300, shard=qlen)
     q = sw.synth.query(qlen, shard=qlen + 5)
     extra = [q[: qlen // 2], q] if selfhit else [q[:400], q[:190]]
@@ -428,16 +431,16 @@ def test_fp16_guard_band(sw, oracle, handle, monkeypatch, qlen, selfhit, scoring
 @pytest.mark.parametrize("variant", ["f32x8", "y32x8"])
 @pytest.mark.parametrize("width", ["16", "300"])
 @pytest.mark.parametrize("group", ["2", "4"])
-def test_wave_pair_kernel(sw, oracle, handle, monkeypatch, variant, width, group):
+def test_wave_pair_kernel(sw, oracle, handle, knobs, variant, width, group):
     """sw_inter_x2p (the widest blocks by wave pairs or quads; width 16 =
     every block): 1 to 15 passes (odd and even counts, fewer passes than
     waves), narrow blocks (the 6- / 12-tick period floor), a block count not
     a multiple of the groups per workgroup, linear and affine, and planted
     near-copies of the query whose blocks the fp16 kernel flags for the
     rescue chain — all against the oracle."""
-    monkeypatch.setenv("SW_INTER_VARIANT", variant)
-    monkeypatch.setenv("SW_PAIR_WIDTH", width)
-    monkeypatch.setenv("SW_PAIR_GROUP", group)
+    knobs(inter_variant=variant)
+    knobs(pair_width=width)
+    knobs(pair_group=group)
     r, o = sw.synth.database(1000, shard=17)
     q0 = sw.synth.query(900, shard=3)
     extra = [q0, q0[:450], q0[100:700]]
@@ -463,8 +466,8 @@ def test_wave_pair_kernel(sw, oracle, handle, monkeypatch, variant, width, group
 
 
 @pytest.mark.parametrize("packed,ri", [("1", ""), ("1", "6"), ("1", "10"), ("1", "20"), ("0", "")])
-def test_intra_two_subjects_per_wave(sw, oracle, handle, monkeypatch, packed, ri):
-    """sw_intra_x2 (two long subjects per wave, packed fp16; SW_INTRA_X2=0:
+def test_intra_two_subjects_per_wave(sw, oracle, handle, knobs, packed, ri):
+    """sw_intra_x2 (two long subjects per wave, packed fp16; intra_x2 0:
     int32 sw_intra only): rows per lane 4..20 by the cost model (query lengths
     40..2100, one to several chunk passes) or forced to the 2-row-element
     shapes 6 and 10 and to the widest, 20 rows by 6-wave workgroups (this
@@ -473,9 +476,9 @@ def test_intra_two_subjects_per_wave(sw, oracle, handle, monkeypatch, packed, ri
     linear and affine scoring, and planted near-copies of the query whose fp16
     maxima cross the fp16 bound (~4,000: cells offset by -2048 + 2 ge;
     re-scored by sw_intra in list mode)."""
-    monkeypatch.setenv("SW_INTRA_X2", packed)
+    knobs(intra_x2=packed)
     if ri:
-        monkeypatch.setenv("SW_INTRA_X2_RI", ri)
+        knobs(intra_x2_rows=ri)
     rng = np.random.default_rng(7)
     q0 = sw.synth.query(2100, shard=8)
     lens = rng.integers(70, 900, size=40)
@@ -499,7 +502,7 @@ def test_intra_two_subjects_per_wave(sw, oracle, handle, monkeypatch, packed, ri
 
 
 @pytest.mark.parametrize("order", ["", "0", "1"])
-def test_intra_rescue_chain_fp16_int16_int32(sw, oracle, handle, monkeypatch, order):
+def test_intra_rescue_chain_fp16_int16_int32(sw, oracle, handle, knobs, order):
     """The intra rescue chain end to end: sw_intra_x2 (fp16) flags subjects
     near its bound (4096 - 2 ge - 2 max S - 26 ge: cells offset by -2048 +
     2 ge) into list 1, its int16 form re-scores list 1 and flags those near
@@ -508,11 +511,11 @@ def test_intra_rescue_chain_fp16_int16_int32(sw, oracle, handle, monkeypatch, or
     score 2,300-7,100 (13 of the 19 above the bound); a planted copy of the
     6,500-aa query scores above 32767;
     ordinary subjects sit next to both in the same pairs.  The chain's order
-    (SW_INTRA_I16_FIRST): adaptive (int16 first once a scan with the same
+    (sw_opts intra_i16_first): adaptive (int16 first once a scan with the same
     scoring flagged over a third of the long subjects at a query no longer than
     this one), never, always."""
     if order:
-        monkeypatch.setenv("SW_INTRA_I16_FIRST", order)
+        knobs(intra_i16_first=order)
     rng = np.random.default_rng(11)
     q = sw.synth.query(6500, shard=21)
     lens = rng.integers(1500, 5500, size=17)
@@ -539,14 +542,14 @@ def test_intra_rescue_chain_fp16_int16_int32(sw, oracle, handle, monkeypatch, or
         assert ((want > 4096) & (want < 32000)).sum() >= (2 if ge == 2 else 1)
 
 
-def test_inter_widest_blocks_int16_first(sw, oracle, handle, monkeypatch):
+def test_inter_widest_blocks_int16_first(sw, oracle, handle, knobs):
     """Long queries whose scores against the widest blocks leave the fp16
     range (true scores up to ~4,000; here BLOSUM50 + 3 with linear gap 2,
     under which random 2,600 x 1,650 pairs score 4,900-8,200, while short
     subjects stay below 1,800) put those blocks in the fp16 guard band; once
     a scan has flagged most of blocks [0, span), later scans with queries at
     least as long run those blocks in int16 by wave pairs beside the fp16
-    launch (SW_INTER_I16_SPAN forces a span: one block, some, more than the
+    launch (sw_opts inter_i16_span forces a span: one block, some, more than the
     pair blocks, all of them; and under affine scoring).  Every scan
     bit-exact against the oracle."""
     r1, o1 = sw.synth.fixed_length_database(1280, 1650, 200, shard=41)
@@ -571,13 +574,13 @@ def test_inter_widest_blocks_int16_first(sw, oracle, handle, monkeypatch):
     assert np.array_equal(db.scan(q2, m, 2, 2), want2)
     assert "+int16" not in handle.last_kernel()       # shorter than any observation
     nblocks = db.stats()["n_blocks"]
-    monkeypatch.setenv("SW_PAIR_WIDTH", "2000")       # few pair blocks: spans beyond them
+    knobs(pair_width="2000")       # few pair blocks: spans beyond them
     for span in (1, 7, 25, nblocks):
-        monkeypatch.setenv("SW_INTER_I16_SPAN", str(span))
+        knobs(inter_i16_span=str(span))
         got = db.scan(q, m, 2, 2)
         assert np.array_equal(got, want), (span, np.nonzero(got != want)[0][:10])
         assert handle.last_kernel().endswith("+int16[0,%d)" % span)
-    monkeypatch.setenv("SW_INTER_I16_SPAN", "5")
+    knobs(inter_i16_span="5")
     m62 = sw.capi.builtin_matrix(1)
     want3 = oracle.scan(q2, r, o, mat=m62, gap_open=12, gap_extend=1)
     assert np.array_equal(db.scan(q2, m62, 12, 1), want3)
@@ -619,7 +622,7 @@ def test_random_scoring_and_shapes(sw, oracle, handle, case):
 
 @pytest.mark.parametrize("quad_width, pipe", [("0", "0"), ("200", "0"), ("16", "0"), ("200", "2"), ("0", "100")])
 @pytest.mark.parametrize("scoring", [(1, 12, 1), (0, 2, 2)])
-def test_merged_lpt_launch(sw, oracle, handle, monkeypatch, quad_width, pipe, scoring):
+def test_merged_lpt_launch(sw, oracle, handle, knobs, quad_width, pipe, scoring):
     """sw_scan_lpt (the inter blocks by quads / pairs / single waves and the
     long subjects' fp16 pass in one launch, longest work first): queries for
     the three intra shapes it supports (4, 6, 8 rows per lane), quads for
@@ -628,10 +631,10 @@ def test_merged_lpt_launch(sw, oracle, handle, monkeypatch, quad_width, pipe, sc
     subject, planted near-copies in both kernels' halves (rescued inside the
     merged launch), against the oracle and the two-launch form."""
     mid, go, ge = scoring
-    monkeypatch.setenv("SW_LPT", "1")
-    monkeypatch.setenv("SW_LPT_PIPE", pipe)
-    monkeypatch.setenv("SW_QUAD_WIDTH", quad_width)
-    monkeypatch.setenv("SW_PAIR_WIDTH", "64")
+    knobs(lpt="1")
+    knobs(lpt_pipe=pipe)
+    knobs(quad_width=quad_width)
+    knobs(pair_width="64")
     r, o = sw.synth.database(2500, shard=23)
     q0 = sw.synth.query(500, shard=8)
     extra = [q0, q0[:300], np.concatenate([q0, q0])]  # a long near-copy goes to the intra half
@@ -645,15 +648,15 @@ def test_merged_lpt_launch(sw, oracle, handle, monkeypatch, quad_width, pipe, sc
         assert "+lpt" in handle.last_kernel(), handle.last_kernel()
         want = oracle.scan(q, r2, o2, mat=m, gap_open=go, gap_extend=ge)
         assert np.array_equal(got, want), (qlen, np.nonzero(got != want)[0][:10])
-        monkeypatch.setenv("SW_LPT", "0")
+        knobs(lpt="0")
         assert np.array_equal(db.scan(q, m, go, ge), got)
         assert "+lpt" not in handle.last_kernel()
-        monkeypatch.setenv("SW_LPT", "1")
+        knobs(lpt="1")
 
 
 @pytest.mark.parametrize("ri", ["4", "8"])
 @pytest.mark.parametrize("scoring", [(0, 2, 2), (0, 12, 1)])
-def test_merged_launch_drains_rescue_lists(sw, oracle, handle, monkeypatch, ri, scoring):
+def test_merged_launch_drains_rescue_lists(sw, oracle, handle, knobs, ri, scoring):
     """The merged launch re-scores what its fp16 cells flag inside the same
     launch (sw_scan_lpt's drain, no rescue launches after it): planted hits
     of every stage — inter blocks above the fp16 bound (int16 re-score) and
@@ -662,13 +665,13 @@ def test_merged_launch_drains_rescue_lists(sw, oracle, handle, monkeypatch, ri, 
     the oracle and the separate-launch form, twice (the lists' entries are
     reset by whoever takes them, so the second scan starts clean)."""
     mid, go, ge = scoring
-    monkeypatch.setenv("SW_LPT", "1")
-    monkeypatch.setenv("SW_INTRA_X2_RI", ri)
-    monkeypatch.setenv("SW_PAIR_WIDTH", "64")
+    knobs(lpt="1")
+    knobs(intra_x2_rows=ri)
+    knobs(pair_width="64")
     # keep the fp16-first order on the second scan (the adaptive routing would
     # send this many flagged blocks / subjects to int16 first)
-    monkeypatch.setenv("SW_INTER_I16_SPAN", "0")
-    monkeypatch.setenv("SW_INTRA_I16_FIRST", "0")
+    knobs(inter_i16_span="0")
+    knobs(intra_i16_first="0")
     W = sw.encode("W")[0]
     q = np.full(2300, W, dtype=np.uint8)  # W/W scores 15: 34,500 for a full copy
     r, o = sw.synth.database(2000, shard=41)
@@ -694,6 +697,51 @@ def test_merged_launch_drains_rescue_lists(sw, oracle, handle, monkeypatch, ri, 
         got = db.scan(q, m, go, ge)
         assert handle.last_kernel().endswith("+lpt+drain"), handle.last_kernel()
         assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
-    monkeypatch.setenv("SW_LPT", "0")
+    knobs(lpt="0")
     assert np.array_equal(db.scan(q, m, go, ge), want)
+    db.close()
+
+
+@pytest.mark.parametrize("scoring", [(0, 12, 1), (1, 12, 1)])
+def test_drain_waits_for_previous_deferred_tail(sw, oracle, handle, knobs, scoring):
+    """in a batch, a merged launch that drains its rescue
+    lists re-scores on the deferred tails' boundary rows, so it must not
+    overlap the rescue tail of a non-merged scan just before it.  A 2,300-aa
+    query that flagged most long subjects and the widest blocks routes later
+    queries at least as long int16-first (two launches, its rescue tail
+    deferred to the tail stream in a batch); a 1,500-aa query with the same
+    scoring still takes the merged launch and drains what it flags on the
+    same rows.  Batches alternating the two equal the oracle, query by
+    query."""
+    mid, go, ge = scoring
+    knobs(pair_width=64, intra_x2_rows=8)  # (the merged launch has the 4-, 6- and 8-row intra forms)
+    W = sw.encode("W")[0]
+    qa = np.full(2300, W, dtype=np.uint8)
+    qb = np.full(1500, W, dtype=np.uint8)
+    r, o = sw.synth.database(2000, shard=43)
+    rng = np.random.default_rng(43)
+
+    def planted(n, at, k):
+        s = sw.synth.query(n, shard=int(rng.integers(1 << 30)))
+        s[at:at + k] = W
+        return s
+    extra = [np.full(2300, W, np.uint8), planted(600, 100, 400), planted(2000, 50, 1800),
+             planted(2400, 0, 2400), np.full(2600, W, np.uint8), planted(3000, 900, 2000),
+             planted(2700, 10, 2290), planted(3200, 200, 2500), planted(2900, 5, 2800)]
+    r2 = np.concatenate([r] + extra)
+    o2 = np.concatenate([o, o[-1] + np.cumsum([len(x) for x in extra])])
+    db = sw.Database(handle, r2, o2, long_threshold=2500)
+    m = sw.capi.builtin_matrix(mid)
+    want = {len(q): oracle.scan(q, r2, o2, mat=m, gap_open=go, gap_extend=ge, nthreads=16) for q in (qa, qb)}
+    # the first scan of A is fp16-first (nothing observed yet) and teaches
+    # the database its int16-first routing for queries of >= 2,300 aa
+    assert np.array_equal(db.scan(qa, m, go, ge), want[2300])
+    assert np.array_equal(db.scan(qa, m, go, ge), want[2300])
+    assert "+lpt" not in handle.last_kernel(), handle.last_kernel()
+    assert np.array_equal(db.scan(qb, m, go, ge), want[1500])
+    assert handle.last_kernel().endswith("+lpt+drain"), handle.last_kernel()
+    for order in ([qa, qb, qa, qb], [qb, qa, qb, qa, qb], [qa, qa, qb, qb, qa, qb]):
+        out = db.scan_batch(order, m, go, ge)
+        for k, q in enumerate(order):
+            assert np.array_equal(out[k], want[len(q)]), (k, len(q), np.nonzero(out[k] != want[len(q)])[0][:10])
     db.close()
