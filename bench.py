@@ -128,7 +128,17 @@ def kernel_source_hash():
 
 
 def workload_key(args, qlen):
-    return "%s/%d/%d/%s-%d-%d" % (args.query, args.db_seqs, qlen, args.matrix, args.gap_open, args.gap_extend)
+    key = "%s/%d/%d/%s-%d-%d" % (args.query, args.db_seqs, qlen, args.matrix, args.gap_open, args.gap_extend)
+    return key if args.config == "c2" else args.config + ":" + key
+
+
+def traffic_entry(tj, key):
+    """The stored PMC measurement of a workload: pmc_traffic.json holds the
+    headline (C2) entry at its top level and every measured workload under
+    "workloads" (scripts/pmc_traffic.py --merge)."""
+    if tj.get("workload_key") == key:
+        return tj
+    return tj.get("workloads", {}).get(key)
 
 
 def host_cores():
@@ -786,6 +796,11 @@ def main():
         wave_gcups = float(qtot) / nq * wave_res / (wave_ms * 1e-3) / 1e9 if wave_ms > 0 else 0.0
         intra_res = residues - inter_res
         roof_kernel = kernel
+        if nq > 1 and "sw_inter_x2" in kernel and "+lpt" not in kernel:
+            # a batch (C3): the queries' inter scans run different forms
+            # (single waves for short queries, wave pairs for longer ones);
+            # the roofline covers them all, per query
+            roof_kernel = "sw_inter_x2* (per query of the batch)"
         if "+lpt" in kernel:
             # one merged launch (sw_scan_lpt) scans every subject: the inter
             # blocks and the long subjects' fp16 pass, longest work first
@@ -804,8 +819,8 @@ def main():
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if (args.config == "c2" and not args.shard_of and world == 1
-                    and tj.get("workload_key") == workload_key(args, qtot) and tj.get("kernel") == roof_kernel):
+            tj = traffic_entry(tj, workload_key(args, qtot)) or {}
+            if not args.shard_of and world == 1 and tj.get("kernel") == roof_kernel:
                 if tj.get("kernel_src_sha16") == kernel_source_hash():
                     traffic = tj.get("hbm_bytes_per_launch")
                     if tj.get("sq_insts_valu_per_launch") and tj.get("profiled_ns_per_launch") and kernel_ms > 0:
@@ -819,9 +834,11 @@ def main():
                         # fraction uses that one pass's clock AND duration
                         cyc = tj["grbm_gui_active_per_launch"] / 8
                         clk = cyc / tj["profiled_ns_per_launch"]  # GHz
-                        cells_launch = float(qtot) / nq * wave_res
+                        intra_dom = roof_kernel == intra_kernel
+                        cells_launch = float(qtot) / nq * (intra_res if intra_dom else wave_res)
+                        per128 = insts / (cells_launch / 128)
                         valu_hw = {"sq_insts_valu_per_launch": insts,
-                                   "valu_insts_per_128_cells": round(insts / (cells_launch / 128), 3),
+                                   "valu_insts_per_128_cells": round(per128, 3),
                                    "clock_ghz_under_load": round(clk, 3),
                                    "profiled_ms_per_launch": round(tj["profiled_ns_per_launch"] * 1e-6, 4),
                                    "cycles_per_valu_inst": 4.25,
@@ -829,6 +846,13 @@ def main():
                                    "issue_frac_4cyc": round(insts * 4.0 / (SIMDS * cyc), 4),
                                    "source": "stored rocprofv3 --pmc SQ pass (pmc_traffic.json), same kernel sources; "
                                              "instructions, cycles and duration all of that one profiled launch"}
+                        if intra_dom and "<" in roof_kernel:
+                            # a wave-step of sw_intra_x2<RI> is 64 lanes x RI rows x 2 subjects
+                            ri = int(roof_kernel.split("<")[1].split(">")[0].split(",")[0])
+                            valu_hw["valu_insts_per_wave_step"] = round(per128 * ri, 1)
+                        if tj.get("sq_lds_bank_conflict_per_launch") and tj.get("sq_active_inst_lds_per_launch"):
+                            valu_hw["lds_bank_conflict_cycles_per_lds_inst"] = round(
+                                tj["sq_lds_bank_conflict_per_launch"] / tj["sq_active_inst_lds_per_launch"], 3)
                     traffic_note = ("stored rocprofv3 --pmc measurement (FETCH_SIZE x2 + WRITE_SIZE) of this "
                                     "workload, taken on a build with the same kernel sources (%s, %s)"
                                     % (tj.get("kernel_src_sha16"), tj.get("measured", "?")))
@@ -880,7 +904,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": traffic, "traffic_note": traffic_note,
-                         "kernel": roof_kernel,
+                         "kernel": roof_kernel, "workload_key": workload_key(args, qtot),
                          "alg_bytes_per_launch": int(alg_bytes), "kernel_ms": round(kernel_ms, 4)},
             "valu_roofline": valu_roofline(roof_kernel, cells_all / world, kt["total_ms"] / nsc * nq, wave_gcups),
             "valu_hw": valu_hw,
