@@ -1567,7 +1567,7 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
         // an addition reads is a rebased row -1 H of bias -2 ge: exact)
         const int zero = -kF16Span + 2 * ge;
         x.sat_limit = kF16Span - zero - 2 * std::max(max_s, 1) - swk::intra_bias_rows(ri2) * ge;
-        for (int j = 0; j < 32; ++j) x.f16_step[j] = f16_pair(j * ge + zero);
+        for (int j = 0; j < swk::kIntraSteps; ++j) x.f16_step[j] = f16_pair(j * ge + zero);
         x.f16_zero = f16_pair(zero);
         x.f16_gog = f16_pair(go - ge);
         if (intra_i16_first) {

@@ -26,8 +26,9 @@
 //
 // Exactness: fp16 holds every integer up to 2048 (the cells are offset by
 // -2048 + 2 ge, so stored values span 4096).  H grows by at most max S per
-// cell and the biased values sit up to intra_bias_rows(RI) = max(26, RI + 10)
-// ge above the true ones, so a subject whose running maximum reaches
+// cell and the biased values sit up to intra_bias_rows(RI) = max(26, RI +
+// period + 2) ge above the true ones (the bias period is 8 steps, 16 at the
+// widest shape, RI 20: half the rebases), so a subject whose running maximum reaches
 // a.sat_limit = 4096 − 2 ge − 2·max S − intra_bias_rows(RI)·ge (computed
 // exactly) is appended to a.rescue_list.
 // The same kernel in int16 (IntraCell<false>, LIST) re-scores that list and
@@ -227,8 +228,9 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
     using Img = IntraImg<RI, F16>;
     using Elem = typename Img::Elem;
     constexpr int NQ = Img::kPer;    // image elements per lane and code
-    constexpr int NB = 8;            // steps per bias period (one rebase each)
+    constexpr int NB = intra_period(RI);  // steps per bias period (one rebase each)
     constexpr int NACC = RI + NB - 1;
+    static_assert(RI + NB + 1 <= kIntraSteps, "f16_step table");
     // profile prefetch distance in steps: the pipelined form's short affine
     // steps (RI 2) do not cover an LDS read's latency on a busy CU with one
     // (C2's 1/8 share +0.6 %; linear steps lost 3 % with 2, 6 % with 3)

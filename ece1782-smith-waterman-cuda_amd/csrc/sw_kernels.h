@@ -38,6 +38,9 @@ constexpr uint8_t kStored[26] = {11, 1, 5, 2, 22, 6, 14, 12, 23, 9, 10, 0, 24, 7
 // ... and its inverse: the code a stored byte stands for
 constexpr uint8_t kCodeOf[26] = {11, 1, 3, 16, 14, 2, 5, 13, 18, 9, 10, 0, 7, 19, 6, 15, 20, 21, 22, 23, 24, 17, 4, 8, 12, 25};
 constexpr int kWavesPerWG = 4;
+// f16_step entries the intra kernels read (IntraArgs): up to RI + the bias
+// period (intra_period) + 1
+constexpr int kIntraSteps = 40;
 
 // Shared by the inter kernels: one wave's residues for SG columns.
 template <int SG>
@@ -142,7 +145,7 @@ struct IntraArgs {
     int32_t prof_stride = 0;
     int32_t bias = 0;
     int32_t sat_limit = 0;       // flag subjects whose maximum reaches this
-    uint32_t f16_step[32] = {};  // as InterArgs: packed fp16 (j ge + z, j ge + z)
+    uint32_t f16_step[kIntraSteps] = {};  // as InterArgs (j ge + z, j ge + z), j < RI + period
     uint32_t f16_zero = 0;       // the offset z = -2048 + 2 ge of every fp16 cell value
     uint32_t f16_gog = 0;        // packed fp16 (go - ge, go - ge)
     int32_t* rescue_list = nullptr;
@@ -296,16 +299,25 @@ hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_
                            hipStream_t s, const DrainArgs* drain = nullptr);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.
 constexpr int kSat16 = 32767 - 1152;
-// The two-subjects intra kernel's biased cell stores values up to this many
-// gap extensions above the true ones at RI rows per lane (row RI - 1 at the
-// last step of a bias period, + 2 ge in the profile, + the F floor's step).
-constexpr int intra_bias_rows(int ri) { return ri + 10 > 26 ? ri + 10 : 26; }
-// Its widest shape: 20 rows per lane, in the same 4-wave workgroups: the
-// 26-code image of 1,280 rows (66.5 KB) leaves two workgroups per CU, 2
-// waves per SIMD.  (Measured on C5: 6-wave workgroups did not fit two per CU,
-// 2 + 2 + 1 + 1 waves per SIMD each: 5,550 GCUPS; 12-wave ones, one per CU,
-// left whole CUs idle in the last round: 7,475; 4-wave: 8,892.)
+// The two-subjects intra kernel's widest shape: 20 rows per lane, in the
+// same 4-wave workgroups: the 26-code image of 1,280 rows (66.5 KB) leaves two
+// workgroups per CU, 2 waves per SIMD.  (Measured on C5: 6-wave workgroups did
+// not fit two per CU, 2 + 2 + 1 + 1 waves per SIMD each: 5,550 GCUPS; 12-wave
+// ones, one per CU, left whole CUs idle in the last round: 7,475; 4-wave:
+// 8,892.)
 constexpr int kIntraX2MaxRI = 20;
+// Steps per bias period of the intra kernel at RI rows per lane (one rebase
+// of every row's H and E per period): 16 at the widest shape, whose 2 waves
+// per SIMD leave registers for the 8 more anti-diagonal maxima; 8 otherwise.
+#ifndef SW_IX2_P16
+#define SW_IX2_P16 1  // (A/B builds: 0 = 8 steps at every shape; host and device alike)
+#endif
+constexpr int intra_period(int ri) { return SW_IX2_P16 && ri == kIntraX2MaxRI ? 16 : 8; }
+// Its biased cell stores values up to this many gap extensions above the
+// true ones (row RI - 1 at the last step of a bias period, + 2 ge in the
+// profile, + the F floor's step).
+constexpr int intra_bias_rows(int ri) { return ri + intra_period(ri) + 2 > 26 ? ri + intra_period(ri) + 2 : 26; }
+
 // int32 re-scoring of the blocks a 16-bit kernel listed (device-side count);
 // strips of rescue_rows(affine) query rows.
 int rescue_rows(bool affine);

@@ -2,7 +2,8 @@
 with a -DSW_TRACE_BLOCKS build via SW_AMD_LIB and SW_TRACE_FILE set):
 blocks in flight over the launch, block durations against their width and
 form (single wave / group), the critical blocks.
-usage: exp_share_trace.py SHARD_OF [LONG_THRESHOLD]"""
+usage: exp_share_trace.py SHARD_OF [LONG_THRESHOLD] [ref]
+(ref: the reference's scoring, BLOSUM50 linear 2, instead of BLOSUM62 11/1)"""
 import json
 import os
 import sys
@@ -23,9 +24,11 @@ with open(os.path.join(REPO, "tests", "golden", "queries", "P07327.fasta")) as f
     q = sw.encode("".join(f.read().split("\n")[1:]))
 h = sw.Handle(0)
 db = sw.Database(h, r, o, long_threshold=(T or None))
-m = sw.builtin_matrix(sw.MATRIX_BLOSUM62)
+REF = len(sys.argv) > 3 and sys.argv[3] == "ref"
+m = sw.builtin_matrix(sw.MATRIX_BLOSUM50_REF if REF else sw.MATRIX_BLOSUM62)
+go, ge = (2, 2) if REF else (12, 1)
 for _ in range(4):
-    db.scan(q, matrix=m, gap_open=12, gap_extend=1)
+    db.scan(q, matrix=m, gap_open=go, gap_extend=ge)
 st = db.stats()
 tm = h.timing()
 db.close()

@@ -745,3 +745,44 @@ def test_drain_waits_for_previous_deferred_tail(sw, oracle, handle, knobs, scori
         for k, q in enumerate(order):
             assert np.array_equal(out[k], want[len(q)]), (k, len(q), np.nonzero(out[k] != want[len(q)])[0][:10])
     db.close()
+
+
+@pytest.mark.parametrize("scoring", [(1, 12, 1), (0, 2, 2), (1, 14, 3)])
+@pytest.mark.parametrize("form", ["single", "merged"])
+def test_single_wave_block_widths(sw, oracle, handle, knobs, scoring, form):
+    """The single-wave fp16 pass (x2s_block, chained passes): block widths
+    8 ... 136 (odd and even multiples of 8), queries of one pass (standalone
+    kernel, no chaining), of two, and of up to six chained passes, planted
+    near-copies that the guard flags for the rescue chain, both gap models;
+    alone and inside the merged launch (the widest block by a wave pair, long
+    subjects beside it), against the oracle.  (Round 5 ran a 16-column bias
+    period with an LDS delay line through it: parity-green, 1.4 % fewer VALU
+    instructions, 2.3 % slower: DESIGN.md §4.)"""
+    mid, go, ge = scoring
+    rng = np.random.default_rng(71)
+    q0 = sw.synth.query(333, shard=71)
+    subs = []
+    for w in (8, 16, 24, 32, 40, 48, 56, 64, 72, 80, 96, 104, 120, 136):
+        lens = rng.integers(max(1, w - 7), w + 1, size=64)
+        subs += [sw.synth.query(int(n), shard=1000 * w + k) for k, n in enumerate(lens)]
+    subs += [q0[:130].copy(), q0[100:200].copy(), np.concatenate([q0[:60], q0[:60]])]  # near-copies
+    long_threshold = 100000
+    if form == "merged":
+        subs += [sw.synth.query(700, shard=72), sw.synth.query(650, shard=73), q0.copy()]  # long subjects
+        long_threshold = 300
+        knobs(lpt=1, pair_width=130)
+    else:
+        knobs(lpt=0, pair_width=100000)
+    r = np.concatenate(subs)
+    o = np.zeros(len(subs) + 1, dtype=np.int64)
+    o[1:] = np.cumsum([len(x) for x in subs])
+    db = sw.Database(handle, r, o, long_threshold=long_threshold)
+    m = sw.capi.builtin_matrix(mid)
+    for qlen in (40, 64, 65, 130, 200, 333):
+        q = q0[:qlen]
+        got = db.scan(q, m, go, ge)
+        want = oracle.scan(q, r, o, mat=m, gap_open=go, gap_extend=ge)
+        assert np.array_equal(got, want), (qlen, np.nonzero(got != want)[0][:10])
+        if form == "merged" and qlen > 64:
+            assert "+lpt" in handle.last_kernel(), handle.last_kernel()
+    db.close()
