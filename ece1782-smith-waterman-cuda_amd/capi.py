@@ -29,7 +29,8 @@ EXPORTED = (
     "sw_db_create", "sw_db_free", "sw_db_get_stats", "sw_db_set_long_threshold", "sw_db_reset_adaptive",
     "sw_scan", "sw_scan_device", "sw_scan_batch", "sw_scan_batch_device", "sw_get_timing",
     "sw_timing_reset", "sw_timing_total", "sw_stream_wait_scan", "sw_last_kernel", "sw_last_intra_kernel",
-    "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_topk_device_ids", "sw_scan_topk", "sw_score_pair",
+    "sw_topk", "sw_topk_device", "sw_topk_keys_device", "sw_topk_device_ids", "sw_scan_topk",
+    "sw_scan_rank_device", "sw_score_pair",
     "sw_align",
     "sw_db_save", "sw_db_load", "sw_db_subjects", "sw_db_create_synthetic", "sw_synth_tables",
     "sw_synth_lengths", "sw_group_create", "sw_group_destroy", "sw_group_info", "sw_group_handle",
@@ -161,6 +162,7 @@ def lib():
         "sw_topk_keys_device": (ctypes.c_int, [vp, vp, i64, i32, vp]),
         "sw_topk_device_ids": (ctypes.c_int, [vp, vp, i64, vp, i32, vp]),
         "sw_scan_topk": (ctypes.c_int, [vp, vp, u8p, i32, ctypes.POINTER(Scoring), i32, i64p]),
+        "sw_scan_rank_device": (ctypes.c_int, [vp, vp, u8p, i32, ctypes.POINTER(Scoring), vp, i32, vp, i64, vp]),
         "sw_score_pair": (ctypes.c_int, [vp, u8p, i32, u8p, i32, ctypes.POINTER(Scoring), i32p]),
         "sw_group_create": (ctypes.c_int, [i32p, i32, ctypes.POINTER(vp)]),
         "sw_group_destroy": (ctypes.c_int, [vp]),
@@ -472,6 +474,18 @@ class Database:
         sc = _ScoringArg(matrix, gap_open, gap_extend)
         _check(lib().sw_scan_device(self.handle.ptr, self._d, qp, len(q), sc.ptr(),
                                     ctypes.c_void_p(scores_dev_ptr)))
+
+    def scan_rank_device(self, query_codes, scores_dev_ptr, k, keys_out_dev_ptr, matrix=None, gap_open=2,
+                         gap_extend=None, gids_dev_ptr=None, id_base=0):
+        """Asynchronous scan into a device int32 buffer and the device top-K
+        of its scores into keys_out_dev_ptr (k int64 keys, best first, global
+        id gids[r] or id_base + r for result id r; sw_scan_rank_device: inside
+        the scan's merged launch when it is one)."""
+        q, qp = _u8(query_codes)
+        sc = _ScoringArg(matrix, gap_open, gap_extend)
+        _check(lib().sw_scan_rank_device(self.handle.ptr, self._d, qp, len(q), sc.ptr(),
+                                         ctypes.c_void_p(scores_dev_ptr), k, ctypes.c_void_p(gids_dev_ptr or 0),
+                                         id_base, ctypes.c_void_p(keys_out_dev_ptr)))
 
     def scan_topk(self, query_codes, k, matrix=None, gap_open=2, gap_extend=None):
         """The k best subjects as int64 keys (score << 32 | 2^31-1-id, best

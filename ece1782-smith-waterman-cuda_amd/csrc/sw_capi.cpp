@@ -339,6 +339,8 @@ struct sw_db {
     uint32_t* d_blk_cols = nullptr;      // block widths rounded to 8 columns (sw_inter_x2s)
     int32_t* d_lane_ids = nullptr;
     int32_t* d_ids = nullptr;            // every subject's result id (sw_scan_topk), on first use
+    int rid_identity = -1;               // result ids are 0 .. n-1 in order (1), or not (0); -1 unknown
+    int32_t* d_rank = nullptr;           // the merged launch's ranking counters (swk::RankArgs::ctl)
     int32_t* d_bnd_h = nullptr;
     int32_t* d_bnd_f = nullptr;
     // two rescue lists [count, block ids...] of nblocks + 1 ints each: the
@@ -482,7 +484,7 @@ int32_t default_long_threshold(const sw_db* db) {
 void free_dev(sw_db* db) {
     void* ptrs[] = {db->d_res, db->d_blk_off, db->d_blk_groups, db->d_blk_cols, db->d_lane_ids, db->d_bnd_h, db->d_bnd_f,
                     db->d_rescue, db->d_lres, db->d_loff, db->d_llen, db->d_lid, db->d_lbnd_h, db->d_lbnd_f,
-                    db->d_lrescue, db->d_rbnd_h, db->d_rbnd_f, db->d_rlbnd_h, db->d_rlbnd_f, db->d_ids};
+                    db->d_lrescue, db->d_rbnd_h, db->d_rbnd_f, db->d_rlbnd_h, db->d_rlbnd_f, db->d_ids, db->d_rank};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     db->d_res = nullptr; db->d_blk_off = nullptr; db->d_blk_groups = nullptr; db->d_lane_ids = nullptr;
@@ -492,6 +494,7 @@ void free_dev(sw_db* db) {
     db->d_lrescue = nullptr;
     db->d_rbnd_h = db->d_rbnd_f = db->d_rlbnd_h = db->d_rlbnd_f = nullptr;
     db->d_ids = nullptr;
+    db->d_rank = nullptr;
     db->rbnd_tried = false;
     for (auto& t : db->lpt_tables) (void)hipFree(t.d_order);
     db->lpt_tables.clear();
@@ -894,7 +897,7 @@ struct Profiles {
 // rows; the first also zeroes the rescue lists' counters `reset`) in one of
 // the handle's profile slots, on the scan's stream.
 int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* mat, int go, bool affine,
-                   int32_t qpad_inter, bool want16, int ri, int32_t qpad_intra, int32_t* const (&reset)[9],
+                   int32_t qpad_inter, bool want16, int ri, int32_t qpad_intra, int32_t* const (&reset)[swk::kResetWords],
                    Profiles* P) {
     for (int32_t i = 0; i < qlen; ++i)
         if (q[i] >= SW_ALPHABET) return fail(SW_E_INVALID, "query residue code out of range (use sw_encode)");
@@ -945,7 +948,7 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     a.ri = ri;
     a.rip = rip;
     a.qpad_intra = ri ? qpad_intra : 0;
-    for (int k = 0; k < 9; ++k) a.reset[k] = reset[k];
+    for (int k = 0; k < swk::kResetWords; ++k) a.reset[k] = reset[k];
     std::memcpy(a.mat, mat, 625);
     const int32_t rows = std::max(P->stride, a.qpad_intra);
     for (int32_t r0 = 0; r0 < rows; r0 += swk::kProfQueryChunk) {
@@ -1189,6 +1192,74 @@ int join_tails(sw_handle* h) {
     return SW_OK;
 }
 
+// A ranking asked for with a scan (sw_scan_rank_device, sw_scan_topk): the
+// k best keys of the scan's scores over the database's subjects — result id
+// r, global id gid ? gid[r] : id_base + r — into out (device, k keys).
+struct RankReq {
+    int32_t k;
+    const int32_t* gid;
+    int64_t id_base;
+    int64_t* out;
+};
+
+// The ranking input over a database's subjects: its scores through the
+// result ids (db->d_ids, uploaded on first use), or directly when the ids
+// are 0 .. n-1 in order (the default).
+int rank_src(sw_db* db, const int32_t* scores, const RankReq& rq, swk::TopkSrc* src) {
+    if (db->rid_identity < 0) {
+        db->rid_identity = db->max_id + 1 == db->n;
+        for (int64_t k = 0; db->rid_identity == 1 && k < db->n; ++k) db->rid_identity = db->h_ids[k] == k;
+    }
+    *src = swk::TopkSrc{};
+    src->scores = scores;
+    src->gid = rq.gid;
+    src->id_base = rq.id_base;
+    if (!db->rid_identity) {
+        if (!db->d_ids) {
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_ids), static_cast<size_t>(db->n) * sizeof(int32_t)));
+            HIPCHECK(hipMemcpy(db->d_ids, db->h_ids.data(), static_cast<size_t>(db->n) * sizeof(int32_t),
+                               hipMemcpyHostToDevice));
+            db->device_bytes += static_cast<size_t>(db->n) * sizeof(int32_t);
+        }
+        src->rid = db->d_ids;
+    }
+    return SW_OK;
+}
+
+// The handle's top-K workspace holds at least `need` bytes.
+int ensure_topk_work(sw_handle* h, size_t need) {
+    if (need > h->topk_cap) {
+        if (h->d_topk_work) {
+            HIPCHECK(hipStreamSynchronize(h->stream));
+            HIPCHECK(hipFree(h->d_topk_work));
+        }
+        h->topk_cap = std::max<size_t>(need, 1 << 20);
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&h->d_topk_work), h->topk_cap));
+    }
+    return SW_OK;
+}
+
+// Chunks of the merged launch's ranking tail (swk::RankArgs, sw_rank.h
+// rank_tail) for n entries: at least 4,096 keys per chunk up to 64 chunks
+// (16 keys per thread: one chunk's selection is a few microseconds), then
+// as many 8,192-key chunks as n needs; false when the final selection's
+// nchunks x k keys would not fit its registers (or k its sort): the scan then
+// ranks in a separate launch after it.
+bool rank_plan(int64_t n, int32_t k, swk::RankArgs* r) {
+    constexpr int64_t T = swk::kWavesPerWG * swk::kLanes;
+    if (n <= 0 || k <= 0 || k > swk::kRankMaxK) return false;
+    int64_t nch = std::max<int64_t>((n + T * swk::kRankChunkPer - 1) / (T * swk::kRankChunkPer),
+                                    std::min<int64_t>(64, (n + 4095) / 4096));
+    const int64_t chunk = (n + nch - 1) / nch;
+    nch = (n + chunk - 1) / chunk;
+    if (nch * k > T * swk::kRankFinalPer) return false;
+    r->n = n;
+    r->k = k;
+    r->nchunks = static_cast<int32_t>(nch);
+    r->chunk = static_cast<int32_t>(chunk);
+    return true;
+}
+
 int next_events(sw_handle* h) {
     if (h->nscans >= 4096) h->nscans = 0;  // bound the pool; older sums are dropped
     if (h->nscans == h->evpool.size()) {
@@ -1205,13 +1276,28 @@ int next_events(sw_handle* h) {
     return SW_OK;
 }
 
+// The ranking of a scan that did not rank in its merged launch: a top-K
+// launch on the scan's stream after every stage that writes its scores.
+int rank_after(sw_handle* h, sw_db* db, const int32_t* scores_dev, const RankReq& rq) {
+    swk::TopkSrc src;
+    int rc;
+    if ((rc = rank_src(db, scores_dev, rq, &src))) return rc;
+    if ((rc = ensure_topk_work(h, swk::topk_workspace_bytes(db->n, rq.k)))) return rc;
+    HIPCHECK(swk::launch_topk(src, db->n, rq.k, rq.out, h->d_topk_work, h->stream));
+    ++h->launches;
+    return SW_OK;
+}
+
 // defer: another scan follows on this handle before the caller waits (the
 // queries of a batch but the last): this scan's rescue tail may run on the
 // tail stream beside the next scan's fp16 passes (sw_handle::tail).
+// rq (nullable): rank the scan's scores too (in the merged launch's tail
+// when it fits, else by a top-K launch after the scan, before its end event).
 int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen, const sw_scoring* sc,
-              int32_t* scores_dev, bool defer = false) {
+              int32_t* scores_dev, bool defer = false, const RankReq* rq = nullptr) {
     sw_db* db = const_cast<sw_db*>(cdb);
     if (!h || !db || (!query && qlen > 0) || qlen < 0 || !scores_dev) return fail(SW_E_INVALID, "null argument");
+    if (rq) defer = false;  // the ranking reads every rescued score
     const int8_t* mat;
     int go, ge, rc;
     if ((rc = check_fault(h))) return rc;
@@ -1354,6 +1440,7 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
         MARK(0, h->stream);
         if (db->max_id >= 0)
             HIPCHECK(hipMemsetAsync(scores_dev, 0, static_cast<size_t>(db->max_id + 1) * 4, h->stream));
+        if (rq && (rc = rank_after(h, db, scores_dev, *rq))) return rc;
         for (int k = 1; k < 8; ++k) MARK(k, h->stream);
         h->timed = true;
         return SW_OK;
@@ -1397,6 +1484,20 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
     // int32 long-subject stage at the fp16 form's rows per lane
     const bool drain = lpt && ensure_rbnd(db, affine, intra_x2);
     db->last_drain = drain;
+    // the ranking in the merged launch's tail (its chunks and counters)
+    swk::RankArgs rank_args{};
+    const bool rank_tail = rq && drain && rank_plan(db->n, rq->k, &rank_args);
+    if (rank_tail) {
+        if (!db->d_rank) {
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rank), 4 * sizeof(int32_t)));
+            db->device_bytes += 4 * sizeof(int32_t);
+        }
+        if ((rc = ensure_topk_work(h, static_cast<size_t>(rank_args.nchunks) * rq->k * sizeof(int64_t)))) return rc;
+        if ((rc = rank_src(db, scores_dev, *rq, &rank_args.src))) return rc;
+        rank_args.work = h->d_topk_work;
+        rank_args.out = rq->out;
+        rank_args.ctl = db->d_rank;
+    }
     if (drain) {
         ri = ri2;
         qpad_intra = static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri));
@@ -1450,9 +1551,11 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
     {
         int32_t* const cA = (rescue && db->nblocks) ? listA : nullptr;
         int32_t* const c1 = (db->nlong && intra_x2) ? list1 : nullptr;
-        int32_t* const reset[9] = {cA, (cA && f16) ? listB : nullptr, (cA && f16) ? maxA : nullptr, c1,
-                                   c1 ? list2 : nullptr, drain ? headA : nullptr, drain ? headA + 1 : nullptr,
-                                   drain ? head1 : nullptr, drain ? head1 + 1 : nullptr};
+        int32_t* const rctl = rank_tail ? db->d_rank : nullptr;
+        int32_t* const reset[swk::kResetWords] = {
+            cA, (cA && f16) ? listB : nullptr, (cA && f16) ? maxA : nullptr, c1, c1 ? list2 : nullptr,
+            drain ? headA : nullptr, drain ? headA + 1 : nullptr, drain ? head1 : nullptr, drain ? head1 + 1 : nullptr,
+            rctl, rctl ? rctl + 1 : nullptr, rctl ? rctl + 2 : nullptr};
         if ((rc = build_profiles(h, query, qlen, mat, go, affine,
                                  std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2}),
                                  x2 || intra_x2, ri, qpad_intra, reset, &P)))
@@ -1752,11 +1855,22 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
                 d.heads[2] = head1;
                 d.heads[3] = head1 + 1;
                 d.fault = h->d_fault;
+                if (rank_tail) {
+                    d.rank = rank_args;
+                    d.rank.nwg = nwg;
+                    d.rank.nfin = std::min({d.rank.nchunks, 128, nwg});
+                }
+                const swk::RankArgs& ra = d.rank;
                 const std::vector<uint64_t> key = {
                     reinterpret_cast<uint64_t>(P.dev), P.off8, P.off16, P.intra_off, static_cast<uint64_t>(par),
                     reinterpret_cast<uint64_t>(scores_dev), static_cast<uint64_t>(qlen), skey,
                     static_cast<uint64_t>(npair), static_cast<uint64_t>(nquad), static_cast<uint64_t>(P.stride),
-                    reinterpret_cast<uint64_t>(a.trace)};
+                    reinterpret_cast<uint64_t>(a.trace),
+                    static_cast<uint64_t>(ra.k), static_cast<uint64_t>(ra.n), static_cast<uint64_t>(ra.nchunks),
+                    static_cast<uint64_t>(ra.chunk), static_cast<uint64_t>(ra.nfin), static_cast<uint64_t>(ra.nwg),
+                    reinterpret_cast<uint64_t>(ra.src.rid), reinterpret_cast<uint64_t>(ra.src.gid),
+                    static_cast<uint64_t>(ra.src.id_base), reinterpret_cast<uint64_t>(ra.work),
+                    reinterpret_cast<uint64_t>(ra.out)};
                 if ((rc = drain_blob(db, h->stream, key, d, &dargs))) return rc;
             }
             HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, order, nwg, affine, ri2, h->stream, dargs));
@@ -1775,6 +1889,7 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
         if (npair) h->last_kernel.replace(0, std::strlen("sw_inter_x2s"), "sw_inter_x2p");  // + wave pairs
         if (nr) h->last_kernel += "+int16[0," + std::to_string(nr) + ")";
         if (lpt) h->last_kernel += drain ? "+lpt+drain" : "+lpt";
+        if (rank_tail) h->last_kernel += "+rank";
         if (!lpt) MARK(7, h->stream);
         ++h->launches;
         if (ncoop || nr) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
@@ -1826,6 +1941,7 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
     if (db->nlong && !lpt) HIPCHECK(hipStreamWaitEvent(h->stream, h->ev[1], 0));
     // the scan completes on the handle's stream: so do earlier deferred tails
     if (!deferred && (rc = join_tails(h))) return rc;
+    if (rq && !rank_tail && (rc = rank_after(h, db, scores_dev, *rq))) return rc;
     MARK(3, h->stream);
     h->open_slot = -1;
     h->evpool[h->nscans - 1].launches = h->launches;
@@ -1870,8 +1986,8 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
 // would not wait for the kernels this one queued.  Drain the handle's streams
 // and release the slot instead.
 int scan_impl(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen, const sw_scoring* sc,
-              int32_t* scores_dev, bool defer = false) {
-    const int rc = scan_impl_body(h, db, query, qlen, sc, scores_dev, defer);
+              int32_t* scores_dev, bool defer = false, const RankReq* rq = nullptr) {
+    const int rc = scan_impl_body(h, db, query, qlen, sc, scores_dev, defer, rq);
     if (h && h->open_slot >= 0) {
         for (hipStream_t st : {h->stream, h->side, h->side2, h->tail})
             if (st) (void)hipStreamSynchronize(st);
@@ -1894,21 +2010,19 @@ int ensure_scores(sw_handle* h, size_t n) {
 
 namespace {
 int topk_impl(sw_handle* h, const int32_t* scores, const int64_t* keys, int64_t n, int64_t id_base,
-              const int32_t* ids, int32_t k, int64_t* out, bool by_id = false) {
+              const int32_t* ids, int32_t k, int64_t* out) {
     if (!h || !out || n < 0 || k <= 0 || k > 4096 || (n > 0 && !scores && !keys))
         return fail(SW_E_INVALID, "bad top-k arguments (1 <= k <= 4096)");
     if (id_base < 0 || id_base + n > (int64_t(1) << 31)) return fail(SW_E_INVALID, "ids must fit in 31 bits");
     HIPCHECK(hipSetDevice(h->device));
-    const size_t need = swk::topk_workspace_bytes(n, k);
-    if (need > h->topk_cap) {
-        if (h->d_topk_work) {
-            HIPCHECK(hipStreamSynchronize(h->stream));
-            HIPCHECK(hipFree(h->d_topk_work));
-        }
-        h->topk_cap = std::max<size_t>(need, 1 << 20);
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&h->d_topk_work), h->topk_cap));
-    }
-    HIPCHECK(swk::launch_topk(scores, keys, n, id_base, ids, k, out, h->d_topk_work, h->stream, by_id));
+    int rc;
+    if ((rc = ensure_topk_work(h, swk::topk_workspace_bytes(n, k)))) return rc;
+    swk::TopkSrc src{};
+    src.scores = keys ? nullptr : scores;
+    src.keys = keys;
+    src.gid = ids;
+    src.id_base = id_base;
+    HIPCHECK(swk::launch_topk(src, n, k, out, h->d_topk_work, h->stream));
     return SW_OK;
 }
 }  // namespace
@@ -2555,6 +2669,18 @@ int sw_topk_keys_device(sw_handle* h, const int64_t* keys_dev, int64_t n, int32_
     return topk_impl(h, nullptr, keys_dev, n, 0, nullptr, k, keys_out_dev);
 }
 
+int sw_scan_rank_device(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen, const sw_scoring* sc,
+                        int32_t* scores_dev, int32_t k, const int32_t* gid_dev, int64_t id_base,
+                        int64_t* keys_out_dev) {
+    sw_db* db = const_cast<sw_db*>(cdb);
+    if (!h || !db || !scores_dev || !keys_out_dev || k <= 0 || k > 4096)
+        return fail(SW_E_INVALID, "bad argument (1 <= k <= 4096)");
+    if (!gid_dev && (id_base < 0 || id_base + db->max_id >= (int64_t(1) << 31)))
+        return fail(SW_E_INVALID, "ids must fit in 31 bits");
+    const RankReq rq{k, gid_dev, gid_dev ? 0 : id_base, keys_out_dev};
+    return scan_impl(h, db, query, qlen, sc, scores_dev, false, &rq);
+}
+
 int sw_scan_topk(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen, const sw_scoring* sc, int32_t k,
                  int64_t* keys_host) {
     sw_db* db = const_cast<sw_db*>(cdb);
@@ -2565,18 +2691,12 @@ int sw_scan_topk(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t q
     }
     int rc;
     HIPCHECK(hipSetDevice(h->device));
-    if (!db->built && (rc = build_db(db))) return rc;
-    if (!db->d_ids) {  // the ranking runs over the result ids of the subjects
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_ids), static_cast<size_t>(db->n) * sizeof(int32_t)));
-        HIPCHECK(hipMemcpy(db->d_ids, db->h_ids.data(), static_cast<size_t>(db->n) * sizeof(int32_t),
-                           hipMemcpyHostToDevice));
-        db->device_bytes += static_cast<size_t>(db->n) * sizeof(int32_t);
-    }
     const size_t slots = static_cast<size_t>(db->max_id + 1);
     if ((rc = ensure_scores(h, slots + static_cast<size_t>(2 * k) + 2))) return rc;  // scores, then the k keys
     int64_t* keys_dev = reinterpret_cast<int64_t*>(h->d_scores + round_up(static_cast<int64_t>(slots), 2));
-    if ((rc = scan_impl(h, db, query, qlen, sc, h->d_scores))) return rc;
-    if ((rc = topk_impl(h, h->d_scores, nullptr, db->n, 0, db->d_ids, k, keys_dev, true))) return rc;
+    // the ranking runs over the result ids of the subjects (rank_src)
+    const RankReq rq{k, nullptr, 0, keys_dev};
+    if ((rc = scan_impl(h, db, query, qlen, sc, h->d_scores, false, &rq))) return rc;
     HIPCHECK(hipMemcpyAsync(keys_host, keys_dev, static_cast<size_t>(k) * sizeof(int64_t), hipMemcpyDeviceToHost,
                             h->stream));
     HIPCHECK(hipStreamSynchronize(h->stream));

@@ -336,10 +336,9 @@ int sw_group_topk(sw_group* g, const sw_gdb* gd, const uint8_t* query, int32_t q
     // 1. every device: scan its shard, rank it (global ids), asynchronously
     rc = for_each_device(G, [&](int d) {
         const int64_t nd = static_cast<int64_t>(gd->ids[d].size());
-        int r;
-        if (nd) {
-            if ((r = sw_scan_device(g->h[d], gd->db[d], query, qlen, sc, gd->d_scores[d]))) return r;
-        }
+        if (nd)  // the shard's scores ranked with global ids, in the scan's launch when it is merged
+            return sw_scan_rank_device(g->h[d], gd->db[d], query, qlen, sc, gd->d_scores[d], k, gd->d_ids[d], 0,
+                                       g->d_keys[d]);
         return sw_topk_device_ids(g->h[d], gd->d_scores[d], nd, gd->d_ids[d], k, g->d_keys[d]);
     });
     if (rc) return rc;
