@@ -545,9 +545,6 @@ def main():
     # high priority: HIP gives such streams their own hardware queues, so the
     # exchange never shares one (in order) with the scan's main, long-subject
     # or int16 side streams (GPU_MAX_HW_QUEUES = 4 normal-priority queues)
-    ap.add_argument("--separate-topk", action="store_true",
-                    help="rank a one-query step by a top-K launch on the exchange stream (round 4's form) "
-                         "instead of inside the scan (sw_scan_rank_device)")
     ap.add_argument("--exchange-priority", type=int, default=-1,
                     help="HIP stream priority of the exchange stream (negative = higher)")
     # the latest rocprofv3 --pmc measurement of the C2 launch (FETCH_SIZE x2 +
@@ -644,9 +641,7 @@ def main():
     NBUF = 8
     scores_buf = [torch.zeros((nq, max(n, 1)), dtype=torch.int32, device=dev) for _ in range(NBUF)]
     K = args.topk
-    # per score buffer: a scan that ranks its own scores writes the keys the
-    # exchange of the step NBUF before may still be reading
-    tops = [torch.empty((nq, K), dtype=torch.int64, device=dev) for _ in range(NBUF)]
+    top = torch.empty((nq, K), dtype=torch.int64, device=dev)
     gathered = torch.empty((world, nq, K), dtype=torch.int64, device=dev)
     final = torch.empty((nq, K), dtype=torch.int64, device=dev)
     gid_dev = torch.from_numpy(gids).to(dev) if id_base is None else None
@@ -669,22 +664,12 @@ def main():
         b = counter[0] % NBUF
         counter[0] += 1
         scores = scores_buf[b]
-        top = tops[b]
         # step i-NBUF's top-K has read this buffer (a wait is a packet the
         # command processor spends ~5 us on: skipped when the host already
         # sees the event complete)
         if counter[0] > NBUF and not ranked[b].query():
             stream.wait_event(ranked[b])
-        # one query: the scan ranks its own scores (sw_scan_rank_device: in
-        # the merged launch's tail, so no top-K kernel waits for CUs behind
-        # the next scan); a batch: the device top-K per query on the exchange
-        # stream, beside the next step's scans
-        ranked_in_scan = nq == 1 and not args.separate_topk
-        if ranked_in_scan:
-            db.scan_rank_device(queries[0], scores.data_ptr(), K, top[0].data_ptr(), *scoring,
-                                gids_dev_ptr=(gid_dev.data_ptr() if gid_dev is not None else None),
-                                id_base=(id_base or 0))
-        elif nq == 1:
+        if nq == 1:
             db.scan_device(queries[0], scores.data_ptr(), *scoring)
         else:
             db.scan_batch_device(queries, scores.data_ptr(), *scoring)
@@ -693,7 +678,7 @@ def main():
             handle.stream_wait_scan(xstream.cuda_stream)
         with torch.cuda.stream(xstream):
             # device top-K per query: int64 keys (score << 32 | 2^31-1-global id), best first
-            for k in range(0 if ranked_in_scan else nq):
+            for k in range(nq):
                 if gid_dev is not None:
                     xhandle.topk_device_ids(scores[k].data_ptr(), n, gid_dev.data_ptr(), K, top[k].data_ptr())
                 else:
@@ -753,7 +738,6 @@ def main():
         n_sus = max(args.steps, int(math.ceil(args.sustained_seconds / (elapsed_max / args.steps))))
         s_elapsed, s_cells, s_kt, _ = timed_loop(steps=n_sus, warmup=0)
         sustained = sustained_summary(s_elapsed, n_sus, s_cells, s_kt["wave_ms"], s_kt["scans"], world)
-    top = tops[(counter[0] - 1) % NBUF]
     final_keys = (final if world > 1 else top).cpu().numpy()
     top_ids, top_scores = sw.capi.decode_keys(final_keys[0])
     # the measured run's scores and keys (its last step's buffer), for the parity leg
@@ -925,12 +909,10 @@ def main():
             "valu_roofline": valu_roofline(roof_kernel, cells_all / world, kt["total_ms"] / nsc * nq, wave_gcups),
             "valu_hw": valu_hw,
             "kernels": {"inter": kernel, "intra": intra_kernel},
-            # where each step's top-K ran: inside the scan's launch (its kernel
-            # name ends "+rank"), after the scan on its stream, or on the
-            # exchange stream beside the next scan
-            "topk": ("in the scan's merged launch" if kernel.endswith("+rank") else
-                     "after the scan, its stream" if nq == 1 and not args.separate_topk else
-                     "exchange stream, beside the next scan"),
+            # each step's device top-K: one launch per query (sw_topk.hip
+            # sw_topk_fused) on the exchange stream, beside the next scan
+            "topk": "one launch per query on the exchange stream, beside the next scan"
+                    if not args.no_overlap else "after the scan, its stream",
             "top_hit": {"id": int(top_ids[0]), "score": int(top_scores[0])},
             "host": {"cores_used": args.cpu_threads or eff, "affinity_cpus": aff, "cgroup_quota_cpus": quota},
         }

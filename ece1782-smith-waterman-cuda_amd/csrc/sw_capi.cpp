@@ -340,7 +340,6 @@ struct sw_db {
     int32_t* d_lane_ids = nullptr;
     int32_t* d_ids = nullptr;            // every subject's result id (sw_scan_topk), on first use
     int rid_identity = -1;               // result ids are 0 .. n-1 in order (1), or not (0); -1 unknown
-    int32_t* d_rank = nullptr;           // the merged launch's ranking counters (swk::RankArgs::ctl)
     int32_t* d_bnd_h = nullptr;
     int32_t* d_bnd_f = nullptr;
     // two rescue lists [count, block ids...] of nblocks + 1 ints each: the
@@ -484,7 +483,7 @@ int32_t default_long_threshold(const sw_db* db) {
 void free_dev(sw_db* db) {
     void* ptrs[] = {db->d_res, db->d_blk_off, db->d_blk_groups, db->d_blk_cols, db->d_lane_ids, db->d_bnd_h, db->d_bnd_f,
                     db->d_rescue, db->d_lres, db->d_loff, db->d_llen, db->d_lid, db->d_lbnd_h, db->d_lbnd_f,
-                    db->d_lrescue, db->d_rbnd_h, db->d_rbnd_f, db->d_rlbnd_h, db->d_rlbnd_f, db->d_ids, db->d_rank};
+                    db->d_lrescue, db->d_rbnd_h, db->d_rbnd_f, db->d_rlbnd_h, db->d_rlbnd_f, db->d_ids};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     db->d_res = nullptr; db->d_blk_off = nullptr; db->d_blk_groups = nullptr; db->d_lane_ids = nullptr;
@@ -494,7 +493,6 @@ void free_dev(sw_db* db) {
     db->d_lrescue = nullptr;
     db->d_rbnd_h = db->d_rbnd_f = db->d_rlbnd_h = db->d_rlbnd_f = nullptr;
     db->d_ids = nullptr;
-    db->d_rank = nullptr;
     db->rbnd_tried = false;
     for (auto& t : db->lpt_tables) (void)hipFree(t.d_order);
     db->lpt_tables.clear();
@@ -897,7 +895,7 @@ struct Profiles {
 // rows; the first also zeroes the rescue lists' counters `reset`) in one of
 // the handle's profile slots, on the scan's stream.
 int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* mat, int go, bool affine,
-                   int32_t qpad_inter, bool want16, int ri, int32_t qpad_intra, int32_t* const (&reset)[swk::kResetWords],
+                   int32_t qpad_inter, bool want16, int ri, int32_t qpad_intra, int32_t* const (&reset)[9],
                    Profiles* P) {
     for (int32_t i = 0; i < qlen; ++i)
         if (q[i] >= SW_ALPHABET) return fail(SW_E_INVALID, "query residue code out of range (use sw_encode)");
@@ -948,7 +946,7 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     a.ri = ri;
     a.rip = rip;
     a.qpad_intra = ri ? qpad_intra : 0;
-    for (int k = 0; k < swk::kResetWords; ++k) a.reset[k] = reset[k];
+    for (int k = 0; k < 9; ++k) a.reset[k] = reset[k];
     std::memcpy(a.mat, mat, 625);
     const int32_t rows = std::max(P->stride, a.qpad_intra);
     for (int32_t r0 = 0; r0 < rows; r0 += swk::kProfQueryChunk) {
@@ -1226,7 +1224,8 @@ int rank_src(sw_db* db, const int32_t* scores, const RankReq& rq, swk::TopkSrc* 
     return SW_OK;
 }
 
-// The handle's top-K workspace holds at least `need` bytes.
+// The handle's top-K workspace holds at least `need` bytes; a new one
+// starts with the one-launch top-K's counter at zero (swk::launch_topk).
 int ensure_topk_work(sw_handle* h, size_t need) {
     if (need > h->topk_cap) {
         if (h->d_topk_work) {
@@ -1235,29 +1234,9 @@ int ensure_topk_work(sw_handle* h, size_t need) {
         }
         h->topk_cap = std::max<size_t>(need, 1 << 20);
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&h->d_topk_work), h->topk_cap));
+        HIPCHECK(hipMemsetAsync(h->d_topk_work, 0, 256, h->stream));
     }
     return SW_OK;
-}
-
-// Chunks of the merged launch's ranking tail (swk::RankArgs, sw_rank.h
-// rank_tail) for n entries: at least 4,096 keys per chunk up to 64 chunks
-// (16 keys per thread: one chunk's selection is a few microseconds), then
-// as many 8,192-key chunks as n needs; false when the final selection's
-// nchunks x k keys would not fit its registers (or k its sort): the scan then
-// ranks in a separate launch after it.
-bool rank_plan(int64_t n, int32_t k, swk::RankArgs* r) {
-    constexpr int64_t T = swk::kWavesPerWG * swk::kLanes;
-    if (n <= 0 || k <= 0 || k > swk::kRankMaxK) return false;
-    int64_t nch = std::max<int64_t>((n + T * swk::kRankChunkPer - 1) / (T * swk::kRankChunkPer),
-                                    std::min<int64_t>(64, (n + 4095) / 4096));
-    const int64_t chunk = (n + nch - 1) / nch;
-    nch = (n + chunk - 1) / chunk;
-    if (nch * k > T * swk::kRankFinalPer) return false;
-    r->n = n;
-    r->k = k;
-    r->nchunks = static_cast<int32_t>(nch);
-    r->chunk = static_cast<int32_t>(chunk);
-    return true;
 }
 
 int next_events(sw_handle* h) {
@@ -1276,8 +1255,8 @@ int next_events(sw_handle* h) {
     return SW_OK;
 }
 
-// The ranking of a scan that did not rank in its merged launch: a top-K
-// launch on the scan's stream after every stage that writes its scores.
+// A scan's ranking: a top-K launch on the scan's stream after every stage
+// that writes its scores.
 int rank_after(sw_handle* h, sw_db* db, const int32_t* scores_dev, const RankReq& rq) {
     swk::TopkSrc src;
     int rc;
@@ -1291,8 +1270,8 @@ int rank_after(sw_handle* h, sw_db* db, const int32_t* scores_dev, const RankReq
 // defer: another scan follows on this handle before the caller waits (the
 // queries of a batch but the last): this scan's rescue tail may run on the
 // tail stream beside the next scan's fp16 passes (sw_handle::tail).
-// rq (nullable): rank the scan's scores too (in the merged launch's tail
-// when it fits, else by a top-K launch after the scan, before its end event).
+// rq (nullable): rank the scan's scores too (a top-K launch after every
+// stage that writes them, before the scan's end event).
 int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t qlen, const sw_scoring* sc,
               int32_t* scores_dev, bool defer = false, const RankReq* rq = nullptr) {
     sw_db* db = const_cast<sw_db*>(cdb);
@@ -1484,20 +1463,6 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
     // int32 long-subject stage at the fp16 form's rows per lane
     const bool drain = lpt && ensure_rbnd(db, affine, intra_x2);
     db->last_drain = drain;
-    // the ranking in the merged launch's tail (its chunks and counters)
-    swk::RankArgs rank_args{};
-    const bool rank_tail = rq && drain && rank_plan(db->n, rq->k, &rank_args);
-    if (rank_tail) {
-        if (!db->d_rank) {
-            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_rank), 4 * sizeof(int32_t)));
-            db->device_bytes += 4 * sizeof(int32_t);
-        }
-        if ((rc = ensure_topk_work(h, static_cast<size_t>(rank_args.nchunks) * rq->k * sizeof(int64_t)))) return rc;
-        if ((rc = rank_src(db, scores_dev, *rq, &rank_args.src))) return rc;
-        rank_args.work = h->d_topk_work;
-        rank_args.out = rq->out;
-        rank_args.ctl = db->d_rank;
-    }
     if (drain) {
         ri = ri2;
         qpad_intra = static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri));
@@ -1551,11 +1516,9 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
     {
         int32_t* const cA = (rescue && db->nblocks) ? listA : nullptr;
         int32_t* const c1 = (db->nlong && intra_x2) ? list1 : nullptr;
-        int32_t* const rctl = rank_tail ? db->d_rank : nullptr;
-        int32_t* const reset[swk::kResetWords] = {
-            cA, (cA && f16) ? listB : nullptr, (cA && f16) ? maxA : nullptr, c1, c1 ? list2 : nullptr,
-            drain ? headA : nullptr, drain ? headA + 1 : nullptr, drain ? head1 : nullptr, drain ? head1 + 1 : nullptr,
-            rctl, rctl ? rctl + 1 : nullptr, rctl ? rctl + 2 : nullptr};
+        int32_t* const reset[9] = {cA, (cA && f16) ? listB : nullptr, (cA && f16) ? maxA : nullptr, c1,
+                                   c1 ? list2 : nullptr, drain ? headA : nullptr, drain ? headA + 1 : nullptr,
+                                   drain ? head1 : nullptr, drain ? head1 + 1 : nullptr};
         if ((rc = build_profiles(h, query, qlen, mat, go, affine,
                                  std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2}),
                                  x2 || intra_x2, ri, qpad_intra, reset, &P)))
@@ -1855,22 +1818,11 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
                 d.heads[2] = head1;
                 d.heads[3] = head1 + 1;
                 d.fault = h->d_fault;
-                if (rank_tail) {
-                    d.rank = rank_args;
-                    d.rank.nwg = nwg;
-                    d.rank.nfin = std::min({d.rank.nchunks, 128, nwg});
-                }
-                const swk::RankArgs& ra = d.rank;
                 const std::vector<uint64_t> key = {
                     reinterpret_cast<uint64_t>(P.dev), P.off8, P.off16, P.intra_off, static_cast<uint64_t>(par),
                     reinterpret_cast<uint64_t>(scores_dev), static_cast<uint64_t>(qlen), skey,
                     static_cast<uint64_t>(npair), static_cast<uint64_t>(nquad), static_cast<uint64_t>(P.stride),
-                    reinterpret_cast<uint64_t>(a.trace),
-                    static_cast<uint64_t>(ra.k), static_cast<uint64_t>(ra.n), static_cast<uint64_t>(ra.nchunks),
-                    static_cast<uint64_t>(ra.chunk), static_cast<uint64_t>(ra.nfin), static_cast<uint64_t>(ra.nwg),
-                    reinterpret_cast<uint64_t>(ra.src.rid), reinterpret_cast<uint64_t>(ra.src.gid),
-                    static_cast<uint64_t>(ra.src.id_base), reinterpret_cast<uint64_t>(ra.work),
-                    reinterpret_cast<uint64_t>(ra.out)};
+                    reinterpret_cast<uint64_t>(a.trace)};
                 if ((rc = drain_blob(db, h->stream, key, d, &dargs))) return rc;
             }
             HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, order, nwg, affine, ri2, h->stream, dargs));
@@ -1889,7 +1841,6 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
         if (npair) h->last_kernel.replace(0, std::strlen("sw_inter_x2s"), "sw_inter_x2p");  // + wave pairs
         if (nr) h->last_kernel += "+int16[0," + std::to_string(nr) + ")";
         if (lpt) h->last_kernel += drain ? "+lpt+drain" : "+lpt";
-        if (rank_tail) h->last_kernel += "+rank";
         if (!lpt) MARK(7, h->stream);
         ++h->launches;
         if (ncoop || nr) HIPCHECK(hipStreamWaitEvent(h->stream, h->coop_done, 0));
@@ -1941,7 +1892,7 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
     if (db->nlong && !lpt) HIPCHECK(hipStreamWaitEvent(h->stream, h->ev[1], 0));
     // the scan completes on the handle's stream: so do earlier deferred tails
     if (!deferred && (rc = join_tails(h))) return rc;
-    if (rq && !rank_tail && (rc = rank_after(h, db, scores_dev, *rq))) return rc;
+    if (rq && (rc = rank_after(h, db, scores_dev, *rq))) return rc;
     MARK(3, h->stream);
     h->open_slot = -1;
     h->evpool[h->nscans - 1].launches = h->launches;

@@ -291,7 +291,7 @@ __device__ __forceinline__ void inter_block(const InterArgs& a, int blk, uint8_t
     }
 done:
     const int id = a.lane_ids[static_cast<size_t>(blk) * kLanes + lane];
-    if (id >= 0) store_score(a.scores + id, best);
+    if (id >= 0) a.scores[id] = best;
 }
 
 // DPP controls (GFX9 family): wave_shr:1 moves lane t-1's value to lane t;
@@ -435,7 +435,7 @@ __device__ __forceinline__ void intra_subject(const IntraArgs& a, int sid, uint8
     // wave max-reduction of best
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) best = max(best, __shfl_xor(best, off));
-    if (lane == 0) store_score(a.scores + a.subj_id[sid], best);
+    if (lane == 0) a.scores[a.subj_id[sid]] = best;
     sync();  // list mode: the next subject restages the LDS profile
 }
 

@@ -35,7 +35,6 @@
 #include "sw_int32.h"
 #include "sw_intra_x2.h"
 #include "sw_kernels.h"
-#include "sw_rank.h"
 
 namespace swk {
 
@@ -400,7 +399,7 @@ __device__ __forceinline__ bool x2s_finish(const InterArgs& a, int blk, int lane
     else
         b = max(static_cast<int>(best.x), static_cast<int>(best.y));
     const int id = a.lane_ids[static_cast<size_t>(blk) * kLanes + lane];
-    if (id >= 0) store_score(a.scores + id, b);
+    if (id >= 0) a.scores[id] = b;
     if (a.rescue_list) {
         const bool sat = F16 ? (b >= a.sat_limit) : (b >= kSat16 || b < 0);
         const uint64_t m = __builtin_amdgcn_ballot_w64(sat);
@@ -1127,10 +1126,6 @@ __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(InterArgs a
     // every wave of the workgroup is done here
     if (threadIdx.x == 0) trace_block(a, a.nblocks + blockIdx.x, t0, 0, item >= 0 ? 2 : 3);
     if (drain && any) lpt_drain<AFFINE, RI>(drain, smem, task);
-    // the scan's ranking, by the last workgroups to finish (every score is
-    // final once all have arrived: the drain leaves no entry behind)
-    static_assert((sizeof(TopkLds<256>) + 15) / 16 * 16 + 8 * kRankMaxK <= kSmem, "ranking LDS");
-    if (drain && drain->rank.k > 0) rank_tail<kWavesPerWG * kLanes>(drain->rank, smem, task);
 }
 
 template <int RI>

@@ -579,14 +579,14 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
         const int ba = C::lo(best) - C::zero_int(a);
         const int bb = C::hi(best) - C::zero_int(a);
         if (hasA) {
-            store_score(a.scores + a.subj_id[sa], ba);
+            a.scores[a.subj_id[sa]] = ba;
             if (a.rescue_list && C::template flag<RI>(a, ba)) {
                 list_publish(a.rescue_list, a.rescue_count, sa);
                 flagged = true;
             }
         }
         if (hasB) {
-            store_score(a.scores + a.subj_id[sb], bb);
+            a.scores[a.subj_id[sb]] = bb;
             if (a.rescue_list && C::template flag<RI>(a, bb)) {
                 list_publish(a.rescue_list, a.rescue_count, sb);
                 flagged = true;

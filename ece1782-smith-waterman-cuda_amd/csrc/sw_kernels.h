@@ -175,14 +175,6 @@ __device__ __forceinline__ void list_publish(int32_t* items, int32_t* count, int
     const int slot = atomicAdd(count, 1);
     __hip_atomic_store(items + slot, item, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// A subject's score: a write-through (sc1) store, so a ranking in the same
-// launch (sw_rank.h rank_tail) reads it from another CU, on any XCD, once the
-// storing workgroup has waited for its stores and arrived: no L2 write-back
-// per workgroup (an agent-scope release fence writes back the XCD's whole L2:
-// C2's merged launch +137 us with one per workgroup, profiles/r05_rank/).
-__device__ __forceinline__ void store_score(int32_t* p, int32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 // Consumer in a later launch (the entry is written): read entry i, reset it.
 // Wave-uniform.
 __device__ __forceinline__ int32_t list_take(const int32_t* items, int i) {
@@ -293,35 +285,6 @@ hipError_t launch_inter_x2p(const InterArgs& a, bool affine, bool f16, bool merg
 // boundary rows (the deferred tails' rows).  In device memory, not in the
 // kernel arguments: read from kernel arguments, the compiler kept the drain's
 // values in registers across the scan loops and spilled.
-// A ranking input (sw_rank.h topk_key): entry g of [0, n) is keys[g], or the
-// key of (scores[r], gid ? gid[r] : id_base + r) with r = rid ? rid[g] : g —
-// rid: a database's result ids (sw_scan_topk: only mapped slots), gid: a
-// shard's global ids (sw_topk_device_ids).
-struct TopkSrc {
-    const int32_t* scores;
-    const int64_t* keys;
-    const int32_t* rid;
-    const int32_t* gid;
-    int64_t id_base;
-};
-// The merged launch's ranking tail (sw_rank.h rank_tail): 256-thread
-// workgroups, chunks of at most kRankChunkPer keys per thread, the final
-// selection over nchunks x k <= kRankFinalPer per thread, k <= kRankMaxK.
-constexpr int kRankChunkPer = 32;
-constexpr int kRankFinalPer = 32;
-constexpr int kRankMaxK = 1024;
-struct RankArgs {
-    TopkSrc src;
-    int64_t n;          // entries
-    int32_t k;          // 0: no ranking
-    int32_t nchunks;    // chunks of `chunk` entries (the last one shorter)
-    int32_t chunk;
-    int32_t nfin;       // finishers: the last nfin workgroups to arrive
-    int32_t nwg;        // the launch's workgroups
-    int64_t* work;      // nchunks x k keys
-    int64_t* out;       // the k best, best first
-    int32_t* ctl;       // arrivals, chunk ticket, chunks ranked (zeroed per scan)
-};
 struct DrainArgs {
     InterArgs a16;
     InterArgs a32;
@@ -330,7 +293,6 @@ struct DrainArgs {
     int32_t* lists[4];  // list A, B, 1, 2: [count, items...]
     int32_t* heads[4];  // their dequeue heads (zeroed per scan)
     int32_t* fault;     // host-mapped word: a claimed entry never appeared (list_wait_take)
-    RankArgs rank;      // the scan's ranking, in the launch's tail (rank.k > 0)
 };
 bool lpt_supported(int ri);
 hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri,
@@ -423,9 +385,7 @@ uint64_t synth_hash(uint64_t seed, uint64_t id, uint64_t k);
 //   pin : the int32 intra kernel's lane-slotted image, rows < qpad_intra:
 //         [chunk of 64 ri rows][code][lane][rip] (null: not built)
 // The first launch also zeroes the rescue lists' counters and dequeue heads
-// and the ranking tail's counters (reset[2] := -1, the largest-flagged-block
-// slot; null pointers skipped).
-constexpr int kResetWords = 12;
+// (reset[2] := -1, the largest-flagged-block slot; null pointers skipped).
 constexpr int kAlphabet = 25;
 constexpr int kProfQueryChunk = 2048;
 struct ProfileArgs {
@@ -437,14 +397,27 @@ struct ProfileArgs {
     int32_t row0, row1;
     int32_t bias;
     int32_t ri, rip, qpad_intra;
-    int32_t* reset[kResetWords];
+    int32_t* reset[9];
     int8_t mat[kAlphabet * kAlphabet + 15];
     uint8_t q[kProfQueryChunk];
 };
 hipError_t launch_build_profile(const ProfileArgs& a, hipStream_t s);
 
+// A ranking input (sw_rank.h topk_key): entry g of [0, n) is keys[g], or the
+// key of (scores[r], gid ? gid[r] : id_base + r) with r = rid ? rid[g] : g —
+// rid: a database's result ids (sw_scan_topk: only mapped slots), gid: a
+// shard's global ids (sw_topk_device_ids).
+struct TopkSrc {
+    const int32_t* scores;
+    const int64_t* keys;
+    const int32_t* rid;
+    const int32_t* gid;
+    int64_t id_base;
+};
 // Device top-K (sw_topk.hip): keys = score << 32 | (2^31 - 1 - id), best
-// first, of entries [0, n) of src (TopkSrc).
+// first, of entries [0, n) of src.  The workspace holds the stages' keys and,
+// at its start, the one-launch form's counter (zero between launches: the
+// launch that uses it resets it).
 size_t topk_workspace_bytes(int64_t n, int k);
 hipError_t launch_topk(const TopkSrc& src, int64_t n, int k, int64_t* out, int64_t* work, hipStream_t s);
 

@@ -167,7 +167,7 @@ __global__ __launch_bounds__(256) void sw_inter_coop(InterArgs a) {
     if (wave == 0) {
         const int b = max(max(red[0][lane], red[1][lane]), max(red[2][lane], red[3][lane]));
         const int id = a.lane_ids[static_cast<size_t>(blk) * kLanes + lane];
-        if (id >= 0) store_score(a.scores + id, b);
+        if (id >= 0) a.scores[id] = b;
     }
 }
 

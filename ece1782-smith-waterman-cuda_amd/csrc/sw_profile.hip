@@ -17,7 +17,7 @@ namespace swk {
 
 // One thread per (code, row) entry of rows [row0, row1).
 __global__ __launch_bounds__(256) void sw_build_profile(ProfileArgs a) {
-    if (blockIdx.x == 0 && threadIdx.x < kResetWords) {  // the rescue lists' and ranking's counters (first launch only)
+    if (blockIdx.x == 0 && threadIdx.x < 9) {  // the rescue lists' counters and heads (first launch only)
         int32_t* p = a.reset[threadIdx.x];
         if (p) *p = threadIdx.x == 2 ? -1 : 0;
     }

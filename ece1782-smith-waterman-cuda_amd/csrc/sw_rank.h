@@ -1,6 +1,5 @@
-// sw_rank.h — device-side ranking: the radix select of sw_topk.hip as a
-// workgroup function, shared by the top-K kernels (sw_topk.hip) and the
-// merged scan launch's ranking tail (sw_inter_x2.hip, sw_scan_lpt).
+// sw_rank.h — device-side ranking: the radix select and the bitonic sort of
+// the top-K kernels (sw_topk.hip) as workgroup functions.
 //
 // Hits are ordered by score descending, then global id ascending; both fold
 // into one int64 key (score << 32 | (2^31 - 1 - id)) sorted descending.  A
@@ -32,14 +31,11 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     return (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo);
 }
 
-// Key g of a ranking input (TopkSrc, sw_kernels.h); SC1: the scores are
-// read with sc1 loads (written in the same launch by store_score).
-template <bool SC1 = false>
+// Key g of a ranking input (TopkSrc, sw_kernels.h).
 __device__ __forceinline__ uint64_t topk_key(const TopkSrc& s, int64_t g) {
     if (s.keys) return key_ord(s.keys[g]);
     const int64_t r = s.rid ? s.rid[g] : g;
-    const int32_t v = SC1 ? __hip_atomic_load(s.scores + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : s.scores[r];
-    return key_ord(make_key(v, s.gid ? s.gid[r] : s.id_base + r));
+    return key_ord(make_key(s.scores[r], s.gid ? s.gid[r] : s.id_base + r));
 }
 
 template <int T>
@@ -181,81 +177,6 @@ __device__ __forceinline__ void topk_sort_out(int64_t* sorted, int n, int k, int
     for (int i = t; i < k; i += T) out[i] = sorted[i];
 }
 
-// The ranking tail of a launch whose workgroups write the scores it ranks
-// (sw_scan_lpt with DrainArgs::rank): called by every thread of every
-// workgroup after its last score store.  The scores are write-through (sc1)
-// stores (store_score): once every wave of a workgroup has waited for its
-// stores, one lane arrives on r.ctl[0] (an agent-scope atomic add) and the
-// workgroups that read the scores use sc1 loads — the hand-off form
-// MI355X_MICROARCH.md measures valid with no release fence, whose L2
-// write-back per workgroup cost C2's launch 137 us.  The last r.nfin
-// workgroups to arrive stay: they
-// wait for every arrival (the last one never waits), take chunks of r.src by
-// ticket (r.ctl[1]) and write each chunk's k best to r.work; the workgroup
-// that ranks the last chunk (r.ctl[2]) selects the k best of those and sorts
-// them into r.out.  A finisher's wait is bounded (~60 ms): one that gives up
-// takes no chunk, so the finishers left (the last arrival at least) rank
-// them all.  smem: sizeof(TopkLds<T>) + 8 kRankMaxK bytes; task: 2 ints.
-template <int T>
-__device__ __forceinline__ void rank_tail(const RankArgs& r, char* smem, int* task) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) task[0] = __hip_atomic_fetch_add(r.ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const int arrived = task[0];
-    if (arrived < r.nwg - r.nfin) return;  // workgroup-uniform
-    if (threadIdx.x == 0) {
-        bool all = arrived == r.nwg - 1;
-        for (int spin = 0; !all && spin < (1 << 17); ++spin) {
-            all = __hip_atomic_load(r.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= r.nwg;
-            if (!all) __builtin_amdgcn_s_sleep(16);
-        }
-        task[1] = all;
-    }
-    __syncthreads();
-    if (!task[1]) return;
-    TopkLds<T>& L = *reinterpret_cast<TopkLds<T>*>(smem);
-    int64_t* const sorted = reinterpret_cast<int64_t*>(smem + (sizeof(TopkLds<T>) + 15) / 16 * 16);
-    const int t = threadIdx.x;
-    for (;;) {
-        __syncthreads();  // every thread has read task[0]
-        if (t == 0) task[0] = __hip_atomic_fetch_add(r.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const int c = task[0];
-        if (c >= r.nchunks) return;
-        const int64_t start = static_cast<int64_t>(c) * r.chunk;
-        const int m = static_cast<int>(min(static_cast<int64_t>(r.chunk), r.n - start));
-        uint64_t u[kRankChunkPer];
-#pragma unroll
-        for (int j = 0; j < kRankChunkPer; ++j) u[j] = j * T + t < m ? topk_key<true>(r.src, start + j * T + t) : 0;
-        int64_t* const w = r.work + static_cast<int64_t>(c) * r.k;
-        topk_select<T>(u, m, r.k, L, [&](int pos, uint64_t v) { w[pos] = key_of(v); });
-        for (int i = min(m, r.k) + t; i < r.k; i += T) w[i] = kKeyPad;
-        // this chunk's keys visible device-wide, then counted
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (t == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const int done = __hip_atomic_fetch_add(r.ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            task[1] = done == r.nchunks - 1;
-            if (task[1]) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-        }
-        __syncthreads();
-        if (!task[1]) continue;
-        // the last chunk ranked: the k best of every chunk's k
-        const int mf = r.nchunks * r.k;
-        uint64_t v[kRankFinalPer];
-#pragma unroll
-        for (int j = 0; j < kRankFinalPer; ++j) v[j] = j * T + t < mf ? key_ord(r.work[j * T + t]) : 0;
-        topk_select<T>(v, mf, r.k, L, [&](int pos, uint64_t x) { sorted[pos] = key_of(x); });
-        topk_sort_out<T>(sorted, min(mf, r.k), r.k, r.out);
-        return;
-    }
-}
 #endif
 
 }  // namespace swk

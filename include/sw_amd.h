@@ -324,13 +324,10 @@ SW_API int sw_topk_device_ids(sw_handle* h, const int32_t* scores_dev, int64_t n
  * of the database as sw_topk_device keys (score << 32 | 2^31 - 1 - global id,
  * best first, INT64_MIN past the database's end), over the subjects' result
  * ids r, with global id gid_dev[r] (device int32, >= 0) or, gid_dev NULL,
- * id_base + r.  The replacement of main.cpp:54-60's scan-then-collect for one
- * rank of the multi-GPU search: when the scan runs as one
- * merged launch (sw_last_kernel ends "+rank") its last workgroups rank the
- * scores in that launch, so the keys are ready when the scan's end event is
- * (sw_stream_wait_scan) and no top-K kernel queues behind the next scan;
- * otherwise a top-K launch follows the scan on its stream, before that
- * event.  1 <= k <= 4096.                                                  */
+ * id_base + r: main.cpp:54-60's scan-then-collect for one shard of the
+ * multi-GPU search in one call.  The top-K launch follows
+ * every stage that writes the scores and precedes the scan's end event
+ * (sw_stream_wait_scan).  1 <= k <= 4096.                                   */
 SW_API int sw_scan_rank_device(sw_handle* h, const sw_db* db, const uint8_t* query, int32_t qlen,
                                const sw_scoring* sc, int32_t* scores_dev, int32_t k, const int32_t* gid_dev,
                                int64_t id_base, int64_t* keys_out_dev);

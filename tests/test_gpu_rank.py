@@ -1,12 +1,11 @@
-"""GPU: sw_scan_rank_device — a scan and the device top-K of its scores in one
-call (the ranking no longer queues behind the next scan).
-When the scan runs as the merged launch its last workgroups rank the scores
-inside that launch (sw_rank.h rank_tail; sw_last_kernel ends "+rank"); other
-scan forms, and rankings too large for the tail, rank by a top-K launch after
-the scan.  Keys must equal the oracle's top-K of the same query at every k,
-id form and kernel form, and — at C2's size, where the oracle is too slow —
-the CPU top-K of the device's own scores (a ranking that read a score before
-its workgroup published it would differ: every scan rewrites every score)."""
+"""GPU: the scan's ranking.  sw_scan_rank_device scans
+and ranks in one call; sw_topk_device ranks in ONE launch (sw_topk_fused:
+chunks, then the last workgroup to arrive selects and sorts the survivors)
+whenever k <= 1,024 and the survivors fit, else by chained stages.  Keys
+must equal the oracle's top-K at every k, id form and scan form, and — at
+C2's size, where the oracle is too slow — the CPU top-K of the device's own
+scores, with the ranking on a second stream beside the next scan as bench.py
+runs it (a survivor read before its workgroup published it would differ)."""
 import numpy as np
 import pytest
 
@@ -27,6 +26,14 @@ def small_db(sw):
     return sw.synth.database(8000, shard=31)
 
 
+@pytest.fixture
+def merged(knobs):
+    """The merged launch on the small database: its wave pairs from 64
+    columns (C2's widths are far above the library's cut), the fp16-first
+    chain kept (the adaptive routing never moves work out of the launch)."""
+    knobs(lpt="1", pair_width="64", inter_i16_span="0", intra_i16_first="0")
+
+
 def _rank(sw, db, q, k, m, go, ge, gids=None, id_base=0):
     import torch
     dev = torch.device("cuda", 0)
@@ -39,51 +46,40 @@ def _rank(sw, db, q, k, m, go, ge, gids=None, id_base=0):
     return keys.cpu().numpy(), scores.cpu().numpy()
 
 
-@pytest.fixture
-def merged(knobs):
-    """The merged launch on the small database: its wave pairs from 64
-    columns (C2's widths are far above the library's cut), the fp16-first
-    chain kept (the adaptive routing never moves work out of the launch)."""
-    knobs(lpt="1", pair_width="64", inter_i16_span="0", intra_i16_first="0")
-
-
 @pytest.mark.parametrize("scoring", SCORINGS)
-def test_rank_in_merged_launch_equals_oracle(sw, oracle, handle, merged, small_db, scoring):
+def test_scan_rank_equals_oracle(sw, oracle, handle, merged, small_db, scoring):
+    """The merged launch's scores ranked at k from 1 to 2,000 (one launch up
+    to 1,024, chained stages past it), with ids offset and mapped."""
     mid, go, ge = scoring
     res, offs = small_db
     n = len(offs) - 1
+    ids = np.arange(n, dtype=np.int32)
     m = sw.capi.builtin_matrix(mid)
     db = sw.Database(handle, res, offs)
     gids = np.random.default_rng(3).permutation(3 * n)[:n].astype(np.int32)
     for L, shard in ((375, 50), (120, 51)):
         q = sw.synth.query(L, shard=shard)
         want = oracle.scan(q, res, offs, mat=m, gap_open=go, gap_extend=ge, nthreads=16)
-        for k in (1, 7, 100, 1024):
+        for k in (1, 7, 100, 1024, 2000):
             keys, _ = _rank(sw, db, q, k, m, go, ge)
-            assert handle.last_kernel().endswith("+rank"), handle.last_kernel()
-            assert np.array_equal(keys, sw.dist.local_topk(want, np.arange(n, dtype=np.int32), k)), (L, k)
+            assert "+lpt" in handle.last_kernel(), handle.last_kernel()
+            assert np.array_equal(keys, sw.dist.local_topk(want, ids, k)), (L, k)
         keys, _ = _rank(sw, db, q, 64, m, go, ge, id_base=12345)
-        assert np.array_equal(keys, sw.dist.local_topk(want, np.arange(n, dtype=np.int32) + 12345, 64))
+        assert np.array_equal(keys, sw.dist.local_topk(want, ids + 12345, 64))
         keys, _ = _rank(sw, db, q, 64, m, go, ge, gids=gids)
-        assert handle.last_kernel().endswith("+rank")
         assert np.array_equal(keys, sw.dist.local_topk(want, gids, 64))
     db.close()
 
 
-def test_rank_fallback_forms_equal_oracle(sw, oracle, handle, merged, knobs, small_db):
-    """k past the tail's limit (kRankMaxK 1,024), and scans that do not run
-    as the merged launch (sw_opts lpt 0; an int32-only scoring), rank by a
-    top-K launch after the scan: the same keys."""
+def test_scan_rank_other_scan_forms(sw, oracle, handle, knobs, small_db):
+    """Scans that do not run as the merged launch (sw_opts lpt 0; the int32
+    forms) rank the same keys."""
     res, offs = small_db
-    n = len(offs) - 1
-    ids = np.arange(n, dtype=np.int32)
+    ids = np.arange(len(offs) - 1, dtype=np.int32)
     db = sw.Database(handle, res, offs)
     q = sw.encode(read_query("P02232"))
     m = sw.capi.builtin_matrix(1)
     want = oracle.scan(q, res, offs, mat=m, gap_open=12, gap_extend=1, nthreads=16)
-    keys, _ = _rank(sw, db, q, 2000, m, 12, 1)
-    assert not handle.last_kernel().endswith("+rank")
-    assert np.array_equal(keys, sw.dist.local_topk(want, ids, 2000))
     knobs(lpt=0)
     keys, _ = _rank(sw, db, q, 100, m, 12, 1)
     assert "+lpt" not in handle.last_kernel()
@@ -94,7 +90,7 @@ def test_rank_fallback_forms_equal_oracle(sw, oracle, handle, merged, knobs, sma
     db.close()
 
 
-def test_rank_custom_result_ids_and_empty_query(sw, oracle, handle, merged):
+def test_scan_rank_custom_result_ids_and_empty_query(sw, oracle, handle, merged):
     """A database with its own result ids (gaps between them): the ranking
     runs over the subjects' ids only (unmapped score slots hold garbage and
     never appear); k past the database pads with INT64_MIN; an empty query
@@ -108,7 +104,6 @@ def test_rank_custom_result_ids_and_empty_query(sw, oracle, handle, merged):
     want = oracle.scan(q, res, offs, mat=m, gap_open=12, gap_extend=1, nthreads=16)
     for k in (1, 64, 1024):
         keys, _ = _rank(sw, db, q, k, m, 12, 1)
-        assert handle.last_kernel().endswith("+rank"), handle.last_kernel()
         assert np.array_equal(keys, sw.dist.local_topk(want, ids, k)), k
     keys, _ = _rank(sw, db, q, n + 50, m, 12, 1)  # k beyond the database: INT64_MIN after the n keys
     assert np.array_equal(keys, _padded(sw.dist.local_topk(want, ids, n), n + 50))
@@ -117,33 +112,67 @@ def test_rank_custom_result_ids_and_empty_query(sw, oracle, handle, merged):
     db.close()
 
 
+@pytest.mark.parametrize("n", [1, 4096, 4097, 8191, 65536, 65537, 524288, 570000, 2_000_000])
+@pytest.mark.parametrize("k", [1, 100, 1024, 1025])
+def test_topk_one_launch_sizes(sw, handle, n, k):
+    """sw_topk_device around the one-launch plan's edges (one chunk; 4,096-
+    and 8,192-key chunks; survivors up to 8,192; k past 1,024 chained),
+    many equal scores (ties broken by id), twice on one workspace (the
+    counter the last workgroup resets)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(n + k)
+    s = rng.integers(0, 60, n).astype(np.int32)
+    d = torch.from_numpy(s).to(dev)
+    for rep in range(2):
+        out = torch.zeros(k, dtype=torch.int64, device=dev)
+        handle.topk_device(d.data_ptr(), n, k, out.data_ptr(), id_base=rep)
+        torch.cuda.synchronize()
+        want = _padded(sw.dist.local_topk(s, np.arange(n, dtype=np.int32) + rep, k), k)
+        assert np.array_equal(out.cpu().numpy(), want), (n, k, rep)
+
+
 @pytest.mark.parametrize("scoring", SCORINGS)
-def test_rank_back_to_back_c2_size(sw, handle, scoring):
+def test_rank_beside_next_scan_c2_size(sw, handle, scoring):
     """C2's database (570,000 synthetic subjects, generated in HBM) scanned
-    back to back with alternating queries into two score buffers, ranked in
-    each scan's launch: every step's keys equal the CPU top-K of that step's
-    own scores (the affine scans rank in the launch's tail, the linear ones
-    — C2's size takes two launches under linear gaps — after it; the tail
-    reads every workgroup's scores through the
-    device-scope release / acquire pairs; a stale read would show the other
-    query's scores); the steps that repeat a query repeat its keys."""
+    back to back with alternating queries into a ring of score buffers; each
+    step's top-K runs on a second handle and stream beside the next scan, as
+    bench.py's exchange does (70 chunks of 8,192 in one launch).  Every
+    step's keys equal the CPU top-K of that step's own scores; the steps
+    that repeat a query repeat its keys."""
     import torch
     mid, go, ge = scoring
     dev = torch.device("cuda", 0)
     db = sw.Database.synthetic(handle, 1782, 570000)
     n = db.n_out
     m = sw.capi.builtin_matrix(mid)
+    stream = torch.cuda.Stream(dev)
+    handle.set_stream(stream.cuda_stream)
+    xstream = torch.cuda.Stream(dev, priority=-1)
+    xh = sw.Handle(0, env_opts=False)
+    xh.set_stream(xstream.cuda_stream)
     qs = [sw.encode(read_query("P07327")), sw.synth.query(250, shard=77)]
-    K = 100
-    bufs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(2)]
-    keys = [torch.zeros(K, dtype=torch.int64, device=dev) for _ in range(6)]
-    for i in range(6):
-        db.scan_rank_device(qs[i % 2], bufs[i % 2].data_ptr(), K, keys[i].data_ptr(), m, go, ge)
-        if i >= 4:  # the last two steps: their buffers are not rewritten afterwards
-            torch.cuda.synchronize()
-            s = bufs[i % 2].cpu().numpy()
+    K, NB, steps = 100, 3, 8
+    bufs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(NB)]
+    keys = [torch.zeros(K, dtype=torch.int64, device=dev) for _ in range(steps)]
+    ranked = [torch.cuda.Event() for _ in range(NB)]
+    try:
+        for i in range(steps):
+            b = i % NB
+            if i >= NB:
+                stream.wait_event(ranked[b])
+            db.scan_device(qs[i % 2], bufs[b].data_ptr(), m, go, ge)
+            handle.stream_wait_scan(xstream.cuda_stream)
+            xh.topk_device(bufs[b].data_ptr(), n, K, keys[i].data_ptr())
+            ranked[b].record(xstream)
+        torch.cuda.synchronize()
+        for i in range(steps - NB, steps):  # buffers not rewritten after their step
+            s = bufs[i % NB].cpu().numpy()
             assert np.array_equal(keys[i].cpu().numpy(), sw.dist.local_topk(s, np.arange(n, dtype=np.int32), K)), i
-    assert handle.last_kernel().endswith("+rank") == (go != ge), handle.last_kernel()
-    for i in range(4):  # same query, same keys
-        assert np.array_equal(keys[i].cpu().numpy(), keys[i + 2].cpu().numpy()), i
-    db.close()
+        for i in range(steps - 2):
+            assert np.array_equal(keys[i].cpu().numpy(), keys[i + 2].cpu().numpy()), i
+    finally:
+        torch.cuda.synchronize()
+        handle.set_stream(None)
+        xh.close()
+        db.close()
