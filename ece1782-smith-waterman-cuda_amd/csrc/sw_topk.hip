@@ -26,9 +26,9 @@
 // allocation granule) fits nowhere until the scan's grid has drained: its
 // kernel traces showed the ranking's first stage taking a whole scan (6.15 ms
 // on C2).  For k <= 1,024 the stages run 256-thread workgroups (one wave per
-// SIMD), which fit in the registers one finished scan workgroup leaves:
-// C2 (570k scores, k = 100) ranks in 3 launches (140 chunks, 4, 1); larger k
-// keeps 1,024 threads (a stage must keep fewer keys than it reads).
+// SIMD), which fit in the registers one finished scan workgroup leaves
+// (chained, C2's 570k scores at k = 100 took 3 launches: 140 chunks, 4, 1);
+// larger k keeps 1,024 threads (a stage must keep fewer keys than it reads).
 #include <algorithm>
 
 #include "sw_rank.h"
