@@ -436,6 +436,35 @@ __device__ __forceinline__ void ring_load(uint32_t (&v)[SG], const int4* ring, i
     }
 }
 
+// Flag-synchronised wave groups (SW_PAIR_FLAGS=1): instead of one workgroup
+// barrier per sub-group (a tick shared by every wave of the workgroup, the
+// two pairs of a workgroup included), each wave publishes in LDS how many
+// sub-groups it has completed over its passes, and waits only where the data
+// need it: before reading column block x of its input (the ring of the wave
+// before it, or for wave 0 of a later round the boundary in HBM) until the
+// producer has completed the sub-group that stored it (x + 1 of its pass),
+// and before writing ring slot x % 4 until the consumer has read the block
+// that slot held (x - 4, read one sub-group ahead).  The producer may then
+// run 3 to 5 sub-groups ahead of its consumer; nothing waits for the other
+// group of the workgroup or for a wave that is not a neighbour.
+#ifndef SW_PAIR_FLAGS
+#define SW_PAIR_FLAGS 0
+#endif
+constexpr bool kPairFlags = SW_PAIR_FLAGS != 0;
+struct PairSync {
+    int* prog;      // LDS: completed sub-groups of each wave of the workgroup
+    int me;         // this wave
+    int base;       // this wave's count at the start of this pass (its k-th: k S)
+    int pred;       // the wave that produced this pass's input (-1: none)
+    int pred_base;  // its count at the start of the pass that produced it
+    int succ;       // the wave that reads this pass's ring output (-1: none)
+    int S;          // sub-groups per pass
+};
+__device__ __forceinline__ void pair_wait(const int* prog, int wave, int need) {
+    while (__hip_atomic_load(prog + wave, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+        __builtin_amdgcn_s_sleep(1);
+}
+
 // One pass (rows [s0, s0 + 2R)) of one 64-subject block.  PAIR: the pass
 // is part of a wave pair's pipeline (sw_inter_x2p): the boundary comes from /
 // goes to the partner wave through an LDS ring instead of HBM when ring_in /
@@ -458,7 +487,7 @@ constexpr bool kHoistFma = SW_HOIST_FMA != 0;
 template <int R, int SG, bool AFFINE, bool F16, bool PAIR, int CR = 16, bool CHAIN = false>
 __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32_t ncols, uint64_t base, int lane,
                                          int s0, Best<F16>& best, const int4* ring_in, int4* ring_out,
-                                         int* tick) {
+                                         int* tick, const PairSync* ps = nullptr) {
     static_assert(!(CHAIN && PAIR), "chained passes: single-wave blocks only");
     // SG: sub-group width = the lag (columns) between the two strips
     // CR: profile rows per LDS chunk (16: 2 x 4 ds_read_b128 in flight; 8
@@ -531,7 +560,14 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
 #pragma unroll
     for (int q = 0; q < SG / 4; ++q) rp[q] = 0x19191919u;  // virtual columns before the subject
     load_codes<SG>(rc, a.residues + base, true);
+    // (flags: column block x of the input is ready once its producer has
+    // completed sub-group x + 1 of its pass)
+    auto wait_in = [&](uint32_t x) {
+        if constexpr (PAIR && kPairFlags)
+            pair_wait(ps->prog, ps->pred, ps->pred_base + min(static_cast<int>(x) + 2, ps->S));
+    };
     if (!first) {
+        wait_in(0);
         if (PAIR && ring_in) ring_load<SG>(bin, ring_in, 0, lane);
         else load_bnd<SG, AFFINE>(bin, bnd, base);
     }
@@ -600,6 +636,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
         if (has_next) {
             load_codes<SG>(rn, a.residues + base + noff, next_lo);
             if (!next_first && next_lo) {
+                wait_in(ncol / SG);
                 if (PAIR && ring_in) ring_load<SG>(bin_n, ring_in, (ncol / SG) % kRingSlots, lane);
                 else load_bnd<SG, AFFINE>(bin_n, bnd, base + noff);
             }
@@ -777,6 +814,9 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
             for (int q = 0; q < SG; ++q) hb[q] = AFFINE ? hi_hi(dl_h[q], dl_f[q]) : hi_hi(dl_h[q], dl_h[q]);
             const uint32_t pc = CHAIN ? (lo_c == 0 ? ncols - SG : lo_c - SG) : col0 - SG;
             if (PAIR && ring_out) {
+                // (flags: the slot's previous block, x - 4, has been read)
+                if constexpr (kPairFlags)
+                    pair_wait(ps->prog, ps->succ, ps->base + static_cast<int>(pc / SG) - kRingSlots);
                 ring_store<SG>(ring_out, (pc / SG) % kRingSlots, lane, hb);
             } else {
                 const uint64_t poff = (pc >> 4) * kGroupBytes + (pc & 15);
@@ -792,7 +832,13 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
 #pragma unroll
             for (int q = 0; q < SG; ++q) bin[q] = (next_first || !next_lo) ? bz[q] : bin_n[q];
         }
-        if constexpr (PAIR) {
+        if constexpr (PAIR && kPairFlags) {
+            // this sub-group's ring and HBM stores (and its ring reads) are
+            // complete before its count
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __hip_atomic_store(ps->prog + ps->me, ps->base + static_cast<int>(col0 / SG) + 1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if constexpr (PAIR) {
             __syncthreads();  // one tick of the pair's clock
             ++*tick;
         }
@@ -901,6 +947,7 @@ struct X2pSmem {
     X2Lds<R> lds[kWavesPerWG];
     int4 ring[kWavesPerWG - kWavesPerWG / GMAX][kRingSlots * (SG / 4) * kLanes];
     uint32_t part[kWavesPerWG][kLanes];
+    int prog[kWavesPerWG];  // SW_PAIR_FLAGS: completed sub-groups per wave
 };
 
 // One workgroup's work (wgi = its index in the launch's numbering):
@@ -935,7 +982,7 @@ __device__ __forceinline__ bool x2p_wg(const InterArgs& a, int wgi, int quad_end
     const int gi = wave / G, w = wave % G;
     const int passes = (a.qpad + 2 * R - 1) / (2 * R);
     // the workgroup's clock runs to the longest of its blocks
-    int tmax = 0;
+    int tmax = 0;  // (the tick form only)
     for (int q = 0; q < NG; ++q) {
         const int b = first + q;
         if (b < npair) tmax = max(tmax, group_ticks(block_cols(a, b), passes, SG, G));
@@ -945,24 +992,42 @@ __device__ __forceinline__ bool x2p_wg(const InterArgs& a, int wgi, int quad_end
     best.init(a);
     int tick = 0;
     const uint64_t t0 = trace_now();
+    if constexpr (kPairFlags) {
+        if (threadIdx.x < kWavesPerWG) sm.prog[threadIdx.x] = 0;
+        __syncthreads();
+    }
     if (blk < npair) {
         const uint32_t ncols = block_cols(a, blk);
         const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
         const int per = max(static_cast<int>(ncols) / SG + 1, G * kPairLag);
         const int4* rin = w > 0 ? ring[gi * (G - 1) + w - 1] : nullptr;
         int4* rout = w < G - 1 ? ring[gi * (G - 1) + w] : nullptr;
+        PairSync ps{sm.prog, wave, 0, -1, 0, w < G - 1 ? wave + 1 : -1, static_cast<int>(ncols) / SG + 1};
         for (int p = w; p < passes && ncols > 0; p += G) {
-            const int start = (p / G) * per + kPairLag * w;
-            while (tick < start) {
-                __syncthreads();
-                ++tick;
+            if constexpr (kPairFlags) {
+                // pass p's input: pass p - 1, by the wave before (this round)
+                // or by the group's last wave (the round before, in HBM)
+                const int k = p / G;
+                ps.base = k * ps.S;
+                ps.pred = p == 0 ? -1 : w > 0 ? wave - 1 : wave + G - 1;
+                ps.pred_base = (w > 0 ? k : k - 1) * ps.S;
+            } else {
+                const int start = (p / G) * per + kPairLag * w;
+                while (tick < start) {
+                    __syncthreads();
+                    ++tick;
+                }
             }
-            x2s_pass<R, SG, AFFINE, F16, true, kPairCR>(a, lds[wave], ncols, base, lane, p * 2 * R, best, rin, rout, &tick);
+            x2s_pass<R, SG, AFFINE, F16, true, kPairCR>(a, lds[wave], ncols, base, lane, p * 2 * R, best, rin, rout,
+                                                        &tick, &ps);
         }
     }
-    while (tick < tmax) {
-        __syncthreads();
-        ++tick;
+    (void)tmax;
+    if constexpr (!kPairFlags) {
+        while (tick < tmax) {
+            __syncthreads();
+            ++tick;
+        }
     }
     if (blk < npair && w > 0) part[wave][lane] = P::bits(best.value(a));
     __syncthreads();
