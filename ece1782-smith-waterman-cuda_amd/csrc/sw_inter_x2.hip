@@ -436,7 +436,7 @@ __device__ __forceinline__ void ring_load(uint32_t (&v)[SG], const int4* ring, i
     }
 }
 
-// Flag-synchronised wave groups (SW_PAIR_FLAGS=1): instead of one workgroup
+// Flag-synchronised wave groups (affine gaps; SW_PAIR_FLAGS): instead of one workgroup
 // barrier per sub-group (a tick shared by every wave of the workgroup, the
 // two pairs of a workgroup included), each wave publishes in LDS how many
 // sub-groups it has completed over its passes, and waits only where the data
@@ -444,13 +444,22 @@ __device__ __forceinline__ void ring_load(uint32_t (&v)[SG], const int4* ring, i
 // before it, or for wave 0 of a later round the boundary in HBM) until the
 // producer has completed the sub-group that stored it (x + 1 of its pass),
 // and before writing ring slot x % 4 until the consumer has read the block
-// that slot held (x - 4, read one sub-group ahead).  The producer may then
-// run 3 to 5 sub-groups ahead of its consumer; nothing waits for the other
-// group of the workgroup or for a wave that is not a neighbour.
+// that slot held (x - 4: the consumer has completed its sub-group x - 4; at
+// a pass's first four blocks, the consumer's previous pass up to its last
+// ring read: the slots restart at every pass, so the previous occupant is
+// not x - 4 across the wrap).  The producer then runs 3 or 4 sub-groups
+// ahead of its consumer; nothing waits for the other group of the workgroup
+// or for a wave that is not a neighbour.
+// Measured (profiles/r05_ab/pair_flags/, same box, two runs each): affine
+// gaps C2 +0.3 %, its 1/8 share +0.9 %, 1/4 +0.4 %, wave groups on every
+// block +1.6 % against the tick form; the linear cell's cheaper sub-groups
+// lost 0.1-0.5 % with the per-sub-group release and count.  SW_PAIR_FLAGS:
+// 0 ticks everywhere, 1 flags everywhere, 2 flags under affine gaps (default).
 #ifndef SW_PAIR_FLAGS
-#define SW_PAIR_FLAGS 0
+#define SW_PAIR_FLAGS 2
 #endif
-constexpr bool kPairFlags = SW_PAIR_FLAGS != 0;
+template <bool AFFINE>
+constexpr bool pair_flags() { return SW_PAIR_FLAGS == 1 || (SW_PAIR_FLAGS == 2 && AFFINE); }
 struct PairSync {
     int* prog;      // LDS: completed sub-groups of each wave of the workgroup
     int me;         // this wave
@@ -562,6 +571,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     load_codes<SG>(rc, a.residues + base, true);
     // (flags: column block x of the input is ready once its producer has
     // completed sub-group x + 1 of its pass)
+    constexpr bool kPairFlags = pair_flags<AFFINE>();
     auto wait_in = [&](uint32_t x) {
         if constexpr (PAIR && kPairFlags)
             pair_wait(ps->prog, ps->pred, ps->pred_base + min(static_cast<int>(x) + 2, ps->S));
@@ -814,9 +824,15 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
             for (int q = 0; q < SG; ++q) hb[q] = AFFINE ? hi_hi(dl_h[q], dl_f[q]) : hi_hi(dl_h[q], dl_h[q]);
             const uint32_t pc = CHAIN ? (lo_c == 0 ? ncols - SG : lo_c - SG) : col0 - SG;
             if (PAIR && ring_out) {
-                // (flags: the slot's previous block, x - 4, has been read)
-                if constexpr (kPairFlags)
-                    pair_wait(ps->prog, ps->succ, ps->base + static_cast<int>(pc / SG) - kRingSlots);
+                // (flags: the slot's previous block has been read: x - 4 of
+                // this pass, read before the consumer's sub-group x - 4 ends
+                // (block 0 before its pass starts, the others one sub-group
+                // ahead), or for x < 4 one of the consumer's previous pass,
+                // whose last ring read is in its sub-group S - 3)
+                if constexpr (kPairFlags) {
+                    const int x = static_cast<int>(pc / SG);
+                    pair_wait(ps->prog, ps->succ, x >= kRingSlots ? ps->base + x - kRingSlots + 1 : ps->base - 2);
+                }
                 ring_store<SG>(ring_out, (pc / SG) % kRingSlots, lane, hb);
             } else {
                 const uint64_t poff = (pc >> 4) * kGroupBytes + (pc & 15);
@@ -892,8 +908,10 @@ __device__ __forceinline__ bool x2s_block(const InterArgs& a, int blk, X2Lds<R>&
 // w + 2G, ..., kPairLag sub-groups behind wave w - 1.  Within a round the
 // boundary (H | F << 16) goes from wave w to wave w + 1 through an LDS ring;
 // from one round to the next (wave G-1 -> wave 0) through HBM as in the
-// single-wave kernel.  All four waves of the workgroup share one clock: one
-// __syncthreads per sub-group.  Schedule of a block whose pass takes
+// single-wave kernel.  Linear gaps: all four waves of the workgroup share one
+// clock, one __syncthreads per sub-group (below); affine gaps: each wave
+// waits only for its neighbours' progress counts (PairSync, above), with the
+// same data dependencies.  Schedule of a block whose pass takes
 // S = width / SG + 1 ticks: round r of wave w starts at tick
 // r * max(S, G kPairLag) + kPairLag w, so
 //   * wave w + 1 reads sub-group g of a ring 2 ticks after wave w wrote it and
@@ -992,6 +1010,7 @@ __device__ __forceinline__ bool x2p_wg(const InterArgs& a, int wgi, int quad_end
     best.init(a);
     int tick = 0;
     const uint64_t t0 = trace_now();
+    constexpr bool kPairFlags = pair_flags<AFFINE>();
     if constexpr (kPairFlags) {
         if (threadIdx.x < kWavesPerWG) sm.prog[threadIdx.x] = 0;
         __syncthreads();
