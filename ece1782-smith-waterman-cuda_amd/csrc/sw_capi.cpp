@@ -401,6 +401,7 @@ struct sw_db {
     // sw_scan_lpt work tables (longest first), per scan shape
     struct LptTable {
         int32_t qpad, qpad_intra, ri, npair, group /* quad blocks */, n;
+        bool affine;
         int32_t npipe;  // the longest pairs, in the pipelined form
         int32_t pipe_opt;  // sw_opts lpt_pipe the table was built under
         int32_t* d_order;
@@ -1024,6 +1025,14 @@ constexpr double kTickUs = 7.4;
 // us, profiles/r04_*/: with the doubled cost the long subjects start early
 // enough, C2's 1/8 share +0.8 %)
 double intra_step_us(int ri) { return 2 * 0.157 * (ri * 28.8 + 80.0) / (6 * 28.8 + 80.0); }
+// Under linear gaps the intra step is relatively dearer than under affine
+// ones (C2's 1/8 share, profiles/r05_trace/: intra / inter item medians 0.31
+// against 0.28); scaling its estimates for linear scans by 85, 120 or 140 %
+// (CAPIFLAGS=-DSW_LPT_LIN_INTRA=...) made the share's reference-scoring rate
+// 1.8, 0.8 and 3.6 % lower (profiles/r05_ab/lpt_lin_intra/): 100.
+#ifndef SW_LPT_LIN_INTRA
+#define SW_LPT_LIN_INTRA 100
+#endif
 
 // The widest group blocks of the merged launch run by quads: those at least
 // kQuadFrac x the long threshold wide, whose pair latency would otherwise
@@ -1062,11 +1071,11 @@ double group_ticks_host(int64_t ncols, int passes, int G) {
 }
 
 // The work table of sw_scan_lpt for this scan shape (built once, cached).
-int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad,
+int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad, bool affine,
               const int32_t** order, int* n, int32_t* npipe_out) {
     for (const auto& t : db->lpt_tables)
         if (t.qpad == qpad && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad &&
-            t.pipe_opt == db->h->opts.lpt_pipe) {
+            t.pipe_opt == db->h->opts.lpt_pipe && t.affine == affine) {
             *order = t.d_order;
             *n = t.n;
             *npipe_out = t.npipe;
@@ -1079,6 +1088,7 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     const int64_t npairs = (db->nlong + 1) / 2;
     const int64_t iwg = (npairs + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
     const int nch = qpad_intra / (swk::kLanes * ri);
+    const double step_us = intra_step_us(ri) * (affine ? 1.0 : SW_LPT_LIN_INTRA / 100.0);
     std::vector<std::pair<double, int32_t>> w;
     w.reserve(static_cast<size_t>(pwg + swg + iwg));
     auto width = [&](int64_t b) { return static_cast<int64_t>(db->h_blk_groups[b]) * swk::kGroupCols; };
@@ -1105,7 +1115,7 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     double inter_max = 0;
     for (const auto& e : w) inter_max = std::max(inter_max, e.first);
     auto pair_us = [&](int64_t p) { return (db->h_llen[static_cast<size_t>(2 * p)] + swk::kLanes - 1) * nch *
-                                           intra_step_us(ri); };
+                                           step_us; };
     int64_t npipe = 0;
     if (nchp <= swk::kWavesPerWG) {
         if (db->h->opts.lpt_pipe >= 0) npipe = db->h->opts.lpt_pipe;
@@ -1117,7 +1127,7 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     for (int64_t g = npipe_wg; g < iwg; ++g) {
         const int64_t first = std::max<int64_t>(8 * g, 2 * npipe);  // its longest subject not pipelined
         if (first >= db->nlong) continue;
-        w.emplace_back((db->h_llen[static_cast<size_t>(first)] + swk::kLanes - 1) * nch * intra_step_us(ri),
+        w.emplace_back((db->h_llen[static_cast<size_t>(first)] + swk::kLanes - 1) * nch * step_us,
                        static_cast<int32_t>(-1 - g));
     }
     // (sw_scan_lpt item -1 - (iwg + pair)), ahead of everything
@@ -1131,7 +1141,7 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
         ord[k] = w[k].second;
         cost[k] = static_cast<float>(w[k].first);
     }
-    sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, static_cast<int32_t>(ord.size()),
+    sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, static_cast<int32_t>(ord.size()), affine,
                       static_cast<int32_t>(npipe), db->h->opts.lpt_pipe, nullptr, cost};
     HIPCHECK(hipMalloc(reinterpret_cast<void**>(&t.d_order), ord.size() * sizeof(int32_t)));
     HIPCHECK(hipMemcpy(t.d_order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -1777,7 +1787,8 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
             const int32_t nquad = lpt_quad_blocks(db, npair);
             a.blk_quad = nquad;
             int32_t npipe = 0;
-            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, &order, &nwg, &npipe))) return rc;
+            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, affine, &order, &nwg, &npipe)))
+                return rc;
             lpt_intra.pipe_pairs = npipe;
             const swk::DrainArgs* dargs = nullptr;
             if (drain) {
