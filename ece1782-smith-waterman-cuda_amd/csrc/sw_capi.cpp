@@ -229,7 +229,7 @@ sw_opts default_opts() {
     o.size = static_cast<int32_t>(sizeof o);
     for (int32_t* f : {&o.lpt, &o.lpt_pipe, &o.quad_width, &o.pair_width, &o.pair_group, &o.coop_width,
                        &o.coop_skew, &o.intra_x2, &o.intra_x2_rows, &o.intra_i16_first, &o.inter_i16_span,
-                       &o.int16_guard, &o.rescue_stats})
+                       &o.int16_guard, &o.rescue_stats, &o.tail_pairs, &o.lpt_persist})
         *f = -1;
     return o;
 }
@@ -400,7 +400,7 @@ struct sw_db {
     std::vector<int32_t> h_llen;         // long subjects' lengths, longest first
     // sw_scan_lpt work tables (longest first), per scan shape
     struct LptTable {
-        int32_t qpad, qpad_intra, ri, npair, group /* quad blocks */, n;
+        int32_t qpad, qpad_intra, ri, npair, group /* quad blocks */, tail /* tail-pair blocks */, n;
         bool affine;
         int32_t npipe;  // the longest pairs, in the pipelined form
         int32_t pipe_opt;  // sw_opts lpt_pipe the table was built under
@@ -896,7 +896,7 @@ struct Profiles {
 // rows; the first also zeroes the rescue lists' counters `reset`) in one of
 // the handle's profile slots, on the scan's stream.
 int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* mat, int go, bool affine,
-                   int32_t qpad_inter, bool want16, int ri, int32_t qpad_intra, int32_t* const (&reset)[9],
+                   int32_t qpad_inter, bool want16, int ri, int32_t qpad_intra, int32_t* const (&reset)[10],
                    Profiles* P) {
     for (int32_t i = 0; i < qlen; ++i)
         if (q[i] >= SW_ALPHABET) return fail(SW_E_INVALID, "query residue code out of range (use sw_encode)");
@@ -947,7 +947,7 @@ int build_profiles(sw_handle* h, const uint8_t* q, int32_t qlen, const int8_t* m
     a.ri = ri;
     a.rip = rip;
     a.qpad_intra = ri ? qpad_intra : 0;
-    for (int k = 0; k < 9; ++k) a.reset[k] = reset[k];
+    for (int k = 0; k < 10; ++k) a.reset[k] = reset[k];
     std::memcpy(a.mat, mat, 625);
     const int32_t rows = std::max(P->stride, a.qpad_intra);
     for (int32_t r0 = 0; r0 < rows; r0 += swk::kProfQueryChunk) {
@@ -1054,6 +1054,32 @@ int32_t lpt_quad_blocks(const sw_db* db, int32_t npair) {
     return n;
 }
 
+// The narrowest blocks of the merged launch run by wave pairs (x2p_wg's tail
+// range): the launch's last-dispatched work is its narrowest single-wave
+// workgroups, which start together once the rest is placed, and the longest
+// of them sets the end — C2's last 10 % ran at 73 % of the workgroup slots,
+// 4 % of the launch idle (profiles/r05_trace/).  Pairs halve those blocks'
+// latency for a few % more wave time on them.  Default: half a round of
+// pair workgroups (2 blocks each; 2 workgroups per CU: as many blocks as
+// workgroup slots) when the single-wave workgroups fill the GPU more than
+// twice over; sw_opts tail_pairs n: the narrowest n blocks.  C2 (256 CUs)
+// over 128-3,072 blocks: 512 best, +1.5 % (1,024 +0.8 %, 3,072 -0.4 %;
+// profiles/r05_ab/tail_pairs/).
+int32_t lpt_tail_blocks(const sw_db* db, int32_t npair, int passes) {
+    const int64_t singles = db->nblocks - npair;
+    if (passes < 2 || singles < 2) return 0;
+    int64_t n = 0;
+    if (db->h->opts.tail_pairs >= 0) {
+        n = db->h->opts.tail_pairs;
+    } else {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, db->h->device) != hipSuccess) cus = 0;
+        const int64_t slots = 2 * static_cast<int64_t>(cus);  // workgroups per CU: 2
+        if (slots > 0 && singles > 2 * swk::kWavesPerWG * slots) n = slots;
+    }
+    return static_cast<int32_t>(std::min<int64_t>(n, singles - 1));
+}
+
 // Ticks of a single-wave block (x2s_block: chained passes when ncols >= 32).
 double single_ticks(int64_t ncols, int passes) {
     if (ncols <= 0) return 0;
@@ -1071,11 +1097,11 @@ double group_ticks_host(int64_t ncols, int passes, int G) {
 }
 
 // The work table of sw_scan_lpt for this scan shape (built once, cached).
-int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad, bool affine,
-              const int32_t** order, int* n, int32_t* npipe_out) {
+int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad, int32_t ntail,
+              bool affine, const int32_t** order, int* n, int32_t* npipe_out) {
     for (const auto& t : db->lpt_tables)
         if (t.qpad == qpad && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad &&
-            t.pipe_opt == db->h->opts.lpt_pipe && t.affine == affine) {
+            t.tail == ntail && t.pipe_opt == db->h->opts.lpt_pipe && t.affine == affine) {
             *order = t.d_order;
             *n = t.n;
             *npipe_out = t.npipe;
@@ -1084,13 +1110,15 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     const int passes = qpad / 64;
     const int64_t nb = db->nblocks;
     const int64_t pwg = nquad + (npair - nquad + 1) / 2;
-    const int64_t swg = (nb - npair + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
+    const int64_t tail = nb - ntail;  // blocks [tail, nb) by pairs
+    const int64_t swg = (tail - npair + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
+    const int64_t twg = (ntail + 1) / 2;
     const int64_t npairs = (db->nlong + 1) / 2;
     const int64_t iwg = (npairs + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
     const int nch = qpad_intra / (swk::kLanes * ri);
     const double step_us = intra_step_us(ri) * (affine ? 1.0 : SW_LPT_LIN_INTRA / 100.0);
     std::vector<std::pair<double, int32_t>> w;
-    w.reserve(static_cast<size_t>(pwg + swg + iwg));
+    w.reserve(static_cast<size_t>(pwg + swg + twg + iwg));
     auto width = [&](int64_t b) { return static_cast<int64_t>(db->h_blk_groups[b]) * swk::kGroupCols; };
     for (int64_t g = 0; g < nquad; ++g) w.emplace_back(group_ticks_host(width(g), passes, 4) * kTickUs, g);
     for (int64_t g = nquad; g < pwg; ++g) {
@@ -1104,6 +1132,10 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     for (int64_t g = 0; g < swg; ++g)  // widest first: the workgroup's first block bounds it
         w.emplace_back(single_ticks(width(npair + g * swk::kWavesPerWG), passes) * kTickUs,
                        static_cast<int32_t>(pwg + g));
+    for (int64_t g = 0; g < twg; ++g) {  // tail pairs: the first block of two is the wider
+        w.emplace_back(group_ticks_host(width(tail + 2 * g), passes, 2) * kTickUs,
+                       static_cast<int32_t>(pwg + swg + g));
+    }
     // The longest pairs whose one-wave latency would exceed every inter
     // item's run in the pipelined form (a 128-row query chunk per wave,
     // ix2::intra_x2_wg PIPE; at most 4 chunks): a pair of one outlier subject
@@ -1141,7 +1173,7 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
         ord[k] = w[k].second;
         cost[k] = static_cast<float>(w[k].first);
     }
-    sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, static_cast<int32_t>(ord.size()), affine,
+    sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, ntail, static_cast<int32_t>(ord.size()), affine,
                       static_cast<int32_t>(npipe), db->h->opts.lpt_pipe, nullptr, cost};
     HIPCHECK(hipMalloc(reinterpret_cast<void**>(&t.d_order), ord.size() * sizeof(int32_t)));
     HIPCHECK(hipMemcpy(t.d_order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -1515,6 +1547,8 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
     int32_t* const list1 = db->d_lrescue ? db->d_lrescue + par * lstride : nullptr;  // flagged by the fp16 pass
     int32_t* const list2 = list1 ? list1 + db->nlong + 1 : nullptr;                  // ... and again by int16
     int32_t* const headA = listA ? maxA + 2 : nullptr;  // the drain's dequeue heads: A, B, 1, 2
+    // the merged launch's work counter (the spare word; persistent form)
+    int32_t* const lpt_next = (lpt && listA && O.lpt_persist != 0) ? maxA + 1 : nullptr;
     int32_t* const head1 = list1 ? list2 + db->nlong + 1 : nullptr;
     // the rescue tail on its own stream and boundary rows (see sw_handle::tail)
     const bool deferred = !drain && defer && (!(multi_inter || multi_intra) || ensure_rbnd(db, affine, intra_x2));
@@ -1526,9 +1560,9 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
     {
         int32_t* const cA = (rescue && db->nblocks) ? listA : nullptr;
         int32_t* const c1 = (db->nlong && intra_x2) ? list1 : nullptr;
-        int32_t* const reset[9] = {cA, (cA && f16) ? listB : nullptr, (cA && f16) ? maxA : nullptr, c1,
-                                   c1 ? list2 : nullptr, drain ? headA : nullptr, drain ? headA + 1 : nullptr,
-                                   drain ? head1 : nullptr, drain ? head1 + 1 : nullptr};
+        int32_t* const reset[10] = {cA, (cA && f16) ? listB : nullptr, (cA && f16) ? maxA : nullptr, c1,
+                                    c1 ? list2 : nullptr, drain ? headA : nullptr, drain ? headA + 1 : nullptr,
+                                    drain ? head1 : nullptr, drain ? head1 + 1 : nullptr, lpt_next};
         if ((rc = build_profiles(h, query, qlen, mat, go, affine,
                                  std::max({qpad_inter, qpad_rescue, qpad_coop, qpad_list, qpad_intra2}),
                                  x2 || intra_x2, ri, qpad_intra, reset, &P)))
@@ -1776,6 +1810,7 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
             ++h->launches;
         }
         MARK(6, h->stream);
+        int32_t ntail = 0;  // merged launch: the narrowest blocks by pairs
         if (lpt) {
             // one launch: the inter groups + single waves and the long
             // subjects' fp16 pass, longest work first; then the long
@@ -1786,8 +1821,10 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
             int nwg = 0;
             const int32_t nquad = lpt_quad_blocks(db, npair);
             a.blk_quad = nquad;
+            ntail = lpt_tail_blocks(db, npair, qpad_inter / 64);
+            a.blk_tail = static_cast<int32_t>(db->nblocks) - ntail;
             int32_t npipe = 0;
-            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, affine, &order, &nwg, &npipe)))
+            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, ntail, affine, &order, &nwg, &npipe)))
                 return rc;
             lpt_intra.pipe_pairs = npipe;
             const swk::DrainArgs* dargs = nullptr;
@@ -1832,11 +1869,13 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
                 const std::vector<uint64_t> key = {
                     reinterpret_cast<uint64_t>(P.dev), P.off8, P.off16, P.intra_off, static_cast<uint64_t>(par),
                     reinterpret_cast<uint64_t>(scores_dev), static_cast<uint64_t>(qlen), skey,
-                    static_cast<uint64_t>(npair), static_cast<uint64_t>(nquad), static_cast<uint64_t>(P.stride),
+                    static_cast<uint64_t>(npair), static_cast<uint64_t>(nquad) | static_cast<uint64_t>(ntail) << 32,
+                    static_cast<uint64_t>(P.stride),
                     reinterpret_cast<uint64_t>(a.trace)};
                 if ((rc = drain_blob(db, h->stream, key, d, &dargs))) return rc;
             }
-            HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, order, nwg, affine, ri2, h->stream, dargs));
+            HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, order, nwg, affine, ri2, h->stream, dargs, lpt_next,
+                                          O.lpt_persist >= 2 ? O.lpt_persist : 0));
             // (a draining launch ends the scan: its end event is ev[3])
             if (!drain) MARK(7, h->stream);
             if ((rc = launch_long(true))) return rc;
@@ -1851,6 +1890,7 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
         h->last_kernel = swk::inter_kernel_name(shape, affine);
         if (npair) h->last_kernel.replace(0, std::strlen("sw_inter_x2s"), "sw_inter_x2p");  // + wave pairs
         if (nr) h->last_kernel += "+int16[0," + std::to_string(nr) + ")";
+        if (ntail) h->last_kernel += "+tail" + std::to_string(ntail);
         if (lpt) h->last_kernel += drain ? "+lpt+drain" : "+lpt";
         if (!lpt) MARK(7, h->stream);
         ++h->launches;
@@ -2141,7 +2181,9 @@ int sw_opts_from_env(sw_opts* o) {
                 {"SW_INTRA_I16_FIRST", &o->intra_i16_first},
                 {"SW_INTER_I16_SPAN", &o->inter_i16_span},
                 {"SW_INT16_GUARD", &o->int16_guard},
-                {"SW_RESCUE_STATS", &o->rescue_stats}};
+                {"SW_RESCUE_STATS", &o->rescue_stats},
+                {"SW_TAIL_PAIRS", &o->tail_pairs},
+                {"SW_LPT_PERSIST", &o->lpt_persist}};
     for (const auto& k : ints)
         if (const char* e = std::getenv(k.name); e && e[0]) *k.field = std::atoi(e);
     if (const char* e = std::getenv("SW_INTER_VARIANT"))

@@ -971,7 +971,8 @@ struct X2pSmem {
 // One workgroup's work (wgi = its index in the launch's numbering):
 // workgroups [0, Q) run the Q blocks [blk_base, quad_end) by quads (GMAX = 4
 // only), the next ones blocks [quad_end, npair) by pairs (two per
-// workgroup), and with MERGED the rest blocks [npair, nblocks) one per wave
+// workgroup), and with MERGED the rest blocks [npair, blk_tail) one per wave
+// and the narrowest, [blk_tail, nblocks), by pairs again
 // (x2s_block): the dispatcher hands out work widest-first across the forms.
 // Returns (per wave) whether this wave appended a block to the rescue list.
 template <int R, int SG, bool AFFINE, bool F16, bool MERGED, int GMAX>
@@ -989,21 +990,27 @@ __device__ __forceinline__ bool x2p_wg(const InterArgs& a, int wgi, int quad_end
     const int qend = GMAX == 4 ? quad_end : a.blk_base;   // blocks [blk_base, qend) by quads
     const int qwg = qend - a.blk_base;                     // quad workgroups
     const int pwg = qwg + (npair - qend + 1) / 2;          // ... and pair workgroups
-    if (MERGED && wgi >= pwg) {
+    // MERGED: blocks [npair, tail) one per wave, then the narrowest blocks
+    // [tail, nblocks) by pairs again (the launch's last-dispatched work)
+    const int tail = MERGED && a.blk_tail > npair && a.blk_tail < a.nblocks ? a.blk_tail : a.nblocks;
+    const int twg = pwg + (tail - npair + kWavesPerWG - 1) / kWavesPerWG;  // first tail-pair workgroup
+    const bool tailp = MERGED && wgi >= twg;               // workgroup-uniform
+    if (MERGED && wgi >= pwg && !tailp) {
         const int blk = npair + (wgi - pwg) * kWavesPerWG + wave;
         // workgroup-uniform branch: no barrier below is skipped by part of it
-        return blk < a.nblocks && x2s_block<R, SG, AFFINE, F16, kSingleCR>(a, blk, lds[wave], lane);
+        return blk < tail && x2s_block<R, SG, AFFINE, F16, kSingleCR>(a, blk, lds[wave], lane);
     }
-    const bool quad = wgi < qwg;                           // workgroup-uniform
+    const bool quad = !tailp && wgi < qwg;                 // workgroup-uniform
     const int G = quad ? 4 : 2, NG = kWavesPerWG / G;
-    const int first = quad ? a.blk_base + wgi : qend + (wgi - qwg) * 2;
+    const int first = quad ? a.blk_base + wgi : tailp ? tail + (wgi - twg) * 2 : qend + (wgi - qwg) * 2;
+    const int gend = tailp ? a.nblocks : npair;            // this workgroup's range end
     const int gi = wave / G, w = wave % G;
     const int passes = (a.qpad + 2 * R - 1) / (2 * R);
     // the workgroup's clock runs to the longest of its blocks
     int tmax = 0;  // (the tick form only)
     for (int q = 0; q < NG; ++q) {
         const int b = first + q;
-        if (b < npair) tmax = max(tmax, group_ticks(block_cols(a, b), passes, SG, G));
+        if (b < gend) tmax = max(tmax, group_ticks(block_cols(a, b), passes, SG, G));
     }
     const int blk = first + gi;
     Best<F16> best;
@@ -1015,7 +1022,7 @@ __device__ __forceinline__ bool x2p_wg(const InterArgs& a, int wgi, int quad_end
         if (threadIdx.x < kWavesPerWG) sm.prog[threadIdx.x] = 0;
         __syncthreads();
     }
-    if (blk < npair) {
+    if (blk < gend) {
         const uint32_t ncols = block_cols(a, blk);
         const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
         const int per = max(static_cast<int>(ncols) / SG + 1, G * kPairLag);
@@ -1048,10 +1055,10 @@ __device__ __forceinline__ bool x2p_wg(const InterArgs& a, int wgi, int quad_end
             ++tick;
         }
     }
-    if (blk < npair && w > 0) part[wave][lane] = P::bits(best.value(a));
+    if (blk < gend && w > 0) part[wave][lane] = P::bits(best.value(a));
     __syncthreads();
     bool flagged = false;
-    if (blk < npair && w == 0) {
+    if (blk < gend && w == 0) {
         V b = best.value(a);
         for (int u = 1; u < G; ++u) {
             const V o = P::from(part[wave + u][lane]);
@@ -1174,10 +1181,36 @@ __device__ __forceinline__ void lpt_drain(const DrainArgs* __restrict__ d, char*
     }
 }
 
-template <int R, int SG, bool AFFINE, int RI>
-__global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(InterArgs a, IntraArgs ia,
-                                                                     const int32_t* __restrict__ order,
-                                                                     const DrainArgs* __restrict__ drain) {
+// The launch's arguments as ONE kernel argument, so that the entry loop
+// below can re-read them through an opaque kernarg pointer per entry: read
+// as plain kernel arguments, the compiler hoists their loads out of the
+// loop and keeps them live across every scan form (169-202 SGPRs of spills).
+struct LptParams {
+    InterArgs a;
+    IntraArgs ia;
+    const int32_t* order;
+    const DrainArgs* drain;
+    int32_t* next;
+    int32_t n;
+    int32_t grid;  // the launch's workgroups
+};
+
+// LOOP = false: one entry per workgroup (entry blockIdx.x), as many
+// workgroups as entries.  LOOP = true (a table of many rounds of workgroups):
+// one workgroup per resident slot, each taking its next entry from the
+// counter `next` once it has finished one — the dispatcher's gaps between
+// a workgroup's end and the next one's start on a CU (median 27 us in
+// C2's launch, 2 % of its slots idle, profiles/r05_trace/) go away.  The
+// loop costs registers: the loop-invariant parts of every scan form (lane
+// and LDS addresses) are hoisted out of it and live across all forms
+// (+20 VGPRs; under affine gaps 124-156 bytes per lane of spills, outside
+// the inner loops), which a launch of few rounds does not win back: C2
+// +1.7 % looping against -1.2 % for the looped code run one entry per
+// workgroup; the 1/8 share (1.7 rounds) -0.6 % (profiles/r05_ab/lpt_loop/).
+// (A noinline entry function instead of the inlined forms faulted on the
+// GPU; not pursued.)
+template <int R, int SG, bool AFFINE, int RI, bool LOOP>
+__global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(LptParams prm) {
     using Elem = typename ix2::IntraImg<RI, true>::Elem;
     using PElem = typename ix2::IntraImg<2, true>::Elem;
     constexpr size_t kInter = sizeof(X2pSmem<R, SG, 4>);
@@ -1187,48 +1220,95 @@ __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(InterArgs a
     constexpr size_t kSmem = std::max(std::max(std::max(kInter, kIntra), kDrain), kPipe);
     __shared__ __attribute__((aligned(16))) char smem[kSmem];
     __shared__ int task[2 + 2 * kWavesPerWG];
-    const int item = order[blockIdx.x];
-    const uint64_t t0 = trace_now();
-    // intra items: -1 - g; g < the launch's intra workgroups (RI rows per
-    // lane, 4 pairs) or, past them, one of the longest pairs in the
-    // pipelined form (2 rows per lane, a chunk per wave)
-    const int niwg = ((ia.nsubj + 1) / 2 + kWavesPerWG - 1) / kWavesPerWG;
-    bool flagged;
-    if (item >= 0)
-        flagged = x2p_wg<R, SG, AFFINE, true, true, 4>(a, item, a.blk_quad, *reinterpret_cast<X2pSmem<R, SG, 4>*>(smem));
-    else if (-1 - item < niwg)
-        flagged = ix2::intra_x2_wg<RI, true, false, !AFFINE, true, false, kLptConv && AFFINE>(ia, -1 - item,
-                                                                                 reinterpret_cast<Elem*>(smem));
-    else
-        flagged = ix2::intra_x2_wg<2, true, false, !AFFINE, true, true, kLptConv && AFFINE>(ia, -1 - item - niwg,
-                                                                                 reinterpret_cast<PElem*>(smem));
-    // Only a workgroup that appended an entry drains (and takes whatever is
-    // listed, its own entries included): every entry is then taken by its
-    // producer at the latest, and the rest of the grid pays one barrier.
-    const bool any = __syncthreads_or(flagged);
-    // per-workgroup timeline (trace builds), after the per-block entries:
-    // every wave of the workgroup is done here
-    if (threadIdx.x == 0) trace_block(a, a.nblocks + blockIdx.x, t0, 0, item >= 0 ? 2 : 3);
-    if (drain && any) lpt_drain<AFFINE, RI>(drain, smem, task);
+    __shared__ int claimed;
+    // Entry k of the table: this workgroup's own index first; then (LOOP)
+    // the entry after the grid's that the counter hands out, until the
+    // table is exhausted.  Every wave leaves the loop on the same k (LDS).
+    if (static_cast<int>(blockIdx.x) >= prm.n) return;
+    for (int k = blockIdx.x;;) {
+        auto kp = __builtin_amdgcn_kernarg_segment_ptr();
+        if constexpr (LOOP) asm volatile("" : "+s"(kp));  // opaque: the arguments are loaded per entry
+        const LptParams& p = *(const LptParams*)(kp);     // (C cast: the address-space cast)
+        const InterArgs& a = p.a;
+        const IntraArgs& ia = p.ia;
+        // intra items: -1 - g; g < the launch's intra workgroups (RI rows per
+        // lane, 4 pairs) or, past them, one of the longest pairs in the
+        // pipelined form (2 rows per lane, a chunk per wave)
+        const int niwg = ((ia.nsubj + 1) / 2 + kWavesPerWG - 1) / kWavesPerWG;
+        const int item = p.order[k];
+        const uint64_t t0 = trace_now();
+        bool flagged;
+        if (item >= 0)
+            flagged = x2p_wg<R, SG, AFFINE, true, true, 4>(a, item, a.blk_quad,
+                                                           *reinterpret_cast<X2pSmem<R, SG, 4>*>(smem));
+        else if (-1 - item < niwg)
+            flagged = ix2::intra_x2_wg<RI, true, false, !AFFINE, true, false, kLptConv && AFFINE>(
+                ia, -1 - item, reinterpret_cast<Elem*>(smem));
+        else
+            flagged = ix2::intra_x2_wg<2, true, false, !AFFINE, true, true, kLptConv && AFFINE>(
+                ia, -1 - item - niwg, reinterpret_cast<PElem*>(smem));
+        // Only a workgroup that appended an entry drains (and takes whatever is
+        // listed, its own entries included): every entry is then taken by its
+        // producer at the latest, and the rest of the grid pays one barrier.
+        const bool any = __syncthreads_or(flagged);
+        // per-entry timeline (trace builds), after the per-block entries:
+        // every wave of the workgroup is done here
+        if (threadIdx.x == 0) trace_block(a, a.nblocks + k, t0, 0, item >= 0 ? 2 : 3);
+        if (p.drain && any) lpt_drain<AFFINE, RI>(p.drain, smem, task);
+        if constexpr (!LOOP) break;
+        if (threadIdx.x == 0) claimed = p.grid + __hip_atomic_fetch_add(p.next, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();  // (also: every wave is done with the LDS of this entry)
+        k = claimed;
+        __syncthreads();  // claimed is read before the next entry's thread 0 rewrites it
+        if (k >= p.n) break;
+    }
 }
 
-template <int RI>
-static void launch_lpt_t(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine,
-                         hipStream_t s, const DrainArgs* drain) {
-    if (affine) hipLaunchKernelGGL((sw_scan_lpt<32, 8, true, RI>), dim3(n), dim3(kWavesPerWG * kLanes), 0, s, a, ia,
-                                   order, drain);
-    else hipLaunchKernelGGL((sw_scan_lpt<32, 8, false, RI>), dim3(n), dim3(kWavesPerWG * kLanes), 0, s, a, ia, order,
-                            drain);
+// Resident workgroups of sw_scan_lpt<...> on the device (the looped grid):
+// occupancy x CUs, once per instantiation.
+template <int RI, bool AFFINE>
+static int lpt_slots() {
+    static const int slots = [] {
+        int dev = 0, cus = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sw_scan_lpt<32, 8, AFFINE, RI, true>,
+                                                         kWavesPerWG * kLanes, 0) != hipSuccess)
+            return 0;
+        return cus * per;
+    }();
+    return slots;
+}
+
+// The looped form from this many rounds of resident workgroups on.
+constexpr int kLptLoopRounds = 3;
+
+template <int RI, bool AFFINE>
+static void launch_lpt_t(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, hipStream_t s,
+                         const DrainArgs* drain, int32_t* next, int loop_grid) {
+    int slots = next ? lpt_slots<RI, AFFINE>() : 0;
+    const dim3 block(kWavesPerWG * kLanes);
+    if (next && loop_grid > 0) slots = std::min(loop_grid, n);  // forced (tests)
+    if (slots > 0 && (n >= kLptLoopRounds * slots || (next && loop_grid > 0))) {
+        const LptParams p{a, ia, order, drain, next, n, slots};
+        hipLaunchKernelGGL((sw_scan_lpt<32, 8, AFFINE, RI, true>), dim3(slots), block, 0, s, p);
+    } else {
+        const LptParams p{a, ia, order, drain, nullptr, n, n};
+        hipLaunchKernelGGL((sw_scan_lpt<32, 8, AFFINE, RI, false>), dim3(n), block, 0, s, p);
+    }
 }
 
 bool lpt_supported(int ri) { return ri == 4 || ri == 6 || ri == 8; }
 
 hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri,
-                           hipStream_t s, const DrainArgs* drain) {
+                           hipStream_t s, const DrainArgs* drain, int32_t* next, int loop_grid) {
     if (n <= 0) return hipSuccess;
-    if (ri == 4) launch_lpt_t<4>(a, ia, order, n, affine, s, drain);
-    else if (ri == 6) launch_lpt_t<6>(a, ia, order, n, affine, s, drain);
-    else if (ri == 8) launch_lpt_t<8>(a, ia, order, n, affine, s, drain);
+    if (ri == 4) affine ? launch_lpt_t<4, true>(a, ia, order, n, s, drain, next, loop_grid)
+                        : launch_lpt_t<4, false>(a, ia, order, n, s, drain, next, loop_grid);
+    else if (ri == 6) affine ? launch_lpt_t<6, true>(a, ia, order, n, s, drain, next, loop_grid)
+                             : launch_lpt_t<6, false>(a, ia, order, n, s, drain, next, loop_grid);
+    else if (ri == 8) affine ? launch_lpt_t<8, true>(a, ia, order, n, s, drain, next, loop_grid)
+                             : launch_lpt_t<8, false>(a, ia, order, n, s, drain, next, loop_grid);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }

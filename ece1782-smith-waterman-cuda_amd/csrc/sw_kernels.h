@@ -116,6 +116,9 @@ struct InterArgs {
     int32_t blk_base;
     // sw_scan_lpt: blocks [blk_base, blk_quad) run by wave quads
     int32_t blk_quad;
+    // sw_scan_lpt: blocks [blk_tail, nblocks) (the narrowest) run by wave
+    // pairs after the single-wave range (0 or nblocks: none)
+    int32_t blk_tail;
     // fp16 kernels: the largest flagged block id (atomicMax; nullable), read
     // back by the host to route the widest blocks to int16 next time
     int32_t* rescue_max;
@@ -295,8 +298,14 @@ struct DrainArgs {
     int32_t* fault;     // host-mapped word: a claimed entry never appeared (list_wait_take)
 };
 bool lpt_supported(int ri);
+// next (nullable; zero at launch): with it, a table of at least 3 rounds of
+// resident workgroups runs one workgroup per resident slot, each taking its
+// next entry of order[] from this counter when it has finished one (the
+// dispatcher's per-workgroup gaps avoided); otherwise one workgroup per
+// entry.  loop_grid > 0 (tests): that form with that many workgroups.
 hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri,
-                           hipStream_t s, const DrainArgs* drain = nullptr);
+                           hipStream_t s, const DrainArgs* drain = nullptr, int32_t* next = nullptr,
+                           int loop_grid = 0);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.
 constexpr int kSat16 = 32767 - 1152;
 // The two-subjects intra kernel's widest shape: 20 rows per lane, in the
@@ -397,7 +406,7 @@ struct ProfileArgs {
     int32_t row0, row1;
     int32_t bias;
     int32_t ri, rip, qpad_intra;
-    int32_t* reset[9];
+    int32_t* reset[10];
     int8_t mat[kAlphabet * kAlphabet + 15];
     uint8_t q[kProfQueryChunk];
 };

@@ -17,7 +17,8 @@ namespace swk {
 
 // One thread per (code, row) entry of rows [row0, row1).
 __global__ __launch_bounds__(256) void sw_build_profile(ProfileArgs a) {
-    if (blockIdx.x == 0 && threadIdx.x < 9) {  // the rescue lists' counters and heads (first launch only)
+    if (blockIdx.x == 0 && threadIdx.x < 10) {  // the rescue lists' counters and heads, the merged
+                                                // launch's work counter (first launch only)
         int32_t* p = a.reset[threadIdx.x];
         if (p) *p = threadIdx.x == 2 ? -1 : 0;
     }

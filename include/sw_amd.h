@@ -172,6 +172,13 @@ typedef struct sw_opts {
     int32_t int16_guard;      /* 0: int32 beyond the static int16 bound        SW_INT16_GUARD */
     int32_t rescue_stats;     /* 1: print what the guard bands flagged per scan
                                  (synchronises)                                SW_RESCUE_STATS */
+    int32_t tail_pairs;       /* the narrowest n blocks of the merged launch run
+                                 by wave pairs (0: none)                       SW_TAIL_PAIRS */
+    int32_t lpt_persist;      /* 0: the merged launch with one workgroup per work
+                                 item, never one per resident slot taking items
+                                 from a counter (default: that form for tables
+                                 of 3+ rounds); n >= 2: that form with n
+                                 workgroups (tests)                           SW_LPT_PERSIST */
     char inter_variant[16];   /* inter kernel shape: "" (auto), "32x8", "64x8"
                                  (int32), "y32x8" (int16 two-strips), "f32x8",
                                  "f32x4" (its fp16 form)                       SW_INTER_VARIANT */
