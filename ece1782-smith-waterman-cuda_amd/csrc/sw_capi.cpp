@@ -229,7 +229,7 @@ sw_opts default_opts() {
     o.size = static_cast<int32_t>(sizeof o);
     for (int32_t* f : {&o.lpt, &o.lpt_pipe, &o.quad_width, &o.pair_width, &o.pair_group, &o.coop_width,
                        &o.coop_skew, &o.intra_x2, &o.intra_x2_rows, &o.intra_i16_first, &o.inter_i16_span,
-                       &o.int16_guard, &o.rescue_stats, &o.tail_pairs, &o.lpt_persist})
+                       &o.int16_guard, &o.rescue_stats, &o.tail_pairs, &o.lpt_persist, &o.lpt_rows})
         *f = -1;
     return o;
 }
@@ -400,7 +400,7 @@ struct sw_db {
     std::vector<int32_t> h_llen;         // long subjects' lengths, longest first
     // sw_scan_lpt work tables (longest first), per scan shape
     struct LptTable {
-        int32_t qpad, qpad_intra, ri, npair, group /* quad blocks */, tail /* tail-pair blocks */, n;
+        int32_t qpad, rows /* per pass */, qpad_intra, ri, npair, group /* quad blocks */, tail /* tail-pair blocks */, n;
         bool affine;
         int32_t npipe;  // the longest pairs, in the pipelined form
         int32_t pipe_opt;  // sw_opts lpt_pipe the table was built under
@@ -1097,17 +1097,18 @@ double group_ticks_host(int64_t ncols, int passes, int G) {
 }
 
 // The work table of sw_scan_lpt for this scan shape (built once, cached).
-int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad, int32_t ntail,
-              bool affine, const int32_t** order, int* n, int32_t* npipe_out) {
+int lpt_table(sw_db* db, int32_t qpad, int rows, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad,
+              int32_t ntail, bool affine, const int32_t** order, int* n, int32_t* npipe_out) {
     for (const auto& t : db->lpt_tables)
-        if (t.qpad == qpad && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad &&
+        if (t.qpad == qpad && t.rows == rows && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad &&
             t.tail == ntail && t.pipe_opt == db->h->opts.lpt_pipe && t.affine == affine) {
             *order = t.d_order;
             *n = t.n;
             *npipe_out = t.npipe;
             return SW_OK;
         }
-    const int passes = qpad / 64;
+    const int passes = qpad / rows;
+    const double tick_us = kTickUs * rows / 64;  // a tick: 8 columns of one pass
     const int64_t nb = db->nblocks;
     const int64_t pwg = nquad + (npair - nquad + 1) / 2;
     const int64_t tail = nb - ntail;  // blocks [tail, nb) by pairs
@@ -1120,20 +1121,20 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
     std::vector<std::pair<double, int32_t>> w;
     w.reserve(static_cast<size_t>(pwg + swg + twg + iwg));
     auto width = [&](int64_t b) { return static_cast<int64_t>(db->h_blk_groups[b]) * swk::kGroupCols; };
-    for (int64_t g = 0; g < nquad; ++g) w.emplace_back(group_ticks_host(width(g), passes, 4) * kTickUs, g);
+    for (int64_t g = 0; g < nquad; ++g) w.emplace_back(group_ticks_host(width(g), passes, 4) * tick_us, g);
     for (int64_t g = nquad; g < pwg; ++g) {
         double c = 0;
         for (int q = 0; q < 2; ++q) {
             const int64_t b = nquad + (g - nquad) * 2 + q;
             if (b < npair) c = std::max(c, group_ticks_host(width(b), passes, 2));
         }
-        w.emplace_back(c * kTickUs, static_cast<int32_t>(g));
+        w.emplace_back(c * tick_us, static_cast<int32_t>(g));
     }
     for (int64_t g = 0; g < swg; ++g)  // widest first: the workgroup's first block bounds it
-        w.emplace_back(single_ticks(width(npair + g * swk::kWavesPerWG), passes) * kTickUs,
+        w.emplace_back(single_ticks(width(npair + g * swk::kWavesPerWG), passes) * tick_us,
                        static_cast<int32_t>(pwg + g));
     for (int64_t g = 0; g < twg; ++g) {  // tail pairs: the first block of two is the wider
-        w.emplace_back(group_ticks_host(width(tail + 2 * g), passes, 2) * kTickUs,
+        w.emplace_back(group_ticks_host(width(tail + 2 * g), passes, 2) * tick_us,
                        static_cast<int32_t>(pwg + swg + g));
     }
     // The longest pairs whose one-wave latency would exceed every inter
@@ -1173,7 +1174,7 @@ int lpt_table(sw_db* db, int32_t qpad, int32_t qpad_intra, int ri, int32_t npair
         ord[k] = w[k].second;
         cost[k] = static_cast<float>(w[k].first);
     }
-    sw_db::LptTable t{qpad, qpad_intra, ri, npair, nquad, ntail, static_cast<int32_t>(ord.size()), affine,
+    sw_db::LptTable t{qpad, rows, qpad_intra, ri, npair, nquad, ntail, static_cast<int32_t>(ord.size()), affine,
                       static_cast<int32_t>(npipe), db->h->opts.lpt_pipe, nullptr, cost};
     HIPCHECK(hipMalloc(reinterpret_cast<void**>(&t.d_order), ord.size() * sizeof(int32_t)));
     HIPCHECK(hipMemcpy(t.d_order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -1353,7 +1354,7 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
                                                                                : 0;
     const swk::InterShape shape = swk::inter_shape(affine, x2_ok, h->opts);
     const int R = shape.R;
-    const int32_t qpad_inter = static_cast<int32_t>(round_up(qlen, R));
+    int32_t qpad_inter = static_cast<int32_t>(round_up(qlen, R));  // (the merged linear launch: see lpt_rows)
     // (the merged launch's drain takes the int32 rows per lane from ri2, below)
     int ri = db->nlong ? swk::intra_rows_for(qlen, db->long_max) : 0;
     int32_t qpad_intra = ri ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri)) : 0;
@@ -1509,6 +1510,14 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
         ri = ri2;
         qpad_intra = static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri));
     }
+    // The merged launch under linear gaps runs 96-row passes (48-row strips):
+    // its widest blocks' wave groups need fewer rounds (a 375-aa query: 4
+    // passes, one round of a quad, against 6 passes and two rounds of 64
+    // rows), and the share's span is those blocks' latency;
+    // the linear cell's registers leave room for the taller strips.  Affine
+    // scans keep 64 rows (their E column would not fit).  sw_opts lpt_rows.
+    const int lpt_rows = (lpt && !affine && O.lpt_rows != 64 && round_up(qlen, 96) > 96) ? 96 : 64;
+    if (lpt_rows == 96) qpad_inter = static_cast<int32_t>(round_up(qlen, 96));
     const int32_t qpad_coop = ncoop ? static_cast<int32_t>(round_up(qlen, swk::inter_coop_rows())) : 0;
     // lists A and B, the largest flagged block, a spare word, the dequeue
     // heads of A and B (the merged launch's drain); every entry starts at -1
@@ -1821,10 +1830,11 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
             int nwg = 0;
             const int32_t nquad = lpt_quad_blocks(db, npair);
             a.blk_quad = nquad;
-            ntail = lpt_tail_blocks(db, npair, qpad_inter / 64);
+            ntail = lpt_tail_blocks(db, npair, qpad_inter / lpt_rows);
             a.blk_tail = static_cast<int32_t>(db->nblocks) - ntail;
             int32_t npipe = 0;
-            if ((rc = lpt_table(db, qpad_inter, qpad_intra2, ri2, npair, nquad, ntail, affine, &order, &nwg, &npipe)))
+            if ((rc = lpt_table(db, qpad_inter, lpt_rows, qpad_intra2, ri2, npair, nquad, ntail, affine, &order, &nwg,
+                                &npipe)))
                 return rc;
             lpt_intra.pipe_pairs = npipe;
             const swk::DrainArgs* dargs = nullptr;
@@ -1875,7 +1885,7 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
                 if ((rc = drain_blob(db, h->stream, key, d, &dargs))) return rc;
             }
             HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, order, nwg, affine, ri2, h->stream, dargs, lpt_next,
-                                          O.lpt_persist >= 2 ? O.lpt_persist : 0));
+                                          O.lpt_persist >= 2 ? O.lpt_persist : 0, lpt_rows));
             // (a draining launch ends the scan: its end event is ev[3])
             if (!drain) MARK(7, h->stream);
             if ((rc = launch_long(true))) return rc;
@@ -2183,7 +2193,8 @@ int sw_opts_from_env(sw_opts* o) {
                 {"SW_INT16_GUARD", &o->int16_guard},
                 {"SW_RESCUE_STATS", &o->rescue_stats},
                 {"SW_TAIL_PAIRS", &o->tail_pairs},
-                {"SW_LPT_PERSIST", &o->lpt_persist}};
+                {"SW_LPT_PERSIST", &o->lpt_persist},
+                {"SW_LPT_ROWS", &o->lpt_rows}};
     for (const auto& k : ints)
         if (const char* e = std::getenv(k.name); e && e[0]) *k.field = std::atoi(e);
     if (const char* e = std::getenv("SW_INTER_VARIANT"))

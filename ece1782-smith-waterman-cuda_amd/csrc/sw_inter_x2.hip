@@ -1266,13 +1266,13 @@ __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(LptParams p
 
 // Resident workgroups of sw_scan_lpt<...> on the device (the looped grid):
 // occupancy x CUs, once per instantiation.
-template <int RI, bool AFFINE>
+template <int R, int RI, bool AFFINE>
 static int lpt_slots() {
     static const int slots = [] {
         int dev = 0, cus = 0, per = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sw_scan_lpt<32, 8, AFFINE, RI, true>,
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sw_scan_lpt<R, 8, AFFINE, RI, true>,
                                                          kWavesPerWG * kLanes, 0) != hipSuccess)
             return 0;
         return cus * per;
@@ -1283,33 +1283,36 @@ static int lpt_slots() {
 // The looped form from this many rounds of resident workgroups on.
 constexpr int kLptLoopRounds = 3;
 
-template <int RI, bool AFFINE>
+template <int R, int RI, bool AFFINE>
 static void launch_lpt_t(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, hipStream_t s,
                          const DrainArgs* drain, int32_t* next, int loop_grid) {
-    int slots = next ? lpt_slots<RI, AFFINE>() : 0;
+    int slots = next ? lpt_slots<R, RI, AFFINE>() : 0;
     const dim3 block(kWavesPerWG * kLanes);
     if (next && loop_grid > 0) slots = std::min(loop_grid, n);  // forced (tests)
     if (slots > 0 && (n >= kLptLoopRounds * slots || (next && loop_grid > 0))) {
         const LptParams p{a, ia, order, drain, next, n, slots};
-        hipLaunchKernelGGL((sw_scan_lpt<32, 8, AFFINE, RI, true>), dim3(slots), block, 0, s, p);
+        hipLaunchKernelGGL((sw_scan_lpt<R, 8, AFFINE, RI, true>), dim3(slots), block, 0, s, p);
     } else {
         const LptParams p{a, ia, order, drain, nullptr, n, n};
-        hipLaunchKernelGGL((sw_scan_lpt<32, 8, AFFINE, RI, false>), dim3(n), block, 0, s, p);
+        hipLaunchKernelGGL((sw_scan_lpt<R, 8, AFFINE, RI, false>), dim3(n), block, 0, s, p);
     }
 }
 
 bool lpt_supported(int ri) { return ri == 4 || ri == 6 || ri == 8; }
 
 hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri,
-                           hipStream_t s, const DrainArgs* drain, int32_t* next, int loop_grid) {
+                           hipStream_t s, const DrainArgs* drain, int32_t* next, int loop_grid, int rows) {
     if (n <= 0) return hipSuccess;
-    if (ri == 4) affine ? launch_lpt_t<4, true>(a, ia, order, n, s, drain, next, loop_grid)
-                        : launch_lpt_t<4, false>(a, ia, order, n, s, drain, next, loop_grid);
-    else if (ri == 6) affine ? launch_lpt_t<6, true>(a, ia, order, n, s, drain, next, loop_grid)
-                             : launch_lpt_t<6, false>(a, ia, order, n, s, drain, next, loop_grid);
-    else if (ri == 8) affine ? launch_lpt_t<8, true>(a, ia, order, n, s, drain, next, loop_grid)
-                             : launch_lpt_t<8, false>(a, ia, order, n, s, drain, next, loop_grid);
+    if ((rows != 64 && rows != 96) || (rows == 96 && affine) || a.qpad % rows) return hipErrorInvalidValue;
+#define SW_LPT_RI(RI)                                                                          \
+    (affine ? launch_lpt_t<32, RI, true>(a, ia, order, n, s, drain, next, loop_grid)           \
+     : rows == 96 ? launch_lpt_t<48, RI, false>(a, ia, order, n, s, drain, next, loop_grid)   \
+                  : launch_lpt_t<32, RI, false>(a, ia, order, n, s, drain, next, loop_grid))
+    if (ri == 4) SW_LPT_RI(4);
+    else if (ri == 6) SW_LPT_RI(6);
+    else if (ri == 8) SW_LPT_RI(8);
     else return hipErrorInvalidValue;
+#undef SW_LPT_RI
     return hipGetLastError();
 }
 

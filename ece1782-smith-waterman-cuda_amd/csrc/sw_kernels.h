@@ -303,9 +303,10 @@ bool lpt_supported(int ri);
 // next entry of order[] from this counter when it has finished one (the
 // dispatcher's per-workgroup gaps avoided); otherwise one workgroup per
 // entry.  loop_grid > 0 (tests): that form with that many workgroups.
+// rows: query rows per pass, 64 (32-row strips) or, linear gaps only, 96.
 hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri,
                            hipStream_t s, const DrainArgs* drain = nullptr, int32_t* next = nullptr,
-                           int loop_grid = 0);
+                           int loop_grid = 0, int rows = 64);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.
 constexpr int kSat16 = 32767 - 1152;
 // The two-subjects intra kernel's widest shape: 20 rows per lane, in the

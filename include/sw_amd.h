@@ -179,6 +179,8 @@ typedef struct sw_opts {
                                  from a counter (default: that form for tables
                                  of 3+ rounds); n >= 2: that form with n
                                  workgroups (tests)                           SW_LPT_PERSIST */
+    int32_t lpt_rows;         /* query rows per pass of the merged launch under
+                                 linear gaps: 64 or 96 (default 96)           SW_LPT_ROWS */
     char inter_variant[16];   /* inter kernel shape: "" (auto), "32x8", "64x8"
                                  (int32), "y32x8" (int16 two-strips), "f32x8",
                                  "f32x4" (its fp16 form)                       SW_INTER_VARIANT */
