@@ -1492,10 +1492,12 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
     // whole C2 database it was 2 % slower than two concurrent launches until
     // the launch drained its own rescue lists (no rescue launches or events
     // after it): now 7.19 -> 7.12 ms under affine scoring (C3 and C4's share
-    // unchanged), but under linear gaps 4.57 -> 5.03 ms (profiles/r04_*/):
-    // affine scans of every database and linear scans of small ones take
-    // it.  sw_opts lpt 0 / 1 forces either form.
-    const bool lpt_want = O.lpt >= 0 ? O.lpt == 1 : affine || static_cast<double>(db->n) < 0.35 * kFillSubjects;
+    // unchanged), but under linear gaps 4.57 -> 5.03 ms (profiles/r04_*/);
+    // since round 5's tail pairs, looped grid and 96-row linear passes the
+    // whole C2 database under linear gaps too: 16,512 -> 16,777 GCUPS
+    // (profiles/r05_ab/lpt_linear_c2/).  Every scan of that shape takes it;
+    // sw_opts lpt 0 / 1 forces either form.
+    const bool lpt_want = O.lpt >= 0 ? O.lpt == 1 : true;
     const bool lpt = lpt_want && db->nlong && db->nblocks && intra_x2 && !intra_i16_first &&
                      f16 && rescue && npair && !ncoop && i16_span == 0 &&
                      swk::lpt_supported(ri2);

@@ -131,3 +131,31 @@ def test_looped_grid_drains(sw, oracle, handle, knobs, small_db):
         got = db.scan(q, m, 12 * f, f)
         assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
     db.close()
+
+
+@pytest.mark.parametrize("scoring", SCORINGS)
+def test_c2_size_merged_equals_separate_launches(sw, oracle, handle, knobs, scoring):
+    """C2's whole database (570,000 subjects) under both scorings: the
+    default merged launch (tail pairs, the looped grid; 96-row passes under
+    the linear scoring) equals the separate-launch form on every subject and
+    the oracle on a sample of 3,000 (the oracle is too slow for all)."""
+    mid, go, ge = scoring
+    res, offs = sw.synth.database(570000, shard=0)
+    db = sw.Database(handle, res, offs)
+    q = sw.encode(__import__("conftest").read_query("P07327"))
+    m = sw.capi.builtin_matrix(mid)
+    knobs(lpt="-1")
+    got = db.scan(q, m, go, ge)
+    k = handle.last_kernel()
+    assert "+tail" in k and "+lpt" in k, k
+    knobs(lpt="0")
+    sep = db.scan(q, m, go, ge)
+    assert "+lpt" not in handle.last_kernel()
+    assert np.array_equal(got, sep), np.nonzero(got != sep)[0][:8]
+    pick = np.sort(np.random.default_rng(mid).choice(len(offs) - 1, 3000, replace=False))
+    lens = offs[pick + 1] - offs[pick]
+    sub = np.concatenate([res[offs[i]:offs[i + 1]] for i in pick])
+    so = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    want = oracle.scan(q, sub, so, mat=m, gap_open=go, gap_extend=ge, nthreads=16)
+    assert np.array_equal(got[pick], want)
+    db.close()
