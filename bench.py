@@ -78,6 +78,8 @@ VALU_MODEL = {
     # packed, 0.32 other
     "sw_inter_x2s<32,8,linear,fp16>": (3.86 * 4.25 + 0.305 * 2.7) / 128,
     "sw_inter_x2p<32,8,linear,fp16>": (3.86 * 4.25 + 0.305 * 2.7) / 128,
+    # (the merged launch's 48-row strips under linear gaps: the same cell)
+    "sw_inter_x2p<48,8,linear,fp16>": (3.86 * 4.25 + 0.305 * 2.7) / 128,
     # the same cells with the widest blocks run by wave pairs in the same launch
     "sw_inter_x2p<32,8,affine,fp16>": (5.91 * 4.25 + 0.305 * 2.7) / 128,
     "sw_inter_x2p<32,8,linear>": (5.0 * 4.25 + 0.29 * 2.7) / 128,

@@ -1901,6 +1901,7 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
         }
         h->last_kernel = swk::inter_kernel_name(shape, affine);
         if (npair) h->last_kernel.replace(0, std::strlen("sw_inter_x2s"), "sw_inter_x2p");  // + wave pairs
+        if (lpt && lpt_rows == 96) h->last_kernel.replace(h->last_kernel.find("<32,"), 4, "<48,");  // 48-row strips
         if (nr) h->last_kernel += "+int16[0," + std::to_string(nr) + ")";
         if (ntail) h->last_kernel += "+tail" + std::to_string(ntail);
         if (lpt) h->last_kernel += drain ? "+lpt+drain" : "+lpt";
