@@ -984,8 +984,9 @@ __device__ __forceinline__ bool x2p_wg(const InterArgs& a, int wgi, int quad_end
     auto& part = sm.part;
     using P = PkCell<F16>;
     using V = typename P::V;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
+    const int tid = tid_x();
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
     const int npair = MERGED ? a.blk_first : a.nblocks;  // blocks [blk_base, npair) by groups
     const int qend = GMAX == 4 ? quad_end : a.blk_base;   // blocks [blk_base, qend) by quads
     const int qwg = qend - a.blk_base;                     // quad workgroups
@@ -1019,7 +1020,7 @@ __device__ __forceinline__ bool x2p_wg(const InterArgs& a, int wgi, int quad_end
     const uint64_t t0 = trace_now();
     constexpr bool kPairFlags = pair_flags<AFFINE>();
     if constexpr (kPairFlags) {
-        if (threadIdx.x < kWavesPerWG) sm.prog[threadIdx.x] = 0;
+        if (tid < kWavesPerWG) sm.prog[tid] = 0;
         __syncthreads();
     }
     if (blk < gend) {

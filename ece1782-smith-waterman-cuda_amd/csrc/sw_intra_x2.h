@@ -237,8 +237,9 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
     constexpr int PF = PIPE ? (LIN ? SW_IX2_PIPE_PF_LIN : SW_IX2_PIPE_PF) : 1;
     constexpr int NBUF = PF == 1 ? 2 : 4;
     static_assert(PF >= 1 && PF <= NBUF - 1, "prefetch distance");
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
+    const int tid = tid_x();  // (opaque: sw_kernels.h)
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
     const bool is_last_lane = lane == kLanes - 1;
     const int p = PIPE ? wgi : wgi * kWavesPerWG + wave;  // subject pair
     int sa = 2 * p, sb = 2 * p + 1;
@@ -509,7 +510,7 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
     if constexpr (!PIPE) {
         for (int c0 = 0; c0 < a.qpad; c0 += CH) {
             __syncthreads();  // the previous chunk's LDS reads are done
-            stage(img, c0, static_cast<int>(threadIdx.x), kWavesPerWG * kLanes);
+            stage(img, c0, tid, kWavesPerWG * kLanes);
             __syncthreads();
             if (!hasA && !hasB) continue;  // wave-uniform; the barriers above are shared
             run_chunk(c0, img, c0 == 0, c0 + CH >= a.qpad, [](int nblk, auto& block) {
@@ -530,7 +531,7 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
         Elem* mine = img + wave * (kCodes * NQ * kLanes);
         int* prog = reinterpret_cast<int*>(img + kWavesPerWG * (kCodes * NQ * kLanes));
         if (wave < nch) stage(mine, wave * CH, lane, kLanes);
-        if (threadIdx.x < kWavesPerWG) prog[threadIdx.x] = 0;
+        if (tid < kWavesPerWG) prog[tid] = 0;
         __syncthreads();
         if (wave < nch) {
             run_chunk(wave * CH, mine, wave == 0, wave == nch - 1, [&](int nb, auto& block) {

@@ -170,6 +170,16 @@ struct IntraArgs {
 // producer (sw_scan_lpt's drain) can wait for an entry whose slot a
 // producer has claimed but not yet written.
 #if defined(__HIPCC__)
+// threadIdx.x made opaque at each read: the merged launch's looped form runs
+// every scan form inside one loop, and the compiler hoists what the forms
+// derive from the thread index (lane and LDS addresses) out of it, holding
+// all of them live across every form at once (sw_inter_x2.hip sw_scan_lpt).
+// Read through this, each form derives them anew per entry.
+__device__ __forceinline__ int tid_x() {
+    int t = static_cast<int>(threadIdx.x);
+    asm volatile("" : "+v"(t));
+    return t;
+}
 // Producer: this wave's results (its scores, its boundary rows) are made
 // visible device-wide before the entry, so a re-scoring stage on another XCD
 // overwrites them, not the reverse.
