@@ -1165,7 +1165,7 @@ __device__ __forceinline__ void lpt_drain(const DrainArgs* __restrict__ d, char*
             IntraArgs y = d->i16;
             y.subj_list = task + 2;
             y.list_count = task + 1;
-            ix2::intra_x2_wg<RI, false, true, !AFFINE, false>(y, 0,
+            ix2::intra_x2_wg<RI, false, true, !AFFINE, false, false, false, true>(y, 0,
                                                                reinterpret_cast<typename ix2::IntraImg<RI, false>::Elem*>(smem));
         } else if (kind == 1) {  // list A: int16 blocks, flagging into list B
             if (wave < n)
@@ -1243,10 +1243,10 @@ __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(LptParams p
             flagged = x2p_wg<R, SG, AFFINE, true, true, 4>(a, item, a.blk_quad,
                                                            *reinterpret_cast<X2pSmem<R, SG, 4>*>(smem));
         else if (-1 - item < niwg)
-            flagged = ix2::intra_x2_wg<RI, true, false, !AFFINE, true, false, kLptConv && AFFINE>(
+            flagged = ix2::intra_x2_wg<RI, true, false, !AFFINE, true, false, kLptConv && AFFINE, true>(
                 ia, -1 - item, reinterpret_cast<Elem*>(smem));
         else
-            flagged = ix2::intra_x2_wg<2, true, false, !AFFINE, true, true, kLptConv && AFFINE>(
+            flagged = ix2::intra_x2_wg<2, true, false, !AFFINE, true, true, kLptConv && AFFINE, true>(
                 ia, -1 - item - niwg, reinterpret_cast<PElem*>(smem));
         // Only a workgroup that appended an entry drains (and takes whatever is
         // listed, its own entries included): every entry is then taken by its

@@ -217,7 +217,7 @@ __device__ __forceinline__ uint32_t* conv_area() {
 }
 
 template <int RI, bool F16, bool LIST, bool LIN = false, bool TAKE = true, bool PIPE = false,
-          bool CONV = false>
+          bool CONV = false, bool OPQ = false>
 __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typename IntraImg<RI, F16>::Elem* img) {
     static_assert(!(PIPE && LIST), "the pipelined form takes its pair by index");
     static_assert(!CONV || kPrefetch, "the LDS conveyor serves the prefetching step");
@@ -237,7 +237,10 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
     constexpr int PF = PIPE ? (LIN ? SW_IX2_PIPE_PF_LIN : SW_IX2_PIPE_PF) : 1;
     constexpr int NBUF = PF == 1 ? 2 : 4;
     static_assert(PF >= 1 && PF <= NBUF - 1, "prefetch distance");
-    const int tid = tid_x();  // (opaque: sw_kernels.h)
+    // OPQ (the merged launch's looped form): the thread index read opaquely
+    // (sw_kernels.h tid_x); the stand-alone kernel reads it plainly (C5: the
+    // opaque read cost 0.3 VALU per wave-step)
+    const int tid = OPQ ? tid_x() : static_cast<int>(threadIdx.x);
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63;
     const bool is_last_lane = lane == kLanes - 1;
