@@ -1367,8 +1367,14 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
     // inter blocks; where the fp16 bias of row 19 fits, as f16_fits; and by
     // the cost model for affine gaps only, see intra_x2_rows_for)
     const bool ri2_wide = db->nblocks == 0 && 2 * max_s + (swk::intra_bias_rows(swk::kIntraX2MaxRI) + 1) * ge + go < 1024;
-    const int ri2 =
+    int ri2 =
         intra_x2 ? swk::intra_x2_rows_for(qlen, db->long_max, ri2_wide ? (affine ? 2 : 1) : 0, O.intra_x2_rows) : 0;
+    // Affine scans with inter blocks take the merged launch (intra rows 4, 6
+    // or 8 only) even where the cost model prefers more rows per lane for the
+    // long subjects alone: its tail pairs and looped grid win more (C3's long
+    // queries at 8 rows: +1.3 %; under linear gaps the wider form stays,
+    // -6.9 % at 8 rows: profiles/r05_ab/c3_ri8/)
+    if (affine && ri2 > 8 && db->nblocks && O.intra_x2_rows < 0) ri2 = 8;
     // The intra chain's order.  Linear scoring with cheap gaps makes random
     // pairs' scores grow with their lengths, so on long subjects the fp16
     // pass can flag many of them and its time on those is wasted.  Once a
