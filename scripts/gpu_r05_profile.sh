@@ -21,7 +21,6 @@ import csv,sys
 rows=list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r:-float(r['TotalDurationNs']))
 print(rows[0]['Name'].split('(')[0].replace('void swk::',''))" $(find $O/kt_$c -name "*kernel_stats.csv"))
-  [ $NS -gt 0 ] && KN="sw_inter_x2"
   LABEL=$(python3 -c "
 import json,sys
 d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1])
@@ -30,6 +29,9 @@ print(d['roofline']['kernel'])" $O/kt_$c.json)
 import json,sys
 d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1])
 print(d['roofline']['workload_key'])" $O/kt_$c.json)
+  # (a batch: every scan's dominant kernel summed, the merged launches when
+  # the batch's label says so, else the inter kernels)
+  [ $NS -gt 0 ] && { case "$LABEL" in *+lpt*) KN="sw_scan_lpt" ;; *) KN="sw_inter_x2" ;; esac; }
   echo "$c: rocprof '$KN' label '$LABEL' key '$KEY'"
   timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d $O/fetch_$c -o run --output-format csv -- python3 $B $a $s > $O/fetch_$c.json 2> $O/fetch_$c.err && \
   timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d $O/write_$c -o run --output-format csv -- python3 $B $a $s > $O/write_$c.json 2> $O/write_$c.err && \
