@@ -1033,10 +1033,6 @@ double intra_step_us(int ri) { return 2 * 0.157 * (ri * 28.8 + 80.0) / (6 * 28.8
 #ifndef SW_LPT_LIN_INTRA
 #define SW_LPT_LIN_INTRA 100
 #endif
-// (the same for affine scans: A/B builds only)
-#ifndef SW_LPT_AFF_INTRA
-#define SW_LPT_AFF_INTRA 100
-#endif
 
 // The widest group blocks of the merged launch run by quads: those at least
 // kQuadFrac x the long threshold wide, whose pair latency would otherwise
@@ -1121,7 +1117,7 @@ int lpt_table(sw_db* db, int32_t qpad, int rows, int32_t qpad_intra, int ri, int
     const int64_t npairs = (db->nlong + 1) / 2;
     const int64_t iwg = (npairs + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
     const int nch = qpad_intra / (swk::kLanes * ri);
-    const double step_us = intra_step_us(ri) * (affine ? SW_LPT_AFF_INTRA : SW_LPT_LIN_INTRA) / 100.0;
+    const double step_us = intra_step_us(ri) * (affine ? 1.0 : SW_LPT_LIN_INTRA / 100.0);
     std::vector<std::pair<double, int32_t>> w;
     w.reserve(static_cast<size_t>(pwg + swg + twg + iwg));
     auto width = [&](int64_t b) { return static_cast<int64_t>(db->h_blk_groups[b]) * swk::kGroupCols; };
