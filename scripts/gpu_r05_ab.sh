@@ -13,7 +13,7 @@ for rep in $(seq 1 ${REPS:-2}); do
     lib=ece1782-smith-waterman-cuda_amd/lib/libswamd.so
     [ "$libd" != "-" ] && lib=ece1782-smith-waterman-cuda_amd/$libd/libswamd.so
     for c in ${CFGS:-s8}; do
-      case $c in s8) args="--shard-of 8" ;; s4) args="--shard-of 4" ;; c2) args="" ;; c5) args="--config c5" ;; c3) args="--config c3" ;; esac
+      case $c in s8) args="--shard-of 8" ;; s4) args="--shard-of 4" ;; s2) args="--shard-of 2" ;; c2) args="" ;; c5) args="--config c5" ;; c3) args="--config c3" ;; *) echo "unknown config $c"; exit 1 ;; esac
       env SW_AMD_LIB=$lib ${envs//,/ } timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-verify --sustained-seconds 0 $args ${BARGS} > $O/${c}_${name}_$rep.json 2> $O/${c}_${name}_$rep.err || { echo "$c $name FAILED"; tail -20 $O/${c}_${name}_$rep.err; exit 1; }
       python3 -c "
 import json
