@@ -1062,9 +1062,12 @@ int32_t lpt_quad_blocks(const sw_db* db, int32_t npair) {
 // latency for a few % more wave time on them.  Default: half a round of
 // pair workgroups (2 blocks each; 2 workgroups per CU: as many blocks as
 // workgroup slots) when the single-wave workgroups fill the GPU more than
-// twice over; sw_opts tail_pairs n: the narrowest n blocks.  C2 (256 CUs)
-// over 128-3,072 blocks: 512 best, +1.5 % (1,024 +0.8 %, 3,072 -0.4 %;
-// profiles/r05_ab/tail_pairs/).
+// twice over, a quarter of that for more single-wave blocks than slots;
+// sw_opts tail_pairs n: the narrowest n blocks.  C2 (256 CUs) over
+// 128-3,072 blocks: 512 best, +1.5 % (1,024 +0.8 %, 3,072 -0.4 %); its 1/4
+// share with 128: +0.6 % affine, +0.9 % linear, its 1/2 share +2.4 %
+// linear; the 1/8 share (432 single-wave blocks: none) -0.6 % with 128
+// (profiles/r05_ab/tail_pairs/).
 int32_t lpt_tail_blocks(const sw_db* db, int32_t npair, int passes) {
     const int64_t singles = db->nblocks - npair;
     if (passes < 2 || singles < 2) return 0;
@@ -1076,6 +1079,7 @@ int32_t lpt_tail_blocks(const sw_db* db, int32_t npair, int passes) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, db->h->device) != hipSuccess) cus = 0;
         const int64_t slots = 2 * static_cast<int64_t>(cus);  // workgroups per CU: 2
         if (slots > 0 && singles > 2 * swk::kWavesPerWG * slots) n = slots;
+        else if (slots > 0 && singles > slots) n = slots / 4;  // (C2's 1/2 and 1/4 shares)
     }
     return static_cast<int32_t>(std::min<int64_t>(n, singles - 1));
 }
