@@ -168,18 +168,75 @@ def host_cores():
     return eff, aff, quota
 
 
-def valu_roofline(kernel, cells_rank, scan_ms, kernel_gcups):
-    """The binding roofline: VALU instruction issue.  peak = the modeled
-    issue-bound rate of the per-wave inter kernel (VALU_MODEL), achieved =
-    the whole scan's rate (all kernels of the scan, concurrent)."""
-    cpc = VALU_MODEL.get(kernel.split("+")[0])  # "+int16[0,n)": the widest blocks in int16 beside it
-    if cpc is None or scan_ms <= 0:
+# The algorithm's VALU floor: packed 16-bit ops per cell PAIR
+# (two cells per instruction) of the biased cell, without the maxima, the
+# rebase or any addressing — affine (Gotoh): v_pk_fma (H_diag + S),
+# v_pk_maximum3 (H), v_pk_add (H - open), v_pk_maximum (E), v_pk_maximum3
+# (F with the floor); linear: v_pk_fma, v_pk_maximum3, v_pk_maximum (floor).
+# Each packed op issues in 4.25 SIMD cycles on gfx950
+# (profiles/r01_f16_rate.txt).
+FLOOR_PACKED_OPS = {True: 5, False: 3}
+PACKED_OP_CYCLES = 4.25
+
+
+def algorithmic_peak_gcups(affine, clock_ghz):
+    """1,024 SIMDs x clock / (floor packed ops x 4.25 cycles) x 128 cells
+    (a wave64 packed op updates 2 x 64 cells)."""
+    return SIMDS * clock_ghz * 1e9 / (FLOOR_PACKED_OPS[affine] * PACKED_OP_CYCLES) * 128 / 1e9
+
+
+def valu_roofline(kernel, cells_rank, scan_ms, kernel_gcups, affine, clock_load_ghz=None):
+    """The binding roofline: VALU instruction issue.  achieved = the whole
+    scan's rate (all kernels of the scan, concurrent).
+    `algorithmic`: peak = the algorithm's floor of packed ops per cell pair
+    (FLOOR_PACKED_OPS) at 4.25 cycles each on every SIMD, at the 2.4 GHz
+    peak clock and at the clock measured under this load (the stored SQ
+    pass, when it is of this build): the distance of the scan from the
+    algorithm, every instruction the kernels add counted against them.
+    `issue_efficiency`: peak = the rate the kernel's OWN compiled
+    instruction mix allows (VALU_MODEL, hipcc -S counts); its frac measures
+    how well the code as written issues, not how far it is from the floor."""
+    if scan_ms <= 0:
         return None
-    peak = SIMDS * CLOCK_HZ / cpc / 1e9
     achieved = cells_rank / (scan_ms * 1e-3) / 1e9
-    return {"bound": "valu-issue", "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "GCUPS",
-            "frac": round(achieved / peak, 4), "kernel": kernel, "simd_cycles_per_cell": round(cpc, 5),
-            "kernel_alone_gcups_while_concurrent": round(kernel_gcups, 1)}
+    peak = algorithmic_peak_gcups(affine, CLOCK_HZ / 1e9)
+    alg = {"floor_packed_ops_per_cell_pair": FLOOR_PACKED_OPS[affine], "cycles_per_packed_op": PACKED_OP_CYCLES,
+           "simds": SIMDS, "clock_ghz": CLOCK_HZ / 1e9, "peak": round(peak, 1), "frac": round(achieved / peak, 4),
+           "clock_ghz_under_load": clock_load_ghz, "peak_under_load": None, "frac_under_load": None}
+    if clock_load_ghz:
+        pl = algorithmic_peak_gcups(affine, clock_load_ghz)
+        alg["peak_under_load"] = round(pl, 1)
+        alg["frac_under_load"] = round(achieved / pl, 4)
+    out = {"bound": "valu-issue", "achieved": round(achieved, 1), "peak": alg["peak"], "unit": "GCUPS",
+           "frac": alg["frac"], "kernel": kernel, "algorithmic": alg,
+           "kernel_alone_gcups_while_concurrent": round(kernel_gcups, 1)}
+    cpc = VALU_MODEL.get(kernel.split("+")[0])  # "+int16[0,n)": the widest blocks in int16 beside it
+    if cpc is not None:
+        ip = SIMDS * CLOCK_HZ / cpc / 1e9
+        out["issue_efficiency"] = {"peak": round(ip, 1), "frac": round(achieved / ip, 4),
+                                   "simd_cycles_per_cell": round(cpc, 5),
+                                   "note": "peak from the kernel's own compiled instruction mix (VALU_MODEL): "
+                                           "issue efficiency of the code as written, not a roofline"}
+    return out
+
+
+def reference_scoring_summary(elapsed_s, cells_all, steps, kt, kernels, cold_ms, parity, parity_ok):
+    """The `reference_scoring` object: the same step timed under the
+    reference's own scoring (BLOSUM50 of SWSolver.cu:54-81, linear gap 2 of
+    :7), with the parity of its last step's scores against the oracle."""
+    n = max(kt["scans"], 1)
+    out = {"scoring": "BLOSUM50 (SWSolver.cu:54-81), linear gap 2 (the reference's own)",
+           "value": round(cells_all * steps / elapsed_s / 1e9, 2), "unit": "GCUPS",
+           "ms_per_step": round(elapsed_s * 1e3 / steps, 3), "kernel": kernels[0], "intra_kernel": kernels[1],
+           "kernel_ms_per_scan": {"sw_inter": round(kt["wave_ms"] / n, 4),
+                                  "sw_inter_coop": round(kt["coop_ms"] / n, 4),
+                                  "sw_intra": round(kt["intra_ms"] / n, 4),
+                                  "scan_total": round(kt["total_ms"] / n, 4)},
+           "cold_first_scan_ms": cold_ms}
+    if parity is not None:
+        out["parity"] = parity
+        out["parity_ok"] = parity_ok
+    return out
 
 
 def host_sampler(res, offs):
@@ -699,6 +756,14 @@ def main():
 
     cells_rank = float(qtot) * residues
 
+    def one_step_ms():
+        """One step alone, synchronised on both sides (host wall clock)."""
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        return round((time.perf_counter() - t) * 1e3, 4)
+
     def timed_loop(steps=None, warmup=None):
         """W untimed steps, then K timed steps between barrier + sync pairs;
         returns (max-over-ranks seconds, all ranks' cells per step, kernel
@@ -731,6 +796,9 @@ def main():
             return float(tmax[0]), float(t[1]), kt, (handle.last_kernel(), handle.last_intra_kernel())
         return elapsed, cells_rank, kt, (handle.last_kernel(), handle.last_intra_kernel())
 
+    # the first step on this database (and scoring): lazy allocations, the
+    # merged launch's table, the adaptive routing's first observation
+    cold_first = one_step_ms()
     elapsed_max, cells_all, kt, (kernel, intra_kernel) = timed_loop()
     st = db.stats()  # the coop split of the timed scans
     sustained = None
@@ -745,20 +813,25 @@ def main():
     # the measured run's scores and keys (its last step's buffer), for the parity leg
     gs = scores_buf[(counter[0] - 1) % NBUF].cpu().numpy()[:, :n]
     dev_top = top.cpu().numpy()
+    # a cold scan next to a warm one: the adaptive routing (which kernel
+    # forms a scan runs depends on what earlier scans of this database
+    # observed: the int16 span of the widest blocks, the intra order) forgotten
+    # by sw_db_reset_adaptive, then the same step again
+    db.reset_adaptive()
+    cold_warm = {"first_scan_ms": cold_first, "after_reset_adaptive_ms": one_step_ms(), "warm_ms": one_step_ms(),
+                 "timed_ms_per_step": round(elapsed_max * 1e3 / args.steps, 4),
+                 "note": "single steps synchronised on both sides (host clock, launch latency included): the "
+                         "database's first step, one after sw_db_reset_adaptive, one after that"}
 
     ref = None
+    r_parity = None
     if not args.no_reference_scoring:
         scoring = (sw.capi.builtin_matrix(0), 2, 2)  # SWSolver.cu:54-81, GAP_PENALTY 2 (:7)
+        r_cold = one_step_ms()
         r_elapsed, r_cells, r_kt, r_kernel = timed_loop()
-        r_n = max(r_kt["scans"], 1)
-        ref = {"scoring": "BLOSUM50 (SWSolver.cu:54-81), linear gap 2 (the reference's own)",
-               "value": round(r_cells * args.steps / r_elapsed / 1e9, 2), "unit": "GCUPS",
-               "ms_per_step": round(r_elapsed * 1e3 / args.steps, 3), "kernel": r_kernel[0],
-               "intra_kernel": r_kernel[1],
-               "kernel_ms_per_scan": {"sw_inter": round(r_kt["wave_ms"] / r_n, 4),
-                                      "sw_inter_coop": round(r_kt["coop_ms"] / r_n, 4),
-                                      "sw_intra": round(r_kt["intra_ms"] / r_n, 4),
-                                      "scan_total": round(r_kt["total_ms"] / r_n, 4)}}
+        # its last step's scores and keys, re-checked against the oracle below
+        r_parity = (scores_buf[(counter[0] - 1) % NBUF].cpu().numpy()[:, :n], top.cpu().numpy(),
+                    (final if world > 1 else top).cpu().numpy(), scoring)
         scoring = (mat, args.gap_open, args.gap_extend)
 
     eff, aff, quota = host_cores()
@@ -768,6 +841,13 @@ def main():
     if not args.no_verify:
         verify_res, verify_ok = verify(sw, sw.dist, world, rank, queries, sampler, n, gids, gs, dev_top, final_keys,
                                        K, scoring, vthreads, args.verify_seconds, args.backend)
+    if r_parity is not None:
+        r_res, r_ok = None, None
+        if not args.no_verify:
+            r_gs, r_top, r_final, r_scoring = r_parity
+            r_res, r_ok = verify(sw, sw.dist, world, rank, queries, sampler, n, gids, r_gs, r_top, r_final, K,
+                                 r_scoring, vthreads, args.verify_seconds, args.backend)
+        ref = reference_scoring_summary(r_elapsed, r_cells, args.steps, r_kt, r_kernel, r_cold, r_res, r_ok)
 
     if rank == 0:
         value = cells_all * args.steps / elapsed_max / 1e9
@@ -818,6 +898,7 @@ def main():
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
         traffic, traffic_note = None, "no rocprofv3 --pmc measurement of this workload and build"
         valu_hw = None
+        affine = args.gap_open != args.gap_extend
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
@@ -908,8 +989,11 @@ def main():
                          "traffic": traffic, "traffic_note": traffic_note,
                          "kernel": roof_kernel, "workload_key": workload_key(args, qtot),
                          "alg_bytes_per_launch": int(alg_bytes), "kernel_ms": round(kernel_ms, 4)},
-            "valu_roofline": valu_roofline(roof_kernel, cells_all / world, kt["total_ms"] / nsc * nq, wave_gcups),
+            "valu_roofline": valu_roofline(roof_kernel, cells_all / world, kt["total_ms"] / nsc * nq, wave_gcups,
+                                           affine, (valu_hw or {}).get("clock_ghz_under_load")),
             "valu_hw": valu_hw,
+            "cold_first_scan_ms": cold_first,
+            "cold_warm": cold_warm,
             "kernels": {"inter": kernel, "intra": intra_kernel},
             # each step's device top-K: one launch per query (sw_topk.hip
             # sw_topk_fused) on the exchange stream, beside the next scan
@@ -927,6 +1011,9 @@ def main():
         if verify_res is not None:
             out["parity"] = verify_res
             out["parity_sample_ok"] = verify_ok
+            if ref is not None and ref.get("parity_ok") is not None:
+                # every scoring the line reports is checked
+                out["parity_sample_ok"] = bool(verify_ok and ref["parity_ok"])
         if not args.no_cpu_baseline and world == 1 and not args.shard_of:
             threads = args.cpu_threads or eff
             cb, cparity = cpu_baseline(queries, sampler, n, gs, args.cpu_seconds, threads, scoring,

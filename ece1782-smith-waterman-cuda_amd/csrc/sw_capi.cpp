@@ -229,7 +229,8 @@ sw_opts default_opts() {
     o.size = static_cast<int32_t>(sizeof o);
     for (int32_t* f : {&o.lpt, &o.lpt_pipe, &o.quad_width, &o.pair_width, &o.pair_group, &o.coop_width,
                        &o.coop_skew, &o.intra_x2, &o.intra_x2_rows, &o.intra_i16_first, &o.inter_i16_span,
-                       &o.int16_guard, &o.rescue_stats, &o.tail_pairs, &o.lpt_persist, &o.lpt_rows})
+                       &o.int16_guard, &o.rescue_stats, &o.tail_pairs, &o.lpt_persist, &o.lpt_rows,
+                       &o.drain_spin})
         *f = -1;
     return o;
 }
@@ -237,6 +238,7 @@ sw_opts default_opts() {
 
 struct sw_handle {
     int device = 0;
+    int cus = 0;  // compute units of the device
     hipStream_t stream = nullptr;
     bool own_stream = false;
     // One event set per scan since the last sw_timing_reset (grows as needed,
@@ -311,11 +313,18 @@ struct sw_handle {
     sw_opts opts = default_opts();  // kernel-form overrides (sw_set_opts); all -1 = the library's choice
 };
 
+// Faults reported so far (any handle): a drain that gave up on an entry
+// left claimed entries of its database's rescue lists un-reset, so every
+// database re-initialises its lists at its first scan after a fault
+// (sw_db::list_epoch) and later scans are exact again.
+static std::atomic<uint64_t> g_fault_epoch{0};
+
 // A kernel of this handle reported a fault since the last check (sw_kernels.h
 // list_wait_take): fail loudly, once.
 static int check_fault(sw_handle* h) {
     if (h && h->h_fault && __atomic_load_n(h->h_fault, __ATOMIC_ACQUIRE)) {
         __atomic_store_n(h->h_fault, 0, __ATOMIC_RELEASE);
+        g_fault_epoch.fetch_add(1);
         return fail(SW_E_DEVICE, "sw_scan_lpt: a claimed rescue-list entry never appeared; the handle's scans "
                                  "since the last successful call may hold unrescued scores");
     }
@@ -348,6 +357,7 @@ struct sw_db {
     // (two parities of these lists: consecutive scans of a batch alternate)
     int32_t* d_rescue = nullptr;
     int32_t* d_lrescue = nullptr;        // [count, subjects...] x 2: the intra rescue chain's lists
+    uint64_t list_epoch = 0;             // g_fault_epoch when the lists were last known clean
     // boundary rows of deferred rescue tails (inter H, F; intra H, F), when
     // device memory allows them (else the tails run in stream order)
     int32_t* d_rbnd_h = nullptr;
@@ -1028,11 +1038,8 @@ double intra_step_us(int ri) { return 2 * 0.157 * (ri * 28.8 + 80.0) / (6 * 28.8
 // Under linear gaps the intra step is relatively dearer than under affine
 // ones (C2's 1/8 share, profiles/r05_trace/: intra / inter item medians 0.31
 // against 0.28); scaling its estimates for linear scans by 85, 120 or 140 %
-// (CAPIFLAGS=-DSW_LPT_LIN_INTRA=...) made the share's reference-scoring rate
-// 1.8, 0.8 and 3.6 % lower (profiles/r05_ab/lpt_lin_intra/): 100.
-#ifndef SW_LPT_LIN_INTRA
-#define SW_LPT_LIN_INTRA 100
-#endif
+// made the share's reference-scoring rate 1.8, 0.8 and 3.6 % lower
+// (profiles/r05_ab/lpt_lin_intra/): the same cost as under affine gaps.
 
 // The widest group blocks of the merged launch run by quads: those at least
 // kQuadFrac x the long threshold wide, whose pair latency would otherwise
@@ -1075,9 +1082,7 @@ int32_t lpt_tail_blocks(const sw_db* db, int32_t npair, int passes) {
     if (db->h->opts.tail_pairs >= 0) {
         n = db->h->opts.tail_pairs;
     } else {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, db->h->device) != hipSuccess) cus = 0;
-        const int64_t slots = 2 * static_cast<int64_t>(cus);  // workgroups per CU: 2
+        const int64_t slots = 2 * static_cast<int64_t>(db->h->cus);  // workgroups per CU: 2
         if (slots > 0 && singles > 2 * swk::kWavesPerWG * slots) n = slots;
         else if (slots > 0 && singles > slots) n = slots / 4;  // (C2's 1/2 and 1/4 shares)
     }
@@ -1121,7 +1126,7 @@ int lpt_table(sw_db* db, int32_t qpad, int rows, int32_t qpad_intra, int ri, int
     const int64_t npairs = (db->nlong + 1) / 2;
     const int64_t iwg = (npairs + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
     const int nch = qpad_intra / (swk::kLanes * ri);
-    const double step_us = intra_step_us(ri) * (affine ? 1.0 : SW_LPT_LIN_INTRA / 100.0);
+    const double step_us = intra_step_us(ri);
     std::vector<std::pair<double, int32_t>> w;
     w.reserve(static_cast<size_t>(pwg + swg + twg + iwg));
     auto width = [&](int64_t b) { return static_cast<int64_t>(db->h_blk_groups[b]) * swk::kGroupCols; };
@@ -1377,7 +1382,10 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
     // or 8 only) even where the cost model prefers more rows per lane for the
     // long subjects alone: its tail pairs and looped grid win more (C3's long
     // queries at 8 rows: +1.3 %; under linear gaps the wider form stays,
-    // -6.9 % at 8 rows: profiles/r05_ab/c3_ri8/)
+    // -6.9 % at 8 rows: profiles/r05_ab/c3_ri8/).  Tentative: a scan that
+    // does not take the merged launch after all (below) gets the cost
+    // model's rows back.
+    const int ri2_model = ri2;
     if (affine && ri2 > 8 && db->nblocks && O.intra_x2_rows < 0) ri2 = 8;
     // The intra chain's order.  Linear scoring with cheap gaps makes random
     // pairs' scores grow with their lengths, so on long subjects the fp16
@@ -1459,7 +1467,7 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
             if (o.key == skey && o.qlen <= qlen) i16_span = std::max(i16_span, o.span);
     }
     i16_span = static_cast<int32_t>(std::min<int64_t>(std::max(i16_span, 0), db->nblocks));
-    const int32_t qpad_intra2 = ri2 ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri2)) : 0;
+    int32_t qpad_intra2 = ri2 ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri2)) : 0;
     // Empty query: every score is 0 (the reference's kernel leaves maxScore 0).
     if (qlen == 0) {
         db->last_ncoop = 0;
@@ -1512,6 +1520,10 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
                      f16 && rescue && npair && !ncoop && i16_span == 0 &&
                      swk::lpt_supported(ri2);
     db->last_lpt = lpt;
+    if (!lpt && ri2 != ri2_model) {  // the separate intra launch: the cost model's shape
+        ri2 = ri2_model;
+        qpad_intra2 = static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri2));
+    }
     // ... and that launch re-scores what it flags itself (sw_scan_lpt's drain,
     // swk::DrainArgs): no rescue launches after it, on boundary rows of its
     // own (the deferred tails', when device memory allows them), with the
@@ -1549,6 +1561,12 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&db->d_lrescue), 2 * lstride * sizeof(int32_t)));
         HIPCHECK(hipMemsetAsync(db->d_lrescue, 0xff, 2 * lstride * sizeof(int32_t), h->stream));
         db->device_bytes += 2 * lstride * sizeof(int32_t);
+    }
+    if (db->list_epoch != g_fault_epoch.load()) {  // a fault since: entries may be left claimed
+        if ((rc = join_tails(h))) return rc;
+        if (db->d_rescue) HIPCHECK(hipMemsetAsync(db->d_rescue, 0xff, 2 * rstride * sizeof(int32_t), h->stream));
+        if (db->d_lrescue) HIPCHECK(hipMemsetAsync(db->d_lrescue, 0xff, 2 * lstride * sizeof(int32_t), h->stream));
+        db->list_epoch = g_fault_epoch.load();
     }
     // this scan's list set; a deferred tail of the scan before last used it
     const int par = h->parity;
@@ -1888,15 +1906,20 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
                 d.heads[2] = head1;
                 d.heads[3] = head1 + 1;
                 d.fault = h->d_fault;
+                d.spin = O.drain_spin >= 0 ? O.drain_spin : (1 << 22);
+                // (every field of d the blob's bytes depend on)
                 const std::vector<uint64_t> key = {
                     reinterpret_cast<uint64_t>(P.dev), P.off8, P.off16, P.intra_off, static_cast<uint64_t>(par),
                     reinterpret_cast<uint64_t>(scores_dev), static_cast<uint64_t>(qlen), skey,
                     static_cast<uint64_t>(npair), static_cast<uint64_t>(nquad) | static_cast<uint64_t>(ntail) << 32,
                     static_cast<uint64_t>(P.stride),
-                    reinterpret_cast<uint64_t>(a.trace)};
+                    reinterpret_cast<uint64_t>(a.trace),
+                    static_cast<uint64_t>(ri2) | static_cast<uint64_t>(lpt_rows) << 16 |
+                        static_cast<uint64_t>(npipe) << 32,
+                    static_cast<uint64_t>(static_cast<uint32_t>(d.spin))};
                 if ((rc = drain_blob(db, h->stream, key, d, &dargs))) return rc;
             }
-            HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, order, nwg, affine, ri2, h->stream, dargs, lpt_next,
+            HIPCHECK(swk::launch_scan_lpt(a, lpt_intra, order, nwg, affine, ri2, h->cus, h->stream, dargs, lpt_next,
                                           O.lpt_persist >= 2 ? O.lpt_persist : 0, lpt_rows));
             // (a draining launch ends the scan: its end event is ev[3])
             if (!drain) MARK(7, h->stream);
@@ -2041,6 +2064,7 @@ int topk_impl(sw_handle* h, const int32_t* scores, const int64_t* keys, int64_t 
     if (id_base < 0 || id_base + n > (int64_t(1) << 31)) return fail(SW_E_INVALID, "ids must fit in 31 bits");
     HIPCHECK(hipSetDevice(h->device));
     int rc;
+    if ((rc = check_fault(h))) return rc;
     if ((rc = ensure_topk_work(h, swk::topk_workspace_bytes(n, k)))) return rc;
     swk::TopkSrc src{};
     src.scores = keys ? nullptr : scores;
@@ -2102,6 +2126,9 @@ int sw_create(int32_t device, sw_handle** out) {
     auto* h = new (std::nothrow) sw_handle();
     if (!h) return fail(SW_E_NOMEM, "out of host memory");
     h->device = device;
+    // the device's CUs, once (the merged launch's slot counts: lpt_tail_blocks,
+    // the looped grid's size)
+    if (hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) h->cus = 0;
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete h; return fail(SW_E_HIP, hipGetErrorString(e)); }
     h->own_stream = true;
@@ -2207,7 +2234,8 @@ int sw_opts_from_env(sw_opts* o) {
                 {"SW_RESCUE_STATS", &o->rescue_stats},
                 {"SW_TAIL_PAIRS", &o->tail_pairs},
                 {"SW_LPT_PERSIST", &o->lpt_persist},
-                {"SW_LPT_ROWS", &o->lpt_rows}};
+                {"SW_LPT_ROWS", &o->lpt_rows},
+                {"SW_DRAIN_SPIN", &o->drain_spin}};
     for (const auto& k : ints)
         if (const char* e = std::getenv(k.name); e && e[0]) *k.field = std::atoi(e);
     if (const char* e = std::getenv("SW_INTER_VARIANT"))
@@ -2637,6 +2665,8 @@ int sw_get_timing(sw_handle* h, sw_timing* out) {
 
 int sw_stream_wait_scan(sw_handle* h, void* hip_stream) {
     if (!h) return fail(SW_E_INVALID, "null handle");
+    int rc;
+    if ((rc = check_fault(h))) return rc;  // (a completed earlier scan's fault)
     if (!h->timed || h->nscans == 0) return SW_OK;  // no scan yet: nothing to wait for
     HIPCHECK(hipSetDevice(h->device));
     HIPCHECK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(hip_stream), h->evpool[h->nscans - 1].ev[3], 0));

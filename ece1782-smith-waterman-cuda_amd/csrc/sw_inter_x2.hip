@@ -436,7 +436,7 @@ __device__ __forceinline__ void ring_load(uint32_t (&v)[SG], const int4* ring, i
     }
 }
 
-// Flag-synchronised wave groups (affine gaps; SW_PAIR_FLAGS): instead of one workgroup
+// Flag-synchronised wave groups (affine gaps): instead of one workgroup
 // barrier per sub-group (a tick shared by every wave of the workgroup, the
 // two pairs of a workgroup included), each wave publishes in LDS how many
 // sub-groups it has completed over its passes, and waits only where the data
@@ -453,13 +453,10 @@ __device__ __forceinline__ void ring_load(uint32_t (&v)[SG], const int4* ring, i
 // Measured (profiles/r05_ab/pair_flags/, same box, two runs each): affine
 // gaps C2 +0.3 %, its 1/8 share +0.9 %, 1/4 +0.4 %, wave groups on every
 // block +1.6 % against the tick form; the linear cell's cheaper sub-groups
-// lost 0.1-0.5 % with the per-sub-group release and count.  SW_PAIR_FLAGS:
-// 0 ticks everywhere, 1 flags everywhere, 2 flags under affine gaps (default).
-#ifndef SW_PAIR_FLAGS
-#define SW_PAIR_FLAGS 2
-#endif
+// lost 0.1-0.5 % with the per-sub-group release and count, so linear groups
+// keep the tick (the other forms' numbers: profiles/r05_ab/pair_flags/).
 template <bool AFFINE>
-constexpr bool pair_flags() { return SW_PAIR_FLAGS == 1 || (SW_PAIR_FLAGS == 2 && AFFINE); }
+constexpr bool pair_flags() { return AFFINE; }
 struct PairSync {
     int* prog;      // LDS: completed sub-groups of each wave of the workgroup
     int me;         // this wave
@@ -488,11 +485,6 @@ __device__ __forceinline__ void pair_wait(const int* prog, int wave, int need) {
 // restart; SG columns later the same for the hi image and the high halves.
 // The low strip's row -1 input of pass k's first columns was stored by pass
 // k-1's high strip at least one sub-group earlier (ncols >= 32).
-#ifndef SW_HOIST_FMA
-#define SW_HOIST_FMA 1
-#endif
-constexpr bool kHoistFma = SW_HOIST_FMA != 0;
-
 template <int R, int SG, bool AFFINE, bool F16, bool PAIR, int CR = 16, bool CHAIN = false>
 __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32_t ncols, uint64_t base, int lane,
                                          int s0, Best<F16>& best, const int4* ring_in, int4* ring_out,
@@ -684,38 +676,13 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
                 diag = H[r];
                 H[r] = h;
                 up = h;
-            } else if constexpr (F16) {
-                // Biased Farrar cell.  Cell (r, jj) holds H~ = H + b, E' = E + b,
-                // F~ = F + b with b = (r % 16 + jj) ge, so both gap extensions
-                // are the drift of the bias: E' = max(E', m) along the row and
-                // F~ = max3(F~, m, floor) down the column with m = H~ - go + ge,
-                // no subtraction.  F carries the 0 floor (H >= 0), b of the
-                // next row.  5 packed ops per cell pair (+ about half a max3
-                // for the maximum, 2 per row per sub-group for the column
-                // rebase, 4 per column for the row-group resets).
-                const int rg = r % kRowGroup;
-                if (rg == 0 && r > 0) f = f - grp_h;  // next row group: its bias restarts at 0
-                const h2 h = max3h(E[r], f, __builtin_elementwise_fma(slo, shi, diag));
-                const h2 m = h - gog_h;
-                E[r] = __builtin_elementwise_maximum(E[r], m);
-                f = max3h(f, m, __builtin_bit_cast(h2, a.f16_step[rg + jj + 1]));
-                h2& acc = best.acc[rg + jj];
-                if (jj & 1) {
-                    if (rg + 1 < kRowGroup) acc = max3h(acc, h, H[r + 1]);  // H[r + 1]: cell (r + 1, jj - 1)
-                    else acc = __builtin_elementwise_maximum(acc, h);
-                } else if (rg == 0) {  // the even columns' other rows are partners above
-                    acc = __builtin_elementwise_maximum(acc, h);
-                }
-                diag = H[r];
-                H[r] = h;
-                up = h;
             } else if constexpr (!AFFINE) {
                 const s2 h = usub2(max2(max2(H[r], up), slo * shi + diag), go2);
                 diag = H[r];
                 H[r] = h;
                 up = h;
                 best.v = max2(best.v, h);
-            } else {
+            } else if constexpr (!F16) {  // (fp16 affine: cell_d below)
                 const s2 h = max2(max2(E[r], f), slo * shi + diag);
                 const s2 n = usub2(h, go2);
                 E[r] = max2(usub2(E[r], ge2), n);
@@ -726,20 +693,27 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
                 best.v = max2(best.v, h);
             }
         };
-        // the biased Farrar cell above with its diagonal sum d given
+        // The biased Farrar cell (fp16, affine), its diagonal sum d given.
+        // Cell (r, jj) holds H~ = H + b, E' = E + b, F~ = F + b with b = (r %
+        // 16 + jj) ge, so both gap extensions are the drift of the bias: E' =
+        // max(E', m) along the row and F~ = max3(F~, m, floor) down the column
+        // with m = H~ - go + ge, no subtraction.  F carries the 0 floor (H >=
+        // 0), b of the next row.  5 packed ops per cell pair (+ about half a
+        // max3 for the maximum, 2 per row per sub-group for the column rebase,
+        // 4 per column for the row-group resets).
         auto cell_d = [&](const int r, const int jj, V& up, V& diag, V& f, const V d) {
           if constexpr (F16 && AFFINE) {
             const int rg = r % kRowGroup;
-            if (rg == 0 && r > 0) f = f - grp_h;
+            if (rg == 0 && r > 0) f = f - grp_h;  // next row group: its bias restarts at 0
             const h2 h = max3h(E[r], f, d);
             const h2 m = h - gog_h;
             E[r] = __builtin_elementwise_maximum(E[r], m);
             f = max3h(f, m, __builtin_bit_cast(h2, a.f16_step[rg + jj + 1]));
             h2& acc = best.acc[rg + jj];
             if (jj & 1) {
-                if (rg + 1 < kRowGroup) acc = max3h(acc, h, H[r + 1]);
+                if (rg + 1 < kRowGroup) acc = max3h(acc, h, H[r + 1]);  // H[r + 1]: cell (r + 1, jj - 1)
                 else acc = __builtin_elementwise_maximum(acc, h);
-            } else if (rg == 0) {
+            } else if (rg == 0) {  // the even columns' other rows are partners above
                 acc = __builtin_elementwise_maximum(acc, h);
             }
             diag = H[r];
@@ -788,7 +762,7 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
             if (k == 0) col_start(up, diag, f, jj);
             const int4(&pl)[CQ] = PL[t & 1];
             const int4(&ph)[CQ] = PH[t & 1];
-            if constexpr (F16 && AFFINE && kHoistFma) {
+            if constexpr (F16 && AFFINE) {
                 // the step's CR diagonal sums first (they read only the old H
                 // values), so the dependent chain h -> m -> F of each row has
                 // independent work beside it
@@ -866,11 +840,6 @@ __device__ __forceinline__ void x2s_pass(const InterArgs& a, X2Lds<R>& L, uint32
     }
 }
 
-#ifndef SW_X2_CHAIN
-#define SW_X2_CHAIN 1
-#endif
-constexpr bool kChainPasses = SW_X2_CHAIN != 0;
-
 // A block's width for the fp16 / int16 kernels: the longest subject rounded
 // up to 8 columns when the host provides it (the last 16-column group may be
 // half used: 8 pad columns fewer per pass for half the blocks, C2 2.1 -> 1.0 %
@@ -886,7 +855,7 @@ __device__ __forceinline__ bool x2s_block(const InterArgs& a, int blk, X2Lds<R>&
     Best<F16> best;
     best.init(a);
     const uint64_t t0 = trace_now();
-    if (kChainPasses && ncols >= 32 && a.qpad > 2 * R) {
+    if (ncols >= 32 && a.qpad > 2 * R) {
         x2s_pass<R, SG, AFFINE, F16, false, CR, true>(a, L, ncols, base, lane, 0, best, nullptr, nullptr, nullptr);
     } else {
         for (int s0 = 0; s0 < a.qpad && ncols > 0; s0 += 2 * R)
@@ -931,21 +900,11 @@ constexpr int kPairLag = 3;
 // 16.  These kernels hold 2 waves per SIMD (LDS and the ring buffers) and
 // the 16-row double buffer left them 148 B of register spills in the pass
 // loop; at 8 rows they spill nothing (C2 10,219 -> 10,320 GCUPS, C3
-// 10,323 -> 10,510, the 1/8 share 1.302 -> 1.309 ms per step).  -D
-// overrides for experiments; 3 waves per SIMD (SW_GROUP_WAVES_PER_EU=3)
-// does not fit: 168 registers spill 400-800 B.
-#ifndef SW_PAIR_CR
-#define SW_PAIR_CR 8
-#endif
-constexpr int kPairCR = SW_PAIR_CR;
-#ifndef SW_SINGLE_CR
-#define SW_SINGLE_CR 8
-#endif
-constexpr int kSingleCR = SW_SINGLE_CR;
-#ifndef SW_GROUP_WAVES_PER_EU
-#define SW_GROUP_WAVES_PER_EU 2
-#endif
-constexpr int kGroupWavesPerEU = SW_GROUP_WAVES_PER_EU;
+// 10,323 -> 10,510, the 1/8 share 1.302 -> 1.309 ms per step).  3 waves
+// per SIMD does not fit: 168 registers spill 400-800 B.
+constexpr int kPairCR = 8;
+constexpr int kSingleCR = 8;
+constexpr int kGroupWavesPerEU = 2;
 
 __device__ __forceinline__ int group_ticks(uint32_t ncols, int passes, int SG, int G) {
     if (ncols == 0 || passes <= 0) return 0;
@@ -965,7 +924,7 @@ struct X2pSmem {
     X2Lds<R> lds[kWavesPerWG];
     int4 ring[kWavesPerWG - kWavesPerWG / GMAX][kRingSlots * (SG / 4) * kLanes];
     uint32_t part[kWavesPerWG][kLanes];
-    int prog[kWavesPerWG];  // SW_PAIR_FLAGS: completed sub-groups per wave
+    int prog[kWavesPerWG];  // affine groups: completed sub-groups per wave
 };
 
 // One workgroup's work (wgi = its index in the launch's numbering):
@@ -1101,12 +1060,7 @@ __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_inter_x2p(InterArgs 
 // The intra forms of the merged launch read lane 0's conveyor inputs from
 // LDS under affine gaps (ix2 CONV, 4 KB beside the launch's 57 KB; C2's 1/8
 // share +0.6 %; the linear steps, shorter, lost 0.4 % with it and keep the
-// readlane form: profiles/r04_ab_lptconv/; SW_LPT_CONV=0: readlane
-// everywhere, for A/B builds)
-#ifndef SW_LPT_CONV
-#define SW_LPT_CONV 1
-#endif
-constexpr bool kLptConv = SW_LPT_CONV != 0;
+// readlane form: profiles/r04_ab_lptconv/)
 
 template <bool AFFINE>
 struct DrainShape {
@@ -1149,7 +1103,7 @@ __device__ __forceinline__ void lpt_drain(const DrainArgs* __restrict__ d, char*
             }
             int m = 0;
             for (int i = 0; i < n; ++i) {
-                const int v = list_wait_take(d->lists[kind - 1] + 1, start + i, d->fault);
+                const int v = list_wait_take(d->lists[kind - 1] + 1, start + i, d->fault, d->spin);
                 if (v >= 0) task[2 + m++] = v;
             }
             task[0] = m ? kind : (n ? -1 : 0);  // -1: claimed entries never appeared; look again
@@ -1243,10 +1197,10 @@ __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(LptParams p
             flagged = x2p_wg<R, SG, AFFINE, true, true, 4>(a, item, a.blk_quad,
                                                            *reinterpret_cast<X2pSmem<R, SG, 4>*>(smem));
         else if (-1 - item < niwg)
-            flagged = ix2::intra_x2_wg<RI, true, false, !AFFINE, true, false, kLptConv && AFFINE, true>(
+            flagged = ix2::intra_x2_wg<RI, true, false, !AFFINE, true, false, AFFINE, true>(
                 ia, -1 - item, reinterpret_cast<Elem*>(smem));
         else
-            flagged = ix2::intra_x2_wg<2, true, false, !AFFINE, true, true, kLptConv && AFFINE, true>(
+            flagged = ix2::intra_x2_wg<2, true, false, !AFFINE, true, true, AFFINE, true>(
                 ia, -1 - item - niwg, reinterpret_cast<PElem*>(smem));
         // Only a workgroup that appended an entry drains (and takes whatever is
         // listed, its own entries included): every entry is then taken by its
@@ -1266,28 +1220,27 @@ __global__ __launch_bounds__(256, kGroupWavesPerEU) void sw_scan_lpt(LptParams p
 }
 
 // Resident workgroups of sw_scan_lpt<...> on the device (the looped grid):
-// occupancy x CUs, once per instantiation.
+// occupancy (per CU, once per instantiation: the code object's, the same on
+// every device of the build's one architecture) x the handle's CUs.
 template <int R, int RI, bool AFFINE>
-static int lpt_slots() {
-    static const int slots = [] {
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sw_scan_lpt<R, 8, AFFINE, RI, true>,
+static int lpt_slots(int cus) {
+    static const int per = [] {
+        int p = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, sw_scan_lpt<R, 8, AFFINE, RI, true>,
                                                          kWavesPerWG * kLanes, 0) != hipSuccess)
             return 0;
-        return cus * per;
+        return p;
     }();
-    return slots;
+    return cus * per;
 }
 
 // The looped form from this many rounds of resident workgroups on.
 constexpr int kLptLoopRounds = 3;
 
 template <int R, int RI, bool AFFINE>
-static void launch_lpt_t(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, hipStream_t s,
-                         const DrainArgs* drain, int32_t* next, int loop_grid) {
-    int slots = next ? lpt_slots<R, RI, AFFINE>() : 0;
+static void launch_lpt_t(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, int cus,
+                         hipStream_t s, const DrainArgs* drain, int32_t* next, int loop_grid) {
+    int slots = next ? lpt_slots<R, RI, AFFINE>(cus) : 0;
     const dim3 block(kWavesPerWG * kLanes);
     if (next && loop_grid > 0) slots = std::min(loop_grid, n);  // forced (tests)
     if (slots > 0 && (n >= kLptLoopRounds * slots || (next && loop_grid > 0))) {
@@ -1302,13 +1255,13 @@ static void launch_lpt_t(const InterArgs& a, const IntraArgs& ia, const int32_t*
 bool lpt_supported(int ri) { return ri == 4 || ri == 6 || ri == 8; }
 
 hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri,
-                           hipStream_t s, const DrainArgs* drain, int32_t* next, int loop_grid, int rows) {
+                           int cus, hipStream_t s, const DrainArgs* drain, int32_t* next, int loop_grid, int rows) {
     if (n <= 0) return hipSuccess;
     if ((rows != 64 && rows != 96) || (rows == 96 && affine) || a.qpad % rows) return hipErrorInvalidValue;
 #define SW_LPT_RI(RI)                                                                          \
-    (affine ? launch_lpt_t<32, RI, true>(a, ia, order, n, s, drain, next, loop_grid)           \
-     : rows == 96 ? launch_lpt_t<48, RI, false>(a, ia, order, n, s, drain, next, loop_grid)   \
-                  : launch_lpt_t<32, RI, false>(a, ia, order, n, s, drain, next, loop_grid))
+    (affine ? launch_lpt_t<32, RI, true>(a, ia, order, n, cus, s, drain, next, loop_grid)           \
+     : rows == 96 ? launch_lpt_t<48, RI, false>(a, ia, order, n, cus, s, drain, next, loop_grid)   \
+                  : launch_lpt_t<32, RI, false>(a, ia, order, n, cus, s, drain, next, loop_grid))
     if (ri == 4) SW_LPT_RI(4);
     else if (ri == 6) SW_LPT_RI(6);
     else if (ri == 8) SW_LPT_RI(8);

@@ -156,19 +156,9 @@ struct IntraImg {
 // LIST: the rescue stage — subject pairs come from the device-side list of
 // the subjects the fp16 pass flagged (a.subj_list / a.list_count); the grid
 // covers the longest possible list and surplus workgroups return at once.
-// SW_IX2_PREFETCH: read the next step's profile words from LDS during this
-// step (its codes are known one step ahead), so the LDS latency is hidden
-// even when the SIMD's waves run in lockstep
-#ifndef SW_IX2_PREFETCH
-#define SW_IX2_PREFETCH 1
-#endif
-constexpr bool kPrefetch = SW_IX2_PREFETCH != 0;
-#ifndef SW_IX2_PIPE_PF
-#define SW_IX2_PIPE_PF 2
-#endif
-#ifndef SW_IX2_PIPE_PF_LIN
-#define SW_IX2_PIPE_PF_LIN 1
-#endif
+// Every step reads the NEXT step's profile words from LDS (its codes are
+// known one step ahead), so the LDS latency is hidden even when the SIMD's
+// waves run in lockstep (C5 7,553 -> 7,609 GCUPS, profiles/r01_prefetch/).
 
 // The LDS image of one chunk: [code][element][lane] (img_elems(RI) elements).
 template <int RI, bool F16>
@@ -220,7 +210,6 @@ template <int RI, bool F16, bool LIST, bool LIN = false, bool TAKE = true, bool 
           bool CONV = false, bool OPQ = false>
 __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typename IntraImg<RI, F16>::Elem* img) {
     static_assert(!(PIPE && LIST), "the pipelined form takes its pair by index");
-    static_assert(!CONV || kPrefetch, "the LDS conveyor serves the prefetching step");
     static_assert(RI % 2 == 0 && RI <= kIntraX2MaxRI, "rows per lane");
     constexpr int CH = kLanes * RI;  // query rows per chunk
     using C = IntraCell<F16>;
@@ -234,7 +223,7 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
     // profile prefetch distance in steps: the pipelined form's short affine
     // steps (RI 2) do not cover an LDS read's latency on a busy CU with one
     // (C2's 1/8 share +0.6 %; linear steps lost 3 % with 2, 6 % with 3)
-    constexpr int PF = PIPE ? (LIN ? SW_IX2_PIPE_PF_LIN : SW_IX2_PIPE_PF) : 1;
+    constexpr int PF = PIPE && !LIN ? 2 : 1;
     constexpr int NBUF = PF == 1 ? 2 : 4;
     static_assert(PF >= 1 && PF <= NBUF - 1, "prefetch distance");
     // OPQ (the merged launch's looped form): the thread index read opaquely
@@ -390,7 +379,7 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
                         cv[3 * kLanes + lane] = in_res_nb;
                     }
                 }
-                if (kPrefetch && k0 == 0) {
+                if (k0 == 0) {
 #pragma unroll
                     for (int d = 0; d < PF; ++d) {
                         rcq[d] = shr1u(__builtin_amdgcn_readlane(in_res, d), d == 0 ? rc : rcq[d > 0 ? d - 1 : 0]);
@@ -409,23 +398,18 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
                         static_assert(NB % NBUF == 0, "buffer period");
                         Elem(&wa)[NQ] = W[b % NBUF][0];
                         Elem(&wb)[NQ] = W[b % NBUF][1];
-                        if constexpr (kPrefetch) {
-                            rc = rcq[0];
+                        rc = rcq[0];
 #pragma unroll
-                            for (int d = 0; d + 1 < PF; ++d) rcq[d] = rcq[d + 1];
-                            // step b + PF's codes: lane 0 takes that column
-                            // (the next block's first ones at the block's last steps)
-                            const bool wrap = (b + PF >= NB) && (m0 + NB == kLanes);
-                            const uint32_t sres_n =
-                                CONV ? cv[2 * kLanes + m + PF]
-                                : wrap ? __builtin_amdgcn_readlane(in_res_nb, (b + PF - NB) & (kLanes - 1))
-                                       : __builtin_amdgcn_readlane(in_res, (m + PF) & (kLanes - 1));
-                            rcq[PF - 1] = shr1u(sres_n, PF > 1 ? rcq[PF > 1 ? PF - 2 : 0] : rc);
-                            read_words(rcq[PF - 1], W[(b + PF) % NBUF][0], W[(b + PF) % NBUF][1]);
-                        } else {
-                            rc = shr1u(__builtin_amdgcn_readlane(in_res, m), rc);
-                            read_words(rc, wa, wb);
-                        }
+                        for (int d = 0; d + 1 < PF; ++d) rcq[d] = rcq[d + 1];
+                        // step b + PF's codes: lane 0 takes that column
+                        // (the next block's first ones at the block's last steps)
+                        const bool wrap = (b + PF >= NB) && (m0 + NB == kLanes);
+                        const uint32_t sres_n =
+                            CONV ? cv[2 * kLanes + m + PF]
+                            : wrap ? __builtin_amdgcn_readlane(in_res_nb, (b + PF - NB) & (kLanes - 1))
+                                   : __builtin_amdgcn_readlane(in_res, (m + PF) & (kLanes - 1));
+                        rcq[PF - 1] = shr1u(sres_n, PF > 1 ? rcq[PF > 1 ? PF - 2 : 0] : rc);
+                        read_words(rcq[PF - 1], W[(b + PF) % NBUF][0], W[(b + PF) % NBUF][1]);
                         // hand-off: the row above's bottom (H, F) from one step back
                         const V adj = diff(RI - 1 + (b == 0 ? NB : 0));
                         // affine: the row above's H is only row 0's next

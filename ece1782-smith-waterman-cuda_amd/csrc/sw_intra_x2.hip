@@ -5,10 +5,6 @@
 
 #include <cstdlib>
 
-#ifndef SW_IX2_CONV
-#define SW_IX2_CONV 1
-#endif
-
 namespace swk {
 
 // The LDS conveyor (ix2 CONV: 1 KB per wave) wherever it leaves the
@@ -17,7 +13,7 @@ namespace swk {
 template <int RI, bool F16, bool LIST, bool LIN>
 __global__ __launch_bounds__(kWavesPerWG * kLanes) void sw_intra_x2(IntraArgs a) {
     __shared__ typename ix2::IntraImg<RI, F16>::Elem img[ix2::img_elems<RI, F16>()];
-    constexpr bool kConv = SW_IX2_CONV && RI != 16;
+    constexpr bool kConv = RI != 16;
     ix2::intra_x2_wg<RI, F16, LIST, LIN, true, false, kConv>(a, blockIdx.x, img);
 }
 

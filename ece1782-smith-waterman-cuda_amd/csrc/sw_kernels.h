@@ -199,13 +199,15 @@ __device__ __forceinline__ int32_t list_take(const int32_t* items, int i) {
 // Consumer in the producer's launch: wait until entry i is written, then
 // reset it.  The producer stores the entry right after its atomicAdd and a
 // wave is not preempted, so the entry appears within microseconds; the wait
-// is still bounded (about 0.1 s) so a wave can never hang here, and a timeout
-// is not silent: it sets *fault (host-visible, mapped), the library fails the
-// next call on that handle (SW_E_DEVICE) and the caller skips the entry.
-__device__ __forceinline__ int32_t list_wait_take(int32_t* items, int i, int32_t* fault) {
+// is still bounded (`bound` polls, by default 2^22: about 0.1 s) so a wave can
+// never hang here, and a timeout is not silent: it sets *fault (host-visible,
+// mapped), the library fails the next call on that handle (SW_E_DEVICE) and
+// the caller skips the entry.  (sw_opts drain_spin 0, tests: every wait times
+// out at once.)
+__device__ __forceinline__ int32_t list_wait_take(int32_t* items, int i, int32_t* fault, int32_t bound) {
     int32_t* p = items + i;
     int32_t v = -1;
-    for (int spin = 0; spin < (1 << 22); ++spin) {
+    for (int spin = 0; spin < bound; ++spin) {
         v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (v >= 0) break;
         __builtin_amdgcn_s_sleep(1);
@@ -306,6 +308,7 @@ struct DrainArgs {
     int32_t* lists[4];  // list A, B, 1, 2: [count, items...]
     int32_t* heads[4];  // their dequeue heads (zeroed per scan)
     int32_t* fault;     // host-mapped word: a claimed entry never appeared (list_wait_take)
+    int32_t spin;       // list_wait_take's bound (sw_opts drain_spin)
 };
 bool lpt_supported(int ri);
 // next (nullable; zero at launch): with it, a table of at least 3 rounds of
@@ -314,7 +317,8 @@ bool lpt_supported(int ri);
 // dispatcher's per-workgroup gaps avoided); otherwise one workgroup per
 // entry.  loop_grid > 0 (tests): that form with that many workgroups.
 // rows: query rows per pass, 64 (32-row strips) or, linear gaps only, 96.
-hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri,
+// cus: the device's compute units (the looped grid's size).
+hipError_t launch_scan_lpt(const InterArgs& a, const IntraArgs& ia, const int32_t* order, int n, bool affine, int ri, int cus,
                            hipStream_t s, const DrainArgs* drain = nullptr, int32_t* next = nullptr,
                            int loop_grid = 0, int rows = 64);
 // Lanes whose 16-bit running maximum reaches this may have overflowed.
@@ -329,10 +333,8 @@ constexpr int kIntraX2MaxRI = 20;
 // Steps per bias period of the intra kernel at RI rows per lane (one rebase
 // of every row's H and E per period): 16 at the widest shape, whose 2 waves
 // per SIMD leave registers for the 8 more anti-diagonal maxima; 8 otherwise.
-#ifndef SW_IX2_P16
-#define SW_IX2_P16 1  // (A/B builds: 0 = 8 steps at every shape; host and device alike)
-#endif
-constexpr int intra_period(int ri) { return SW_IX2_P16 && ri == kIntraX2MaxRI ? 16 : 8; }
+// (8 at RI 20 too: C5 8,809 against 8,983 GCUPS, profiles/r05_ab/intra_period16/)
+constexpr int intra_period(int ri) { return ri == kIntraX2MaxRI ? 16 : 8; }
 // Its biased cell stores values up to this many gap extensions above the
 // true ones (row RI - 1 at the last step of a bias period, + 2 ge in the
 // profile, + the F floor's step).

@@ -68,9 +68,6 @@ __global__ __launch_bounds__(kTopkThreads) void sw_topk_select(TopkSrc src, int6
 // The one-launch form: chunks of at most 8,192 keys (32 per thread), at
 // least 4,096 keys each up to 64 chunks; the final selection holds the
 // chunks' k survivors each in the same 8,192.
-#ifndef SW_TOPK_FUSED
-#define SW_TOPK_FUSED 1  // (A/B builds: 0 = the chained stages for every k)
-#endif
 constexpr int kFusedPer = 32;
 constexpr int kFusedMaxK = 1024;
 constexpr int64_t kFusedCap = 256 * kFusedPer;
@@ -84,7 +81,7 @@ struct TopkFused {
 };
 
 static bool fused_plan(int64_t n, int k, TopkFused* r) {
-    if (!SW_TOPK_FUSED || k > kFusedMaxK || n <= 0) return false;
+    if (k > kFusedMaxK || n <= 0) return false;
     int64_t c = std::max<int64_t>((n + kFusedCap - 1) / kFusedCap, std::min<int64_t>(64, (n + 4095) / 4096));
     const int64_t ch = (n + c - 1) / c;
     c = (n + ch - 1) / ch;
@@ -102,6 +99,19 @@ static bool fused_plan(int64_t n, int k, TopkFused* r) {
 // MI355X_MICROARCH.md measures valid without a release fence, whose L2
 // write-back would also flush the concurrent scan's dirty lines), selects
 // and sorts the k best and resets the counter.  One chunk: select and sort.
+//
+// What the hand-off relies on: on gfx94x / gfx950 (CDNA3/4)
+// (1) an agent-scope relaxed store is a write-through (sc1) store that
+// reaches the L2 every CU of the agent reads, and an agent-scope relaxed load
+// bypasses the CU's L1 (sc1), and (2) vector-memory STORES are counted in
+// vmcnt (these targets have no separate vscnt counter, unlike gfx10+), so
+// `s_waitcnt vmcnt(0)` in every wave, then the barrier, completes the
+// workgroup's stores before its arrival is counted.  Targets without both
+// would need a release / acquire pair (or the chained stages): the build
+// refuses them rather than rank on stale survivors.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "sw_topk_fused: the write-through hand-off is specified for gfx942 / gfx950 only"
+#endif
 __global__ __launch_bounds__(256) void sw_topk_fused(TopkFused r) {
     constexpr int T = 256;
     __shared__ TopkLds<T> L;

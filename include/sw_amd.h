@@ -54,7 +54,14 @@ extern "C" {
 #define SW_E_IO -6          /* file could not be read / written / validated */
 #define SW_E_DEVICE -7      /* a kernel reported an internal fault: the scores of the
                                handle's scans since the last successful call are not
-                               trusted (see sw_last_error) */
+                               trusted (see sw_last_error).  The device writes a
+                               host-mapped word; the asynchronous entry points
+                               (sw_scan_device, sw_scan_rank_device, the batch and
+                               group forms) return before their kernels end, so a
+                               fault is reported by the first call on the handle
+                               after the faulting kernel has completed (the
+                               synchronous sw_scan / sw_scan_topk / sw_scan_batch
+                               report their own) */
 
 #define SW_ALPHABET 25    /* residue codes 0..24 */
 #define SW_CODE_STAR 24
@@ -181,6 +188,10 @@ typedef struct sw_opts {
                                  workgroups (tests)                           SW_LPT_PERSIST */
     int32_t lpt_rows;         /* query rows per pass of the merged launch under
                                  linear gaps: 64 or 96 (default 96)           SW_LPT_ROWS */
+    int32_t drain_spin;       /* (tests) polls the merged launch's drain spends
+                                 waiting for a claimed rescue-list entry before
+                                 it gives up and faults (default 2^22; 0: at
+                                 once, i.e. the SW_E_DEVICE path)             SW_DRAIN_SPIN */
     char inter_variant[16];   /* inter kernel shape: "" (auto), "32x8", "64x8"
                                  (int32), "y32x8" (int16 two-strips), "f32x8",
                                  "f32x4" (its fp16 form)                       SW_INTER_VARIANT */

@@ -6,6 +6,8 @@ import os
 import subprocess
 import sys
 
+import numpy as np
+
 from conftest import REPO
 
 CONTRACT = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
@@ -113,3 +115,56 @@ def test_bench_rendezvous_retry(monkeypatch):
     monkeypatch.setattr(bench.subprocess, "Popen", FakeProc)
     assert bench.launch_ranks(2, ["--gpus", "2"]) == 0
     assert len(calls) == 2
+
+
+def test_bench_valu_roofline_algorithmic():
+    """valu_roofline: the algorithmic floor (5 packed ops per cell pair
+    affine, 3 linear, 4.25 cycles each, 1,024 SIMDs) beside the kernel's own
+    instruction mix (issue_efficiency)."""
+    sys.path.insert(0, REPO)
+    import bench
+    assert abs(bench.algorithmic_peak_gcups(True, 2.4) - 14803.0) < 1.0
+    assert abs(bench.algorithmic_peak_gcups(False, 2.4) - 24672.0) < 1.0
+    kern = "sw_inter_x2s<32,8,affine,fp16>"
+    v = bench.valu_roofline(kern, 7.68e10, 6.93, 11000.0, True, 2.2)
+    assert v["bound"] == "valu-issue" and v["unit"] == "GCUPS"
+    alg = v["algorithmic"]
+    assert alg["floor_packed_ops_per_cell_pair"] == 5 and alg["clock_ghz"] == 2.4
+    assert abs(v["achieved"] - 7.68e10 / 6.93e-3 / 1e9) < 0.1
+    assert abs(alg["frac"] - v["achieved"] / alg["peak"]) < 1e-3 and v["frac"] == alg["frac"]
+    assert abs(alg["peak_under_load"] - bench.algorithmic_peak_gcups(True, 2.2)) < 0.1
+    assert alg["frac_under_load"] > alg["frac"]
+    ie = v["issue_efficiency"]
+    assert ie["peak"] < alg["peak"] and ie["frac"] > alg["frac"]  # the kernel's own mix: more ops than the floor
+    lin = bench.valu_roofline("no-such-kernel", 1e10, 1.0, 0.0, False)
+    assert lin["algorithmic"]["floor_packed_ops_per_cell_pair"] == 3 and "issue_efficiency" not in lin
+    assert lin["algorithmic"]["peak_under_load"] is None
+
+
+def test_bench_reference_scoring_parity(sw, oracle):
+    """The reference-scoring leg's parity: bench.verify
+    under BLOSUM50 / linear 2 re-scores the whole (small) share with the
+    oracle and passes for the oracle's own scores, fails for one changed
+    score; reference_scoring_summary carries the result."""
+    sys.path.insert(0, REPO)
+    import bench
+    res, offs = sw.synth.database(400, shard=0)
+    n = len(offs) - 1
+    q = sw.encode(bench.read_query("P02232"))
+    scoring = (sw.capi.builtin_matrix(0), 2, 2)
+    gs = np.stack([oracle.scan(q, res, offs, mat=scoring[0], gap_open=2, gap_extend=2, nthreads=4)])
+    gids = np.arange(n, dtype=np.int32)
+    K = 10
+    top = np.stack([bench._pad_keys(sw.dist.local_topk(gs[0], gids, K), K)])
+    sampler = bench.host_sampler(res, offs)
+    sampler.full = (res, offs)
+    r, ok = bench.verify(sw, sw.dist, 1, 0, [q], sampler, n, gids, gs, top, top, K, scoring, 4, 30.0, "gloo")
+    assert ok and r["whole_database"] and r["scores_equal_oracle"] and r["merged_topk_equal"]
+    kt = {"scans": 4, "wave_ms": 4.0, "coop_ms": 0.0, "intra_ms": 0.4, "total_ms": 4.4}
+    d = bench.reference_scoring_summary(0.5, 1e9, 100, kt, ("k", "i"), 1.5, r, ok)
+    assert d["parity"]["scores_equal_oracle"] and d["parity_ok"] is True and d["cold_first_scan_ms"] == 1.5
+    assert abs(d["value"] - 1e9 * 100 / 0.5 / 1e9) < 1e-6 and "BLOSUM50" in d["scoring"]
+    bad = gs.copy()
+    bad[0, n // 2] += 1
+    r2, ok2 = bench.verify(sw, sw.dist, 1, 0, [q], sampler, n, gids, bad, top, top, K, scoring, 4, 30.0, "gloo")
+    assert not ok2 and not r2["scores_equal_oracle"]

@@ -702,6 +702,34 @@ def test_merged_launch_drains_rescue_lists(sw, oracle, handle, knobs, ri, scorin
     db.close()
 
 
+@pytest.mark.gpu
+def test_drain_timeout_reports_sw_e_device(sw, oracle, handle, knobs):
+    """a drain wait that gives up on a claimed rescue-list entry
+    (sw_opts drain_spin 0 makes every wait give up at once) is not silent:
+    the scan returns SW_E_DEVICE (-7) instead of unrescued scores, and the
+    database's next scan, with the default bound, re-initialises the lists
+    and equals the oracle again."""
+    knobs(lpt="1", pair_width="64", inter_i16_span="0", intra_i16_first="0", intra_x2_rows="8")
+    W = sw.encode("W")[0]
+    q = np.full(1200, W, dtype=np.uint8)  # planted copies score above fp16's 2,048: they flag
+    r, o = sw.synth.database(1500, shard=43)
+    extra = [np.full(1200, W, np.uint8), np.full(2600, W, np.uint8)]  # an inter block and a long subject
+    r2 = np.concatenate([r] + extra)
+    o2 = np.concatenate([o, o[-1] + np.cumsum([len(x) for x in extra])])
+    db = sw.Database(handle, r2, o2, long_threshold=2500)
+    m = sw.capi.builtin_matrix(1)
+    want = oracle.scan(q, r2, o2, mat=m, gap_open=12, gap_extend=1, nthreads=16)
+    assert int(want.max()) > 4096
+    knobs(drain_spin="0")
+    with pytest.raises(sw.capi.SWError, match="error -7"):
+        db.scan(q, m, 12, 1)
+    assert handle.last_kernel().endswith("+lpt+drain"), handle.last_kernel()
+    knobs(drain_spin="")
+    for _ in range(2):
+        assert np.array_equal(db.scan(q, m, 12, 1), want)
+    db.close()
+
+
 @pytest.mark.parametrize("scoring", [(0, 12, 1), (1, 12, 1)])
 def test_drain_waits_for_previous_deferred_tail(sw, oracle, handle, knobs, scoring):
     """in a batch, a merged launch that drains its rescue
