@@ -3,7 +3,7 @@ for offline analysis (run with a -DSW_TRACE_BLOCKS build via SW_AMD_LIB and
 SW_TRACE_FILE set).  Writes OUT.npz: trace [entries][start, end, HW_ID,
 XCC_ID | kind << 32] (s_memrealtime, 100 MHz), the block widths, the long
 subjects' lengths and the library's timing of the traced scan.
-usage: exp_share_dump.py SHARD_OF OUT.npz [LONG_THRESHOLD] [ref]
+usage: exp_share_dump.py SHARD_OF[:RANK] OUT.npz [LONG_THRESHOLD] [ref]
 (ref: the reference's scoring, BLOSUM50 with linear gap 2; default BLOSUM62
 affine 11/1)"""
 import json
@@ -18,13 +18,13 @@ import _swpkg  # noqa: E402
 
 sw = _swpkg.load()
 path = os.environ["SW_TRACE_FILE"]
-S = int(sys.argv[1])
+S, R = (int(x) for x in (sys.argv[1] + ":0").split(":")[:2])
 out = sys.argv[2]
 T = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 REF = len(sys.argv) > 4 and sys.argv[4] == "ref"
 res, offs = sw.synth.database(570000, shard=0)
 if S > 1:
-    _, res, offs = sw.dist.shard(res, offs, 0, S)
+    _, res, offs = sw.dist.shard(res, offs, R, S)
 with open(os.path.join(REPO, "tests", "golden", "queries", "P07327.fasta")) as f:
     q = sw.encode("".join(f.read().split("\n")[1:]))
 h = sw.Handle(0)
