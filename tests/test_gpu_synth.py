@@ -52,3 +52,36 @@ def test_synthetic_align_and_save(sw, oracle, handle, tmp_path):
     db.save(p)
     db2 = sw.Database.load(handle, p)
     assert np.array_equal(db2.scan(q), scores)
+
+
+def test_c4_full_rank_shard(sw, oracle, handle):
+    """one rank's WHOLE C4 shard at its bench size — the
+    last of 8 id ranges of the 50,000,000-subject database (6,250,000
+    subjects, ~2.25e9 residues generated in HBM) — scanned with the bench's
+    query and scoring (P07327, BLOSUM62 affine 12/1).  The device top-100
+    (sw_scan_topk) equals the CPU top-100 of the GPU's scores; every top-100
+    hit and a random sample of 400 subjects, regenerated on the CPU from
+    (seed, global id) by synth.counter_residues, score the same in the
+    oracle."""
+    seed, total, ranks = 1782, 50_000_000, 8
+    per = -(-total // ranks)
+    id_base = (ranks - 1) * per
+    n = total - id_base
+    assert n == 6_250_000
+    db = sw.Database.synthetic(handle, seed, n, id_base=id_base)
+    from conftest import read_query
+    q = sw.encode(read_query("P07327"))
+    m = sw.capi.builtin_matrix(1)
+    scores = db.scan(q, m, 12, 1)
+    assert scores.shape[0] >= n
+    scores = scores[:n]
+    keys = db.scan_topk(q, 100, m, 12, 1)
+    ids, sc = sw.capi.decode_keys(keys)
+    want_ids, want_sc = sw.capi.topk(scores, 100)
+    assert np.array_equal(ids, want_ids) and np.array_equal(sc, want_sc)
+    rng = np.random.default_rng(4)
+    sample = np.unique(np.concatenate([rng.choice(n, 400, replace=False), ids]))
+    r, o = regenerate(sw, seed, id_base + sample)
+    want = oracle.scan(q, r, o, mat=m, gap_open=12, gap_extend=1, nthreads=16)
+    assert np.array_equal(scores[sample], want), np.nonzero(scores[sample] != want)[0][:10]
+    db.close()
