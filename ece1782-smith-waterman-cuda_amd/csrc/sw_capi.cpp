@@ -230,7 +230,7 @@ sw_opts default_opts() {
     for (int32_t* f : {&o.lpt, &o.lpt_pipe, &o.quad_width, &o.pair_width, &o.pair_group, &o.coop_width,
                        &o.coop_skew, &o.intra_x2, &o.intra_x2_rows, &o.intra_i16_first, &o.inter_i16_span,
                        &o.int16_guard, &o.rescue_stats, &o.tail_pairs, &o.lpt_persist, &o.lpt_rows,
-                       &o.drain_spin})
+                       &o.tri_width, &o.drain_spin})
         *f = -1;
     return o;
 }
@@ -412,6 +412,7 @@ struct sw_db {
     struct LptTable {
         int32_t qpad, rows /* per pass */, qpad_intra, ri, npair, group /* quad blocks */, tail /* tail-pair blocks */, n;
         bool affine;
+        bool tri;  // the group blocks by 3-wave groups with a spare wave (InterArgs::blk_tri)
         int32_t npipe;  // the longest pairs, in the pipelined form
         int32_t pipe_opt;  // sw_opts lpt_pipe the table was built under
         int32_t* d_order;
@@ -1061,6 +1062,20 @@ int32_t lpt_quad_blocks(const sw_db* db, int32_t npair) {
     return n;
 }
 
+// ... or, under affine gaps, by 3-wave groups (InterArgs::blk_tri): a query
+// of P passes takes ceil(P / 3) rounds instead of ceil(P / 4), no wave idle
+// in the last round, and the workgroup's fourth wave runs a single-wave
+// block (the widest singles, beside the widest groups).  Where the rounds are
+// as few as the quads' (P = 1, 2, 3, 5, 6, 9: a 375-aa query is 6 passes of
+// 64 rows) and sw_opts tri_width w > 0: the group blocks at least w wide.
+int32_t lpt_tri_blocks(const sw_db* db, int32_t npair, int passes) {
+    const int64_t wmin = db->h->opts.tri_width;
+    if (wmin <= 0 || passes <= 0 || (passes + 2) / 3 > (passes + 3) / 4) return 0;
+    int32_t n = 0;
+    while (n < npair && static_cast<int64_t>(db->h_blk_groups[n]) * swk::kGroupCols >= wmin) ++n;
+    return n;
+}
+
 // The narrowest blocks of the merged launch run by wave pairs (x2p_wg's tail
 // range): the launch's last-dispatched work is its narrowest single-wave
 // workgroups, which start together once the rest is placed, and the longest
@@ -1107,10 +1122,10 @@ double group_ticks_host(int64_t ncols, int passes, int G) {
 
 // The work table of sw_scan_lpt for this scan shape (built once, cached).
 int lpt_table(sw_db* db, int32_t qpad, int rows, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad,
-              int32_t ntail, bool affine, const int32_t** order, int* n, int32_t* npipe_out) {
+              int32_t ntail, bool affine, bool tri, const int32_t** order, int* n, int32_t* npipe_out) {
     for (const auto& t : db->lpt_tables)
         if (t.qpad == qpad && t.rows == rows && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad &&
-            t.tail == ntail && t.pipe_opt == db->h->opts.lpt_pipe && t.affine == affine) {
+            t.tail == ntail && t.pipe_opt == db->h->opts.lpt_pipe && t.affine == affine && t.tri == tri) {
             *order = t.d_order;
             *n = t.n;
             *npipe_out = t.npipe;
@@ -1121,7 +1136,10 @@ int lpt_table(sw_db* db, int32_t qpad, int rows, int32_t qpad_intra, int ri, int
     const int64_t nb = db->nblocks;
     const int64_t pwg = nquad + (npair - nquad + 1) / 2;
     const int64_t tail = nb - ntail;  // blocks [tail, nb) by pairs
-    const int64_t swg = (tail - npair + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
+    // tris: the spare wave of tri workgroup g runs single block npair + g
+    const int64_t nspare = tri ? std::max<int64_t>(0, std::min<int64_t>(nquad, tail - npair)) : 0;
+    const int64_t s0 = npair + nspare;  // the single-wave workgroups' first block
+    const int64_t swg = (tail - s0 + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
     const int64_t twg = (ntail + 1) / 2;
     const int64_t npairs = (db->nlong + 1) / 2;
     const int64_t iwg = (npairs + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
@@ -1130,7 +1148,11 @@ int lpt_table(sw_db* db, int32_t qpad, int rows, int32_t qpad_intra, int ri, int
     std::vector<std::pair<double, int32_t>> w;
     w.reserve(static_cast<size_t>(pwg + swg + twg + iwg));
     auto width = [&](int64_t b) { return static_cast<int64_t>(db->h_blk_groups[b]) * swk::kGroupCols; };
-    for (int64_t g = 0; g < nquad; ++g) w.emplace_back(group_ticks_host(width(g), passes, 4) * tick_us, g);
+    for (int64_t g = 0; g < nquad; ++g) {
+        double c = group_ticks_host(width(g), passes, tri ? 3 : 4);
+        if (g < nspare) c = std::max(c, single_ticks(width(npair + g), passes));
+        w.emplace_back(c * tick_us, g);
+    }
     for (int64_t g = nquad; g < pwg; ++g) {
         double c = 0;
         for (int q = 0; q < 2; ++q) {
@@ -1140,7 +1162,7 @@ int lpt_table(sw_db* db, int32_t qpad, int rows, int32_t qpad_intra, int ri, int
         w.emplace_back(c * tick_us, static_cast<int32_t>(g));
     }
     for (int64_t g = 0; g < swg; ++g)  // widest first: the workgroup's first block bounds it
-        w.emplace_back(single_ticks(width(npair + g * swk::kWavesPerWG), passes) * tick_us,
+        w.emplace_back(single_ticks(width(s0 + g * swk::kWavesPerWG), passes) * tick_us,
                        static_cast<int32_t>(pwg + g));
     for (int64_t g = 0; g < twg; ++g) {  // tail pairs: the first block of two is the wider
         w.emplace_back(group_ticks_host(width(tail + 2 * g), passes, 2) * tick_us,
@@ -1183,7 +1205,7 @@ int lpt_table(sw_db* db, int32_t qpad, int rows, int32_t qpad_intra, int ri, int
         ord[k] = w[k].second;
         cost[k] = static_cast<float>(w[k].first);
     }
-    sw_db::LptTable t{qpad, rows, qpad_intra, ri, npair, nquad, ntail, static_cast<int32_t>(ord.size()), affine,
+    sw_db::LptTable t{qpad, rows, qpad_intra, ri, npair, nquad, ntail, static_cast<int32_t>(ord.size()), affine, tri,
                       static_cast<int32_t>(npipe), db->h->opts.lpt_pipe, nullptr, cost};
     HIPCHECK(hipMalloc(reinterpret_cast<void**>(&t.d_order), ord.size() * sizeof(int32_t)));
     HIPCHECK(hipMemcpy(t.d_order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -1850,6 +1872,7 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
         }
         MARK(6, h->stream);
         int32_t ntail = 0;  // merged launch: the narrowest blocks by pairs
+        int32_t ntri = 0;   // ... and the widest by 3-wave groups
         if (lpt) {
             // one launch: the inter groups + single waves and the long
             // subjects' fp16 pass, longest work first; then the long
@@ -1858,13 +1881,15 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
             a.blk_first = npair;
             const int32_t* order = nullptr;
             int nwg = 0;
-            const int32_t nquad = lpt_quad_blocks(db, npair);
+            ntri = affine ? lpt_tri_blocks(db, npair, qpad_inter / lpt_rows) : 0;
+            const int32_t nquad = ntri ? ntri : lpt_quad_blocks(db, npair);
             a.blk_quad = nquad;
+            a.blk_tri = ntri ? 1 : 0;
             ntail = lpt_tail_blocks(db, npair, qpad_inter / lpt_rows);
             a.blk_tail = static_cast<int32_t>(db->nblocks) - ntail;
             int32_t npipe = 0;
-            if ((rc = lpt_table(db, qpad_inter, lpt_rows, qpad_intra2, ri2, npair, nquad, ntail, affine, &order, &nwg,
-                                &npipe)))
+            if ((rc = lpt_table(db, qpad_inter, lpt_rows, qpad_intra2, ri2, npair, nquad, ntail, affine, ntri != 0,
+                                &order, &nwg, &npipe)))
                 return rc;
             lpt_intra.pipe_pairs = npipe;
             const swk::DrainArgs* dargs = nullptr;
@@ -1911,7 +1936,8 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
                 const std::vector<uint64_t> key = {
                     reinterpret_cast<uint64_t>(P.dev), P.off8, P.off16, P.intra_off, static_cast<uint64_t>(par),
                     reinterpret_cast<uint64_t>(scores_dev), static_cast<uint64_t>(qlen), skey,
-                    static_cast<uint64_t>(npair), static_cast<uint64_t>(nquad) | static_cast<uint64_t>(ntail) << 32,
+                    static_cast<uint64_t>(npair) | static_cast<uint64_t>(a.blk_tri) << 32,
+                    static_cast<uint64_t>(nquad) | static_cast<uint64_t>(ntail) << 32,
                     static_cast<uint64_t>(P.stride),
                     reinterpret_cast<uint64_t>(a.trace),
                     static_cast<uint64_t>(ri2) | static_cast<uint64_t>(lpt_rows) << 16 |
@@ -1937,6 +1963,7 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
         if (lpt && lpt_rows == 96) h->last_kernel.replace(h->last_kernel.find("<32,"), 4, "<48,");  // 48-row strips
         if (nr) h->last_kernel += "+int16[0," + std::to_string(nr) + ")";
         if (ntail) h->last_kernel += "+tail" + std::to_string(ntail);
+        if (ntri) h->last_kernel += "+tri" + std::to_string(ntri);
         if (lpt) h->last_kernel += drain ? "+lpt+drain" : "+lpt";
         if (!lpt) MARK(7, h->stream);
         ++h->launches;
@@ -2235,6 +2262,7 @@ int sw_opts_from_env(sw_opts* o) {
                 {"SW_TAIL_PAIRS", &o->tail_pairs},
                 {"SW_LPT_PERSIST", &o->lpt_persist},
                 {"SW_LPT_ROWS", &o->lpt_rows},
+                {"SW_TRI_WIDTH", &o->tri_width},
                 {"SW_DRAIN_SPIN", &o->drain_spin}};
     for (const auto& k : ints)
         if (const char* e = std::getenv(k.name); e && e[0]) *k.field = std::atoi(e);

@@ -953,18 +953,28 @@ __device__ __forceinline__ bool x2p_wg(const InterArgs& a, int wgi, int quad_end
     // MERGED: blocks [npair, tail) one per wave, then the narrowest blocks
     // [tail, nblocks) by pairs again (the launch's last-dispatched work)
     const int tail = MERGED && a.blk_tail > npair && a.blk_tail < a.nblocks ? a.blk_tail : a.nblocks;
-    const int twg = pwg + (tail - npair + kWavesPerWG - 1) / kWavesPerWG;  // first tail-pair workgroup
+    // 3-wave groups (MERGED, affine gaps, a.blk_tri) instead of quads over
+    // [blk_base, qend): a 6-pass block takes two rounds of three passes, no
+    // wave idle in the second, and the workgroup's fourth wave (the spare)
+    // runs single-wave block npair + wgi — the widest singles beside the
+    // widest groups; the single-wave range then starts after them (s0)
+    const bool tri_on = MERGED && GMAX == 4 && AFFINE && a.blk_tri != 0;
+    const int nspare = tri_on ? max(0, min(qwg, tail - npair)) : 0;
+    const int s0 = npair + nspare;
+    const int twg = pwg + (tail - s0 + kWavesPerWG - 1) / kWavesPerWG;  // first tail-pair workgroup
     const bool tailp = MERGED && wgi >= twg;               // workgroup-uniform
     if (MERGED && wgi >= pwg && !tailp) {
-        const int blk = npair + (wgi - pwg) * kWavesPerWG + wave;
+        const int blk = s0 + (wgi - pwg) * kWavesPerWG + wave;
         // workgroup-uniform branch: no barrier below is skipped by part of it
         return blk < tail && x2s_block<R, SG, AFFINE, F16, kSingleCR>(a, blk, lds[wave], lane);
     }
     const bool quad = !tailp && wgi < qwg;                 // workgroup-uniform
-    const int G = quad ? 4 : 2, NG = kWavesPerWG / G;
+    const bool tri = tri_on && quad;                       // workgroup-uniform
+    const bool spare = tri && wave == kWavesPerWG - 1;     // wave-uniform
+    const int G = tri ? 3 : quad ? 4 : 2, NG = tri ? 1 : kWavesPerWG / G;
     const int first = quad ? a.blk_base + wgi : tailp ? tail + (wgi - twg) * 2 : qend + (wgi - qwg) * 2;
     const int gend = tailp ? a.nblocks : npair;            // this workgroup's range end
-    const int gi = wave / G, w = wave % G;
+    const int gi = spare ? 0 : wave / G, w = spare ? 0 : wave % G;
     const int passes = (a.qpad + 2 * R - 1) / (2 * R);
     // the workgroup's clock runs to the longest of its blocks
     int tmax = 0;  // (the tick form only)
@@ -982,7 +992,11 @@ __device__ __forceinline__ bool x2p_wg(const InterArgs& a, int wgi, int quad_end
         if (tid < kWavesPerWG) sm.prog[tid] = 0;
         __syncthreads();
     }
-    if (blk < gend) {
+    bool flagged = false;
+    if (spare) {
+        const int sb = npair + wgi;  // (x2s_block synchronises with no other wave)
+        if (sb < s0) flagged = x2s_block<R, SG, AFFINE, F16, kSingleCR>(a, sb, lds[wave], lane);
+    } else if (blk < gend) {
         const uint32_t ncols = block_cols(a, blk);
         const uint64_t base = a.blk_off[blk] + static_cast<uint64_t>(lane) * kGroupCols;
         const int per = max(static_cast<int>(ncols) / SG + 1, G * kPairLag);
@@ -1015,10 +1029,9 @@ __device__ __forceinline__ bool x2p_wg(const InterArgs& a, int wgi, int quad_end
             ++tick;
         }
     }
-    if (blk < gend && w > 0) part[wave][lane] = P::bits(best.value(a));
+    if (!spare && blk < gend && w > 0) part[wave][lane] = P::bits(best.value(a));
     __syncthreads();
-    bool flagged = false;
-    if (blk < gend && w == 0) {
+    if (!spare && blk < gend && w == 0) {
         V b = best.value(a);
         for (int u = 1; u < G; ++u) {
             const V o = P::from(part[wave + u][lane]);
@@ -1026,7 +1039,7 @@ __device__ __forceinline__ bool x2p_wg(const InterArgs& a, int wgi, int quad_end
             else b = max2(b, o);
         }
         flagged = x2s_finish<F16>(a, blk, lane, b);
-        trace_block(a, blk, t0, lane, quad ? 4 : 1);
+        trace_block(a, blk, t0, lane, tri ? 3 : quad ? 4 : 1);
     }
     return flagged;
 }

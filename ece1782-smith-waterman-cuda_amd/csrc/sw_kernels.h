@@ -114,8 +114,11 @@ struct InterArgs {
     // sw_inter_x2p: its pair blocks are [blk_base, blk_first) (merged) or
     // [blk_base, nblocks); blocks below blk_base run elsewhere
     int32_t blk_base;
-    // sw_scan_lpt: blocks [blk_base, blk_quad) run by wave quads
+    // sw_scan_lpt: blocks [blk_base, blk_quad) run by wave quads, or (affine
+    // gaps, blk_tri != 0) by 3-wave groups whose workgroup's fourth wave runs
+    // a single-wave block
     int32_t blk_quad;
+    int32_t blk_tri;
     // sw_scan_lpt: blocks [blk_tail, nblocks) (the narrowest) run by wave
     // pairs after the single-wave range (0 or nblocks: none)
     int32_t blk_tail;

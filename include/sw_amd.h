@@ -188,6 +188,11 @@ typedef struct sw_opts {
                                  workgroups (tests)                           SW_LPT_PERSIST */
     int32_t lpt_rows;         /* query rows per pass of the merged launch under
                                  linear gaps: 64 or 96 (default 96)           SW_LPT_ROWS */
+    int32_t tri_width;        /* under affine gaps, the merged launch's widest group
+                                 blocks at least this wide run by 3-wave groups
+                                 (two rounds of a 6-pass query, no idle wave),
+                                 whose workgroup's fourth wave runs a single-wave
+                                 block, instead of quads (0: quads)          SW_TRI_WIDTH */
     int32_t drain_spin;       /* (tests) polls the merged launch's drain spends
                                  waiting for a claimed rescue-list entry before
                                  it gives up and faults (default 2^22; 0: at

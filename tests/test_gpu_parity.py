@@ -654,6 +654,39 @@ def test_merged_lpt_launch(sw, oracle, handle, knobs, quad_width, pipe, scoring)
         knobs(lpt="1")
 
 
+@pytest.mark.parametrize("tri_width", ["16", "200", "450"])
+@pytest.mark.parametrize("scoring", [(1, 12, 1), (0, 13, 3), (0, 2, 2)])
+def test_tri_groups(sw, oracle, handle, knobs, tri_width, scoring):
+    """The merged launch's 3-wave groups (sw_opts tri_width; affine gaps,
+    queries of 3, 5 or 6 passes of 64 rows): every group block, the widest
+    ones or a few as tris, each workgroup's fourth wave on a single-wave
+    block (more tris than singles included: 2,500 subjects, pair width 64),
+    planted near-copies rescued inside the launch, against the oracle and
+    the two-launch form; other pass counts and linear gaps keep the quads."""
+    mid, go, ge = scoring
+    knobs(lpt="1", tri_width=tri_width, pair_width="64", inter_i16_span="0", intra_i16_first="0")
+    r, o = sw.synth.database(2500, shard=29)
+    q0 = sw.synth.query(500, shard=9)
+    extra = [q0, q0[:300], np.concatenate([q0, q0])]
+    r2 = np.concatenate([r] + extra)
+    o2 = np.concatenate([o, o[-1] + np.cumsum([len(x) for x in extra])])
+    db = sw.Database(handle, r2, o2, long_threshold=700)
+    m = sw.capi.builtin_matrix(mid)
+    for qlen in (150, 300, 375, 500):
+        q = q0[:qlen]
+        got = db.scan(q, m, go, ge)
+        passes = -(-qlen // 64)
+        tri = go != ge and -(-passes // 3) <= -(-passes // 4)
+        assert ("+tri" in handle.last_kernel()) == tri, (qlen, handle.last_kernel())
+        want = oracle.scan(q, r2, o2, mat=m, gap_open=go, gap_extend=ge)
+        assert np.array_equal(got, want), (qlen, np.nonzero(got != want)[0][:10])
+        assert np.array_equal(db.scan(q, m, go, ge), want)  # the cached table, twice
+        knobs(lpt="0")
+        assert np.array_equal(db.scan(q, m, go, ge), want)
+        knobs(lpt="1")
+    db.close()
+
+
 @pytest.mark.parametrize("ri", ["4", "8"])
 @pytest.mark.parametrize("scoring", [(0, 2, 2), (0, 12, 1)])
 def test_merged_launch_drains_rescue_lists(sw, oracle, handle, knobs, ri, scoring):
