@@ -1065,11 +1065,23 @@ int32_t lpt_quad_blocks(const sw_db* db, int32_t npair) {
 // ... or, under affine gaps, by 3-wave groups (InterArgs::blk_tri): a query
 // of P passes takes ceil(P / 3) rounds instead of ceil(P / 4), no wave idle
 // in the last round, and the workgroup's fourth wave runs a single-wave
-// block (the widest singles, beside the widest groups).  Where the rounds are
-// as few as the quads' (P = 1, 2, 3, 5, 6, 9: a 375-aa query is 6 passes of
-// 64 rows) and sw_opts tri_width w > 0: the group blocks at least w wide.
+// block (the widest singles, beside the widest groups) — used where the
+// rounds are as few as the quads' (P = 1, 2, 3, 5, 6, 9: a 375-aa query is 6
+// passes of 64 rows), for the group blocks at least kTriFrac x the long
+// threshold wide (sw_opts tri_width w: at least w columns; 0: none), on the
+// databases that run quads.  Measured on C2's shares (profiles/r06_tri/):
+// the 1/8 share's slowest rank 8,551 -> 9,001 GCUPS at 430 of its 891 (the
+// widest pair blocks, the launch's critical path, take two rounds of a tri
+// instead of three of a pair: -32 % latency at the same wave time, the
+// spare wave doing work a single-wave workgroup would); 350-460 all +3 to +5
+// %; the 1/4 share +0.7 % at 700 (-0.3 % at 530), the 1/2 share -0.4 % at
+// 1,300 and worse below, C2 -1.3 % at 1,500 and worse below.
+constexpr double kTriFrac = 0.48;
+
 int32_t lpt_tri_blocks(const sw_db* db, int32_t npair, int passes) {
-    const int64_t wmin = db->h->opts.tri_width;
+    int64_t wmin = static_cast<double>(db->n) < kQuadMaxFill * kFillSubjects
+                       ? static_cast<int64_t>(kTriFrac * db->long_threshold) : 0;
+    if (db->h->opts.tri_width >= 0) wmin = db->h->opts.tri_width;
     if (wmin <= 0 || passes <= 0 || (passes + 2) / 3 > (passes + 3) / 4) return 0;
     int32_t n = 0;
     while (n < npair && static_cast<int64_t>(db->h_blk_groups[n]) * swk::kGroupCols >= wmin) ++n;

@@ -192,7 +192,9 @@ typedef struct sw_opts {
                                  blocks at least this wide run by 3-wave groups
                                  (two rounds of a 6-pass query, no idle wave),
                                  whose workgroup's fourth wave runs a single-wave
-                                 block, instead of quads (0: quads)          SW_TRI_WIDTH */
+                                 block, instead of quads (0: none; default
+                                 0.48 x the long threshold on databases that run
+                                 quads)                                      SW_TRI_WIDTH */
     int32_t drain_spin;       /* (tests) polls the merged launch's drain spends
                                  waiting for a claimed rescue-list entry before
                                  it gives up and faults (default 2^22; 0: at

@@ -633,7 +633,7 @@ def test_merged_lpt_launch(sw, oracle, handle, knobs, quad_width, pipe, scoring)
     mid, go, ge = scoring
     knobs(lpt="1")
     knobs(lpt_pipe=pipe)
-    knobs(quad_width=quad_width)
+    knobs(quad_width=quad_width, tri_width="0")  # (3-wave groups: test_tri_groups)
     knobs(pair_width="64")
     r, o = sw.synth.database(2500, shard=23)
     q0 = sw.synth.query(500, shard=8)
