@@ -13,8 +13,8 @@ cp pmc_traffic.json $O/pmc_traffic.json
 B="bench.py --no-cpu-baseline --no-verify --no-reference-scoring --sustained-seconds 0"
 csvdir() { dirname $(find $1 -name run_counter_collection.csv); }
 for c in ${CFGS:-c2 c5 c3}; do
-  # NS: scans per profiled run when the dominant work is a family of kernels (C3: 2 batches x 20 queries)
-  case $c in c2) a="" ; s="--steps 3 --warmup 1" ; NS=0 ;; c5) a="--config c5" ; s="--steps 3 --warmup 1" ; NS=0 ;; c3) a="--config c3" ; s="--steps 1 --warmup 1" ; NS=40 ;; esac
+  # NS: scans per profiled run when the dominant work is a family of kernels (C3: 20 queries x 5 steps: the cold first step, 1 warm-up, 1 timed, the two cold/warm steps)
+  case $c in c2) a="" ; s="--steps 3 --warmup 1" ; NS=0 ;; c5) a="--config c5" ; s="--steps 3 --warmup 1" ; NS=0 ;; c3) a="--config c3" ; s="--steps 1 --warmup 1" ; NS=100 ;; esac
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_$c -o run --output-format csv -- python3 $B $a $s > $O/kt_$c.json 2> $O/kt_$c.err || { echo "TRACE $c FAILED"; tail -5 $O/kt_$c.err; exit 1; }
   KN=$(python3 -c "
 import csv,sys
