@@ -69,7 +69,7 @@ class Opts(ctypes.Structure):
     is listed there."""
     INT_FIELDS = ("lpt", "lpt_pipe", "quad_width", "pair_width", "pair_group", "coop_width", "coop_skew",
                   "intra_x2", "intra_x2_rows", "intra_i16_first", "inter_i16_span", "int16_guard",
-                  "rescue_stats", "tail_pairs", "lpt_persist", "lpt_rows", "tri_width", "drain_spin")
+                  "rescue_stats", "tail_pairs", "lpt_persist", "lpt_rows", "tri_width", "lpt_pipe_tail", "drain_spin")
     _fields_ = [("size", ctypes.c_int32)] + [(f, ctypes.c_int32) for f in INT_FIELDS] + \
         [("inter_variant", ctypes.c_char * 16), ("trace_file", ctypes.c_char * 256)]
 

@@ -230,7 +230,7 @@ sw_opts default_opts() {
     for (int32_t* f : {&o.lpt, &o.lpt_pipe, &o.quad_width, &o.pair_width, &o.pair_group, &o.coop_width,
                        &o.coop_skew, &o.intra_x2, &o.intra_x2_rows, &o.intra_i16_first, &o.inter_i16_span,
                        &o.int16_guard, &o.rescue_stats, &o.tail_pairs, &o.lpt_persist, &o.lpt_rows,
-                       &o.tri_width, &o.drain_spin})
+                       &o.tri_width, &o.lpt_pipe_tail, &o.drain_spin})
         *f = -1;
     return o;
 }
@@ -415,6 +415,8 @@ struct sw_db {
         bool tri;  // the group blocks by 3-wave groups with a spare wave (InterArgs::blk_tri)
         int32_t npipe;  // the longest pairs, in the pipelined form
         int32_t pipe_opt;  // sw_opts lpt_pipe the table was built under
+        int32_t pipe_tail;  // pairs [pipe_tail, ...) pipelined too (the shortest)
+        int32_t tail_opt;   // sw_opts lpt_pipe_tail the table was built under
         int32_t* d_order;
         std::vector<float> cost;  // estimated duration of each entry, longest first
     };
@@ -1134,13 +1136,16 @@ double group_ticks_host(int64_t ncols, int passes, int G) {
 
 // The work table of sw_scan_lpt for this scan shape (built once, cached).
 int lpt_table(sw_db* db, int32_t qpad, int rows, int32_t qpad_intra, int ri, int32_t npair, int32_t nquad,
-              int32_t ntail, bool affine, bool tri, const int32_t** order, int* n, int32_t* npipe_out) {
+              int32_t ntail, bool affine, bool tri, const int32_t** order, int* n, int32_t* npipe_out,
+              int32_t* pipe_tail_out) {
     for (const auto& t : db->lpt_tables)
         if (t.qpad == qpad && t.rows == rows && t.qpad_intra == qpad_intra && t.ri == ri && t.npair == npair && t.group == nquad &&
-            t.tail == ntail && t.pipe_opt == db->h->opts.lpt_pipe && t.affine == affine && t.tri == tri) {
+            t.tail == ntail && t.pipe_opt == db->h->opts.lpt_pipe && t.affine == affine && t.tri == tri &&
+            t.tail_opt == db->h->opts.lpt_pipe_tail) {
             *order = t.d_order;
             *n = t.n;
             *npipe_out = t.npipe;
+            *pipe_tail_out = t.pipe_tail;
             return SW_OK;
         }
     const int passes = qpad / rows;
@@ -1199,15 +1204,27 @@ int lpt_table(sw_db* db, int32_t qpad, int rows, int32_t qpad_intra, int ri, int
             while (npipe < std::min<int64_t>(npairs, 4) && pair_us(npipe) > inter_max) ++npipe;
     }
     npipe = std::min(npipe, npairs);
+    // The SHORTEST pairs in the pipelined form too (sw_opts lpt_pipe_tail n:
+    // the last n pairs): the table ends with them, when the grid's slots
+    // empty, and the pipeline cuts their latency to (length + 63 + 128
+    // (chunks - 1)) steps of 2 rows per lane instead of (length + 63) of RI
+    int64_t ntp = 0;
+    if (nchp <= swk::kWavesPerWG && db->h->opts.lpt_pipe_tail > 0) ntp = db->h->opts.lpt_pipe_tail;
+    ntp = std::max<int64_t>(0, std::min(ntp, npairs - npipe));
+    const int64_t pipe_tail = npairs - ntp;
     const int64_t npipe_wg = npipe / swk::kWavesPerWG;  // ordinary workgroups left with no pair
     for (int64_t g = npipe_wg; g < iwg; ++g) {
         const int64_t first = std::max<int64_t>(8 * g, 2 * npipe);  // its longest subject not pipelined
-        if (first >= db->nlong) continue;
+        if (first >= db->nlong || first >= 2 * pipe_tail) continue;
         w.emplace_back((db->h_llen[static_cast<size_t>(first)] + swk::kLanes - 1) * nch * step_us,
                        static_cast<int32_t>(-1 - g));
     }
     // (sw_scan_lpt item -1 - (iwg + pair)), ahead of everything
     for (int64_t p = 0; p < npipe; ++p) w.emplace_back(1e30 - p, static_cast<int32_t>(-1 - (iwg + p)));
+    const double pstep_us = intra_step_us(2);
+    for (int64_t p = pipe_tail; p < npairs; ++p)
+        w.emplace_back((db->h_llen[static_cast<size_t>(2 * p)] + swk::kLanes - 1 + 128.0 * (nchp - 1)) * pstep_us,
+                       static_cast<int32_t>(-1 - (iwg + p)));
     std::stable_sort(w.begin(), w.end(), [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) {
         return x.first > y.first;
     });
@@ -1218,7 +1235,8 @@ int lpt_table(sw_db* db, int32_t qpad, int rows, int32_t qpad_intra, int ri, int
         cost[k] = static_cast<float>(w[k].first);
     }
     sw_db::LptTable t{qpad, rows, qpad_intra, ri, npair, nquad, ntail, static_cast<int32_t>(ord.size()), affine, tri,
-                      static_cast<int32_t>(npipe), db->h->opts.lpt_pipe, nullptr, cost};
+                      static_cast<int32_t>(npipe), db->h->opts.lpt_pipe, static_cast<int32_t>(pipe_tail),
+                      db->h->opts.lpt_pipe_tail, nullptr, cost};
     HIPCHECK(hipMalloc(reinterpret_cast<void**>(&t.d_order), ord.size() * sizeof(int32_t)));
     HIPCHECK(hipMemcpy(t.d_order, ord.data(), ord.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     db->device_bytes += ord.size() * sizeof(int32_t);
@@ -1230,6 +1248,7 @@ int lpt_table(sw_db* db, int32_t qpad, int rows, int32_t qpad_intra, int ri, int
     *order = t.d_order;
     *n = t.n;
     *npipe_out = t.npipe;
+    *pipe_tail_out = t.pipe_tail;
     return SW_OK;
 }
 
@@ -1899,11 +1918,12 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
             a.blk_tri = ntri ? 1 : 0;
             ntail = lpt_tail_blocks(db, npair, qpad_inter / lpt_rows);
             a.blk_tail = static_cast<int32_t>(db->nblocks) - ntail;
-            int32_t npipe = 0;
+            int32_t npipe = 0, pipe_tail = 0;
             if ((rc = lpt_table(db, qpad_inter, lpt_rows, qpad_intra2, ri2, npair, nquad, ntail, affine, ntri != 0,
-                                &order, &nwg, &npipe)))
+                                &order, &nwg, &npipe, &pipe_tail)))
                 return rc;
             lpt_intra.pipe_pairs = npipe;
+            lpt_intra.pipe_tail = pipe_tail;
             const swk::DrainArgs* dargs = nullptr;
             if (drain) {
                 // the four rescue stages of launch_inter_tail / launch_intra_tail,
@@ -1954,6 +1974,7 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
                     reinterpret_cast<uint64_t>(a.trace),
                     static_cast<uint64_t>(ri2) | static_cast<uint64_t>(lpt_rows) << 16 |
                         static_cast<uint64_t>(npipe) << 32,
+                    static_cast<uint64_t>(static_cast<uint32_t>(pipe_tail)),
                     static_cast<uint64_t>(static_cast<uint32_t>(d.spin))};
                 if ((rc = drain_blob(db, h->stream, key, d, &dargs))) return rc;
             }
@@ -2275,6 +2296,7 @@ int sw_opts_from_env(sw_opts* o) {
                 {"SW_LPT_PERSIST", &o->lpt_persist},
                 {"SW_LPT_ROWS", &o->lpt_rows},
                 {"SW_TRI_WIDTH", &o->tri_width},
+                {"SW_LPT_PIPE_TAIL", &o->lpt_pipe_tail},
                 {"SW_DRAIN_SPIN", &o->drain_spin}};
     for (const auto& k : ints)
         if (const char* e = std::getenv(k.name); e && e[0]) *k.field = std::atoi(e);

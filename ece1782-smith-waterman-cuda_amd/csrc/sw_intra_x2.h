@@ -236,7 +236,7 @@ __device__ __forceinline__ bool intra_x2_wg(const IntraArgs& a, int wgi, typenam
     const int p = PIPE ? wgi : wgi * kWavesPerWG + wave;  // subject pair
     int sa = 2 * p, sb = 2 * p + 1;
     // (pairs the merged launch runs in the pipelined form are skipped here)
-    const bool skip = !PIPE && !LIST && p < a.pipe_pairs;
+    const bool skip = !PIPE && !LIST && (p < a.pipe_pairs || p >= a.pipe_tail);
     bool hasA = !skip && sa < a.nsubj, hasB = !skip && sb < a.nsubj;
     if constexpr (LIST) {
         const int n = __builtin_amdgcn_readfirstlane(*a.list_count);

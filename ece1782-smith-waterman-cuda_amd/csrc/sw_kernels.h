@@ -162,6 +162,9 @@ struct IntraArgs {
     // sw_scan_lpt: pairs [0, pipe_pairs) run in the pipelined form; the
     // launch's ordinary intra workgroups skip them
     int32_t pipe_pairs = 0;
+    // ... and pairs [pipe_tail, ...) too (the launch's last items: the
+    // shortest long subjects, whose latency the pipeline cuts at the end)
+    int32_t pipe_tail = 0x7fffffff;
 };
 
 // ---- device-side rescue lists: [count, item 0, item 1, ...] --------------

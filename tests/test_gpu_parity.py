@@ -654,6 +654,34 @@ def test_merged_lpt_launch(sw, oracle, handle, knobs, quad_width, pipe, scoring)
         knobs(lpt="1")
 
 
+@pytest.mark.parametrize("tail", ["1", "37", "100000"])
+@pytest.mark.parametrize("scoring", [(1, 12, 1), (0, 2, 2)])
+def test_tail_pipelined_pairs(sw, oracle, handle, knobs, tail, scoring):
+    """The merged launch's last long-subject pairs in the pipelined form too
+    (sw_opts lpt_pipe_tail: one, some, every pair; with the longest pairs
+    pipelined as well, and without): every pair is scored exactly once,
+    planted copies rescued in the launch, against the oracle."""
+    mid, go, ge = scoring
+    knobs(lpt="1", lpt_pipe_tail=tail, pair_width="64", inter_i16_span="0", intra_i16_first="0")
+    r, o = sw.synth.database(2500, shard=31)
+    q0 = sw.synth.query(500, shard=10)
+    extra = [np.concatenate([q0, q0]), q0[:300], np.concatenate([q0[:400], q0[:400]])]
+    r2 = np.concatenate([r] + extra)
+    o2 = np.concatenate([o, o[-1] + np.cumsum([len(x) for x in extra])])
+    db = sw.Database(handle, r2, o2, long_threshold=700)
+    m = sw.capi.builtin_matrix(mid)
+    for pipe in ("0", "3"):
+        knobs(lpt_pipe=pipe)
+        for qlen in (200, 375, 500):
+            q = q0[:qlen]
+            want = oracle.scan(q, r2, o2, mat=m, gap_open=go, gap_extend=ge)
+            for _ in range(2):
+                got = db.scan(q, m, go, ge)
+                assert "+lpt" in handle.last_kernel(), handle.last_kernel()
+                assert np.array_equal(got, want), (pipe, qlen, np.nonzero(got != want)[0][:10])
+    db.close()
+
+
 @pytest.mark.parametrize("tri_width", ["16", "200", "450"])
 @pytest.mark.parametrize("scoring", [(1, 12, 1), (0, 13, 3), (0, 2, 2)])
 def test_tri_groups(sw, oracle, handle, knobs, tri_width, scoring):

@@ -13,7 +13,8 @@ ENV = {"lpt": "SW_LPT", "lpt_pipe": "SW_LPT_PIPE", "quad_width": "SW_QUAD_WIDTH"
        "intra_x2": "SW_INTRA_X2", "intra_x2_rows": "SW_INTRA_X2_RI", "intra_i16_first": "SW_INTRA_I16_FIRST",
        "inter_i16_span": "SW_INTER_I16_SPAN", "int16_guard": "SW_INT16_GUARD", "rescue_stats": "SW_RESCUE_STATS",
        "tail_pairs": "SW_TAIL_PAIRS", "lpt_persist": "SW_LPT_PERSIST",
-       "lpt_rows": "SW_LPT_ROWS", "tri_width": "SW_TRI_WIDTH", "drain_spin": "SW_DRAIN_SPIN"}
+       "lpt_rows": "SW_LPT_ROWS", "tri_width": "SW_TRI_WIDTH",
+       "lpt_pipe_tail": "SW_LPT_PIPE_TAIL", "drain_spin": "SW_DRAIN_SPIN"}
 
 
 def test_init_is_all_auto_and_sized(sw):
