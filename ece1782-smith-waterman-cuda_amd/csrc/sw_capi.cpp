@@ -1207,9 +1207,17 @@ int lpt_table(sw_db* db, int32_t qpad, int rows, int32_t qpad_intra, int ri, int
     // The SHORTEST pairs in the pipelined form too (sw_opts lpt_pipe_tail n:
     // the last n pairs): the table ends with them, when the grid's slots
     // empty, and the pipeline cuts their latency to (length + 63 + 128
-    // (chunks - 1)) steps of 2 rows per lane instead of (length + 63) of RI
+    // (chunks - 1)) steps of 2 rows per lane instead of (length + 63) of RI.
+    // Default: 2 % of the pairs (to a multiple of 8) for linear scans of the
+    // databases that run quads — measured on C2's 1/8 share under the
+    // reference scoring (profiles/r06_tailpipe/): 12,794 / 12,802 / 12,803
+    // -> 13,011 / 13,027 / 13,011 GCUPS with the last 32 of 1,561 pairs (16:
+    // 13,018; 8, 24, 48, 64: 12,831, 12,879, 12,694, 12,772; 128 and more:
+    // slower), affine scans within noise (their end is the tri groups').
     int64_t ntp = 0;
-    if (nchp <= swk::kWavesPerWG && db->h->opts.lpt_pipe_tail > 0) ntp = db->h->opts.lpt_pipe_tail;
+    if (db->h->opts.lpt_pipe_tail >= 0) ntp = db->h->opts.lpt_pipe_tail;
+    else if (!affine && static_cast<double>(db->n) < kQuadMaxFill * kFillSubjects) ntp = (npairs * 2 / 100 + 4) / 8 * 8;
+    if (nchp > swk::kWavesPerWG) ntp = 0;
     ntp = std::max<int64_t>(0, std::min(ntp, npairs - npipe));
     const int64_t pipe_tail = npairs - ntp;
     const int64_t npipe_wg = npipe / swk::kWavesPerWG;  // ordinary workgroups left with no pair

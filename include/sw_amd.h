@@ -197,7 +197,8 @@ typedef struct sw_opts {
                                  quads)                                      SW_TRI_WIDTH */
     int32_t lpt_pipe_tail;    /* the last n long-subject pairs of the merged
                                  launch (the shortest) run in the pipelined form
-                                 too (0: none)                               SW_LPT_PIPE_TAIL */
+                                 too (0: none; default: 2 % of the pairs for
+                                 linear scans of databases that run quads)   SW_LPT_PIPE_TAIL */
     int32_t drain_spin;       /* (tests) polls the merged launch's drain spends
                                  waiting for a claimed rescue-list entry before
                                  it gives up and faults (default 2^22; 0: at
