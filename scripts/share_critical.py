@@ -1,6 +1,6 @@
 """Critical path of a merged launch from an exp_share_dump.py trace (.npz):
 slot-time by item kind (inter / intra workgroups), each inter form's block
-widths and durations (4 = quads, 1 = pairs, 0 = single waves), when the
+widths and durations (4 = quads, 3 = tris, 1 = pairs, 0 = single waves), when the
 intra items start, workgroups in flight every 5 % of the span and the last
 entries to end.
 usage: share_critical.py TRACE.npz"""
@@ -34,7 +34,7 @@ def main(path):
     inter_lens = z["lens"][int(z["n_long"]):]
     width = np.array([inter_lens[i * 64] for i in range(nb)])
     forms = {}
-    for kd, name in ((4, "quads"), (1, "pairs"), (0, "single")):
+    for kd, name in ((4, "quads"), (3, "tris"), (1, "pairs"), (0, "single")):
         m = okb & (bk == kd)
         if m.any():
             forms[name] = {"blocks": int(m.sum()), "width_min_max": [int(width[m].min()), int(width[m].max())],
