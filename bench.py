@@ -109,7 +109,7 @@ C3_QUERIES = ["P02232", "P05013", "P14942", "P07327", "P01008", "P03435", "P4235
 # sources whose change can change the dominant kernel's HBM traffic: a stored
 # rocprofv3 --pmc measurement (pmc_traffic.json) is only reported for the
 # build it was taken on
-KERNEL_SOURCES = ["sw_inter_x2.hip", "sw_intra_x2.hip", "sw_intra_x2.h", "sw_int32.h", "sw_kernels.hip", "sw_kernels.h", "sw_capi.cpp"]
+KERNEL_SOURCES = ["sw_inter_x2.hip", "sw_intra_x2.hip", "sw_intra_x2.h", "sw_int32.h", "sw_kernels.hip", "sw_kernels.h", "sw_capi.cpp", "sw_plan.cpp"]
 
 
 def log(*a):
