@@ -584,6 +584,10 @@ def main():
     ap.add_argument("--shard-of", type=int, default=0,
                     help="measure one rank's share of this many GPUs on this GPU (strong-scaling rehearsal)")
     ap.add_argument("--shard-rank", type=int, default=0)
+    ap.add_argument("--rehearse-exchange", action="store_true",
+                    help="with --shard-of N: each step also runs the N-rank exchange's device work on the "
+                         "exchange stream: a one-rank RCCL all-gather of the top-K, the other N-1 rows "
+                         "copied in, and the device merge of N x K keys")
     ap.add_argument("--query", default="P07327")
     ap.add_argument("--topk", type=int, default=100)
     ap.add_argument("--matrix", default="blosum62", choices=sorted(MATRICES))
@@ -647,6 +651,8 @@ def main():
     shard_world, shard_rank = (args.shard_of, args.shard_rank) if args.shard_of else (world, rank)
     if args.shard_of and world > 1:
         raise SystemExit("--shard-of is a one-process rehearsal")
+    if args.rehearse_exchange and not args.shard_of:
+        raise SystemExit("--rehearse-exchange needs --shard-of")
     gpu = local if args.device is None else args.device
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
@@ -655,6 +661,11 @@ def main():
             tdist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         else:
             tdist.init_process_group("gloo", rank=rank, world_size=world)
+    elif args.rehearse_exchange:
+        # a one-rank RCCL communicator: the all-gather's launch and kernel on
+        # the exchange stream (the peers' transfers are not rehearsed)
+        tdist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0,
+                                 world_size=1, device_id=dev)
 
     import _swpkg
     sw = _swpkg.load()
@@ -701,7 +712,9 @@ def main():
     scores_buf = [torch.zeros((nq, max(n, 1)), dtype=torch.int32, device=dev) for _ in range(NBUF)]
     K = args.topk
     top = torch.empty((nq, K), dtype=torch.int64, device=dev)
-    gathered = torch.empty((world, nq, K), dtype=torch.int64, device=dev)
+    # rows of the gathered top-K: the ranks (or the rehearsed ranks)
+    xworld = shard_world if args.rehearse_exchange else world
+    gathered = torch.empty((xworld, nq, K), dtype=torch.int64, device=dev)
     final = torch.empty((nq, K), dtype=torch.int64, device=dev)
     gid_dev = torch.from_numpy(gids).to(dev) if id_base is None else None
 
@@ -749,9 +762,13 @@ def main():
                     parts = [torch.empty((nq, K), dtype=torch.int64) for _ in range(world)]
                     tdist.all_gather(parts, top.cpu())
                     gathered.copy_(torch.stack(parts))
+            elif args.rehearse_exchange:
+                tdist.all_gather_into_tensor(gathered[:1], top)
+                gathered[1:].copy_(top.unsqueeze(0).expand(xworld - 1, nq, K))
+            if xworld > 1:
                 for k in range(nq):
                     merged = gathered[:, k, :].contiguous()
-                    xhandle.topk_keys_device(merged.data_ptr(), world * K, K, final[k].data_ptr())
+                    xhandle.topk_keys_device(merged.data_ptr(), xworld * K, K, final[k].data_ptr())
             ranked[b].record(xstream)
 
     cells_rank = float(qtot) * residues
@@ -1004,6 +1021,10 @@ def main():
         }
         if args.shard_of:
             out["rehearsal"] = "rank %d's share of %d GPUs measured alone on one GPU" % (shard_rank, shard_world)
+            if args.rehearse_exchange:
+                out["exchange_rehearsed"] = ("each step: device top-%d, a one-rank RCCL all-gather, %d rows "
+                                             "copied in, the device merge of %d x %d keys, on the exchange "
+                                             "stream beside the next scan" % (K, shard_world - 1, shard_world, K))
         if ref is not None:
             out["reference_scoring"] = ref
         if sustained is not None:
@@ -1023,6 +1044,7 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         tdist.barrier()
+    if tdist.is_initialized():
         tdist.destroy_process_group()
     db.close()
     if xhandle is not handle:
