@@ -629,6 +629,8 @@ def main():
         if args.shard_of:
             raise SystemExit("--shard-of is a one-process rehearsal")
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.rehearse_exchange and not args.shard_of:
+        raise SystemExit("--rehearse-exchange needs --shard-of")
     if args.steps is None:
         args.steps = 3 if args.config in ("c3", "c4") else 100
     if args.warmup is None:
@@ -651,8 +653,6 @@ def main():
     shard_world, shard_rank = (args.shard_of, args.shard_rank) if args.shard_of else (world, rank)
     if args.shard_of and world > 1:
         raise SystemExit("--shard-of is a one-process rehearsal")
-    if args.rehearse_exchange and not args.shard_of:
-        raise SystemExit("--rehearse-exchange needs --shard-of")
     gpu = local if args.device is None else args.device
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)

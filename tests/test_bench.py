@@ -168,3 +168,12 @@ def test_bench_reference_scoring_parity(sw, oracle):
     bad[0, n // 2] += 1
     r2, ok2 = bench.verify(sw, sw.dist, 1, 0, [q], sampler, n, gids, bad, top, top, K, scoring, 4, 30.0, "gloo")
     assert not ok2 and not r2["scores_equal_oracle"]
+
+
+def test_bench_rehearse_exchange_needs_a_share():
+    """--rehearse-exchange rehearses the N-rank exchange beside a share's
+    scans: without --shard-of it exits non-zero before touching a GPU."""
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--rehearse-exchange"],
+                         capture_output=True, text=True, timeout=120, cwd=REPO)
+    assert out.returncode != 0 and "--rehearse-exchange needs --shard-of" in out.stderr
+    assert out.stdout.strip() == ""
