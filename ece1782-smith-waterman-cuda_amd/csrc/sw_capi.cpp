@@ -473,6 +473,90 @@ swplan::PlanDb plan_view(const sw_db* db) {
     return v;
 }
 
+// ---- adaptive routing: what earlier scans of this database observed --------
+// The intra chain's order.  Linear scoring with cheap gaps makes random
+// pairs' scores grow with their lengths, so on long subjects the fp16 pass
+// can flag many of them and its time on those is wasted.  Once a scan with
+// the same scoring (skey) has flagged over a third of the long subjects at a
+// query no longer than this one, the int16 form runs first, over all of them
+// (the int16 cell costs ~1.4x the fp16 one, so fp16 first + int16 over the
+// flagged fraction p wins while p < ~0.3).  The last observation is read
+// here once its event has completed (scan_impl_body records it).  opt =
+// sw_opts intra_i16_first: 0 / 1 never / always, else the observations.
+bool adapt_intra_i16_first(sw_db* db, uint64_t skey, int32_t qlen, int32_t opt) {
+    if (db->lcount_pending && hipEventQuery(db->lcount_ev) == hipSuccess) {
+        db->lcount_pending = false;
+        db->lcount_seen = true;
+        db->lseen_key = db->lcount_key;
+        db->lseen_qhash = db->lcount_qhash;
+        db->lseen_qlen = db->lcount_qlen;
+        if (3 * static_cast<int64_t>(*db->h_lcount) > db->nlong) {
+            bool seen = false;
+            for (auto& e : db->i16_first)
+                if (e.first == db->lcount_key) {
+                    e.second = std::min(e.second, db->lcount_qlen);
+                    seen = true;
+                }
+            if (!seen) db->i16_first.emplace_back(db->lcount_key, db->lcount_qlen);
+        }
+    }
+    bool intra_i16_first = false;
+    if (opt == 0 || opt == 1) {
+        intra_i16_first = opt == 1;
+    } else {
+        for (const auto& e : db->i16_first)
+            if (e.first == skey && e.second <= qlen) intra_i16_first = true;
+    }
+    return intra_i16_first;
+}
+
+// The same for the inter scan, per block: long queries under cheap linear
+// gaps put the WIDEST blocks (length-sorted, ids 0, 1, ...) in the fp16
+// guard band, and their re-scoring by the list kernel (one wave per block,
+// every pass in turn) takes longer than the whole scan.  A scan with the
+// same scoring whose fp16 pass flagged most of blocks [0, span) makes
+// later queries at least as long run those blocks in int16, by wave pairs
+// beside the fp16 launch.  opt = sw_opts inter_i16_span: n forces n blocks (0: off).
+int32_t adapt_inter_i16_span(sw_db* db, uint64_t skey, int32_t qlen, int32_t opt) {
+    if (db->icount_pending && hipEventQuery(db->icount_ev) == hipSuccess) {
+        db->icount_pending = false;
+        db->icount_seen = true;
+        db->seen_key = db->icount_key;
+        db->seen_qhash = db->icount_qhash;
+        db->seen_qlen = db->icount_qlen;
+        db->seen_nr = db->icount_nr;
+        const int32_t cnt = db->h_icount[0], span = db->h_icount[1] + 1;
+        // most of [nr, span) flagged: not a few high-scoring hits far out
+        if (cnt > 0 && span > db->icount_nr && 2 * static_cast<int64_t>(cnt) >= span - db->icount_nr) {
+            // keep a staircase per scoring: drop what the new observation
+            // dominates (a query at least as long with a span no larger),
+            // skip it if an existing one dominates it
+            const uint64_t k = db->icount_key;
+            const int32_t q = db->icount_qlen;
+            bool dominated = false;
+            for (const auto& e : db->i16_span)
+                if (e.key == k && e.qlen <= q && e.span >= span) dominated = true;
+            if (!dominated) {
+                db->i16_span.erase(std::remove_if(db->i16_span.begin(), db->i16_span.end(),
+                                                  [&](const sw_db::SpanObs& e) {
+                                                      return e.key == k && e.qlen >= q && e.span <= span;
+                                                  }),
+                                   db->i16_span.end());
+                db->i16_span.push_back({k, q, span});
+            }
+        }
+    }
+    int32_t i16_span = 0;
+    if (opt >= 0) {
+        i16_span = opt;
+    } else {
+        for (const auto& o : db->i16_span)
+            if (o.key == skey && o.qlen <= qlen) i16_span = std::max(i16_span, o.span);
+    }
+    i16_span = static_cast<int32_t>(std::min<int64_t>(std::max(i16_span, 0), db->nblocks));
+    return i16_span;
+}
+
 void free_dev(sw_db* db) {
     void* ptrs[] = {db->d_res, db->d_blk_off, db->d_blk_groups, db->d_blk_cols, db->d_lane_ids, db->d_bnd_h, db->d_bnd_f,
                     db->d_rescue, db->d_lres, db->d_loff, db->d_llen, db->d_lid, db->d_lbnd_h, db->d_lbnd_f,
@@ -1181,86 +1265,16 @@ int scan_impl_body(sw_handle* h, const sw_db* cdb, const uint8_t* query, int32_t
     // model's rows back.
     const int ri2_model = ri2;
     if (affine && ri2 > 8 && db->nblocks && O.intra_x2_rows < 0) ri2 = 8;
-    // The intra chain's order.  Linear scoring with cheap gaps makes random
-    // pairs' scores grow with their lengths, so on long subjects the fp16
-    // pass can flag many of them and its time on those is wasted.  Once a
-    // scan with the same scoring has flagged over a third of the long
-    // subjects at a query no longer than this one, the int16 form runs
-    // first, over all of them (the int16 cell costs ~1.4x the fp16 one, so
-    // fp16 first + int16 over the flagged fraction p wins while p < ~0.3).
-    // sw_opts intra_i16_first 0 / 1: never / always.
+    // The intra chain's order from the database's earlier scans
+    // (adapt_intra_i16_first), keyed by the scoring and the query:
     uint64_t skey = 1469598103934665603ull;  // FNV-1a of the scoring
     for (int k = 0; k < 625; ++k) skey = (skey ^ static_cast<uint8_t>(mat[k])) * 1099511628211ull;
     skey = ((skey ^ static_cast<uint32_t>(go)) * 1099511628211ull ^ static_cast<uint32_t>(ge)) * 1099511628211ull;
     uint64_t qhash = 1469598103934665603ull;  // FNV-1a of the query (which
     for (int32_t k = 0; k < qlen; ++k) qhash = (qhash ^ query[k]) * 1099511628211ull;  // readbacks repeat)
-    if (db->lcount_pending && hipEventQuery(db->lcount_ev) == hipSuccess) {
-        db->lcount_pending = false;
-        db->lcount_seen = true;
-        db->lseen_key = db->lcount_key;
-        db->lseen_qhash = db->lcount_qhash;
-        db->lseen_qlen = db->lcount_qlen;
-        if (3 * static_cast<int64_t>(*db->h_lcount) > db->nlong) {
-            bool seen = false;
-            for (auto& e : db->i16_first)
-                if (e.first == db->lcount_key) {
-                    e.second = std::min(e.second, db->lcount_qlen);
-                    seen = true;
-                }
-            if (!seen) db->i16_first.emplace_back(db->lcount_key, db->lcount_qlen);
-        }
-    }
-    bool intra_i16_first = false;
-    if (O.intra_i16_first == 0 || O.intra_i16_first == 1) {
-        intra_i16_first = O.intra_i16_first == 1;
-    } else {
-        for (const auto& e : db->i16_first)
-            if (e.first == skey && e.second <= qlen) intra_i16_first = true;
-    }
-    intra_i16_first = intra_i16_first && intra_x2;
-    // The same for the inter scan, per block: long queries under cheap linear
-    // gaps put the WIDEST blocks (length-sorted, ids 0, 1, ...) in the fp16
-    // guard band, and their re-scoring by the list kernel (one wave per block,
-    // every pass in turn) takes longer than the whole scan.  A scan with the
-    // same scoring whose fp16 pass flagged most of blocks [0, span) makes
-    // later queries at least as long run those blocks in int16, by wave pairs
-    // beside the fp16 launch.  sw_opts inter_i16_span n forces n blocks (0: off).
-    if (db->icount_pending && hipEventQuery(db->icount_ev) == hipSuccess) {
-        db->icount_pending = false;
-        db->icount_seen = true;
-        db->seen_key = db->icount_key;
-        db->seen_qhash = db->icount_qhash;
-        db->seen_qlen = db->icount_qlen;
-        db->seen_nr = db->icount_nr;
-        const int32_t cnt = db->h_icount[0], span = db->h_icount[1] + 1;
-        // most of [nr, span) flagged: not a few high-scoring hits far out
-        if (cnt > 0 && span > db->icount_nr && 2 * static_cast<int64_t>(cnt) >= span - db->icount_nr) {
-            // keep a staircase per scoring: drop what the new observation
-            // dominates (a query at least as long with a span no larger),
-            // skip it if an existing one dominates it
-            const uint64_t k = db->icount_key;
-            const int32_t q = db->icount_qlen;
-            bool dominated = false;
-            for (const auto& e : db->i16_span)
-                if (e.key == k && e.qlen <= q && e.span >= span) dominated = true;
-            if (!dominated) {
-                db->i16_span.erase(std::remove_if(db->i16_span.begin(), db->i16_span.end(),
-                                                  [&](const sw_db::SpanObs& e) {
-                                                      return e.key == k && e.qlen >= q && e.span <= span;
-                                                  }),
-                                   db->i16_span.end());
-                db->i16_span.push_back({k, q, span});
-            }
-        }
-    }
-    int32_t i16_span = 0;
-    if (O.inter_i16_span >= 0) {
-        i16_span = O.inter_i16_span;
-    } else {
-        for (const auto& o : db->i16_span)
-            if (o.key == skey && o.qlen <= qlen) i16_span = std::max(i16_span, o.span);
-    }
-    i16_span = static_cast<int32_t>(std::min<int64_t>(std::max(i16_span, 0), db->nblocks));
+    const bool intra_i16_first = adapt_intra_i16_first(db, skey, qlen, O.intra_i16_first) && intra_x2;
+    // ... and the inter scan's widest blocks in int16 first (adapt_inter_i16_span)
+    const int32_t i16_span = adapt_inter_i16_span(db, skey, qlen, O.inter_i16_span);
     int32_t qpad_intra2 = ri2 ? static_cast<int32_t>(round_up(qlen, static_cast<int64_t>(swk::kLanes) * ri2)) : 0;
     // Empty query: every score is 0 (the reference's kernel leaves maxScore 0).
     if (qlen == 0) {
