@@ -218,12 +218,13 @@ LptPlan lpt_plan(const PlanDb& db, int32_t qpad, int rows, int32_t qpad_intra, i
     const double tick_us = kTickUs * rows / 64;  // a tick: 8 columns of one pass
     const int64_t nb = db.nblocks;
     const int64_t pwg = nquad + (npair - nquad + 1) / 2;
-    const int64_t tail = nb - ntail;  // blocks [tail, nb) by pairs
+    // blocks [tail, nb) by pairs (x2p_wg's clamp: none unless tail lies in (npair, nb))
+    const int64_t tail = ntail > 0 && nb - ntail > npair && nb - ntail < nb ? nb - ntail : nb;
     // tris: the spare wave of tri workgroup g runs single block npair + g
     const int64_t nspare = tri ? std::max<int64_t>(0, std::min<int64_t>(nquad, tail - npair)) : 0;
     const int64_t s0 = npair + nspare;  // the single-wave workgroups' first block
     const int64_t swg = (tail - s0 + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
-    const int64_t twg = (ntail + 1) / 2;
+    const int64_t twg = (nb - tail + 1) / 2;
     const int64_t npairs = (db.nlong + 1) / 2;
     const int64_t iwg = (npairs + swk::kWavesPerWG - 1) / swk::kWavesPerWG;
     const int nch = qpad_intra / (swk::kLanes * ri);

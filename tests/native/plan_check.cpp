@@ -126,6 +126,8 @@ int main() {
     scenario("tris-exceed-singles", 200, 800, 100, 40, 2000, 190, 190, 0, true, true, 375, 64, 6, o);
     // tail pairs beside tris
     scenario("tris-and-tail-pairs", 2000, 1500, 16, 500, 4000, 600, 100, 256, true, true, 300, 64, 4, o);
+    // a tail-pair count reaching into the group blocks: the kernel runs none
+    scenario("tail-pairs-clamped", 300, 900, 48, 80, 3000, 250, 20, 100, true, true, 375, 64, 6, o);
     // forced pipes at both ends, odd long count
     sw_opts f = o;
     f.lpt_pipe = 3;
